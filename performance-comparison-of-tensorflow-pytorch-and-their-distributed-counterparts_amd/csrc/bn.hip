@@ -1,0 +1,463 @@
+// BatchNorm2d (NHWC, bf16 activations, fp32 statistics) for CDNA4.
+//
+// Replaces the BatchNorm2d(+ReLU)(+residual add) layers of torchvision ResNet-50
+// (pytorch_training_inference_on_image.ipynb:454-626; SURVEY.md §2.4.1 "BatchNorm2d ... fused
+// with ReLU, and with residual add+ReLU at the block tail").  Train mode uses batch statistics
+// and updates running stats with momentum (running_var unbiased), eval mode uses running stats.
+//
+// Forward is split into three memory passes at most:
+//   1. per-block column partial sums (fused into the producing conv's epilogue, or
+//      bn_partials_kernel when the producer is not ours),
+//   2. bn_finalize_kernel: fp64 reduction of the partials -> mean/invstd, per-channel scale/shift,
+//      running-stat update,
+//   3. bn_apply_kernel: y = act(x*scale+shift [+ x2*scale2+shift2 | + res]) with 16-B vectors.
+// Backward: bn_bwd_reduce_kernel (g = dy*(y>0) recomputed, partial sums of g and g*xhat for up
+// to two BN layers that share g -- the bottleneck tail and its downsample branch), then
+// bn_bwd_finalize_kernel (dgamma/dbeta into the flat gradient buffer, per-channel dx
+// coefficients), then bn_bwd_apply_kernel dx = k1*g + k2*x + k3 (optionally also writing g for
+// the identity path).
+#include "common.h"
+
+namespace pcmp {
+
+struct RowMap {
+  int CV;    // 8-channel vectors per row
+  int tpr;   // threads per row
+  int rpp;   // rows per pass
+  int vpt;   // vectors per thread per row
+};
+static RowMap make_rowmap(int C) {
+  RowMap r;
+  r.CV = C / 8;
+  r.tpr = r.CV < 256 ? r.CV : 256;
+  r.rpp = 256 / r.tpr;
+  r.vpt = r.CV / r.tpr;
+  return r;
+}
+
+__device__ __forceinline__ void load8(const __bf16* p, float* v) {
+  const u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = bf2f(u[e]);
+}
+__device__ __forceinline__ void store8(__bf16* p, const float* v) {
+  u16x8 u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+  *reinterpret_cast<u16x8*>(p) = u;
+}
+
+// ---- forward partial statistics of x (used when the producer did not emit them) ----------
+__global__ void bn_partials_kernel(const __bf16* __restrict__ x, float* __restrict__ part, int M, int C,
+                                   int rows_per_block, RowMap rm) {
+  extern __shared__ float sh[];  // [rpp][2][C]
+  const int tid = threadIdx.x;
+  const int tr = tid / rm.tpr, tc = tid % rm.tpr;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  for (int k = 0; k < rm.vpt; ++k) {
+    const int cv = tc + k * rm.tpr;
+    float s1[8] = {0}, s2[8] = {0};
+    for (int r = r0 + tr; r < r1; r += rm.rpp) {
+      float v[8];
+      load8(x + (size_t)r * C + cv * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sh[(tr * 2 + 0) * C + cv * 8 + e] = s1[e];
+      sh[(tr * 2 + 1) * C + cv * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * C; i += blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < rm.rpp; ++r) s += sh[r * 2 * C + i];
+    part[(size_t)blockIdx.x * 2 * C + i] = s;
+  }
+}
+
+// ---- finalize: partials [T][2][C] -> mean, invstd, scale, shift; running stats update --------
+// block = 256 threads handles 64 channels (4 row-groups of partials).
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int T, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
+                                   float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                   float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  __shared__ double sh[2][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  double s1 = 0, s2 = 0;
+  if (c < C) {
+    for (int t = g; t < T; t += 4) {
+      s1 += part[(size_t)t * 2 * C + c];
+      s2 += part[(size_t)t * 2 * C + C + c];
+    }
+  }
+  sh[0][g][threadIdx.x & 63] = s1;
+  sh[1][g][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    for (int k = 1; k < 4; ++k) { s1 += sh[0][k][threadIdx.x]; s2 += sh[1][k][threadIdx.x]; }
+    const double mean = s1 / count;
+    double var = s2 / count - mean * mean;
+    if (var < 0) var = 0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    mean_out[c] = (float)mean;
+    invstd_out[c] = invstd;
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    scale_out[c] = gm * invstd;
+    shift_out[c] = bt - (float)mean * gm * invstd;
+    if (rmean) {
+      const double unbiased = count > 1 ? var * count / (count - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+    }
+  }
+}
+
+// eval-mode coefficients from running statistics
+__global__ void bn_eval_coeff_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                     const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                     float eps, float* __restrict__ scale_out, float* __restrict__ shift_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(rvar[c] + eps);
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale_out[c] = gm * invstd;
+  shift_out[c] = bt - rmean[c] * gm * invstd;
+}
+
+// ---- apply: y = act(x*sc+sh [+ x2*sc2+sh2 | + res]) ------------------------------------------
+__global__ void bn_apply_kernel(const __bf16* __restrict__ x, const float* __restrict__ sc,
+                                const float* __restrict__ shf, const __bf16* __restrict__ x2,
+                                const float* __restrict__ sc2, const float* __restrict__ shf2,
+                                __bf16* __restrict__ y, int64_t nvec, int CV, int relu) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    float v[8];
+    load8(x + i * 8, v);
+    const f32x4 a0 = reinterpret_cast<const f32x4*>(sc)[cv * 2], a1 = reinterpret_cast<const f32x4*>(sc)[cv * 2 + 1];
+    const f32x4 b0 = reinterpret_cast<const f32x4*>(shf)[cv * 2], b1 = reinterpret_cast<const f32x4*>(shf)[cv * 2 + 1];
+    const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const float b[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * a[e] + b[e];
+    if (x2) {
+      float w[8];
+      load8(x2 + i * 8, w);
+      if (sc2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += w[e] * sc2[cv * 8 + e] + shf2[cv * 8 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += w[e];
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    store8(y + i * 8, v);
+  }
+}
+
+// ---- backward reduce: partial sums of g and g*xhat (g = dy * (y>0) when y given) -------------
+// Up to two BN layers (x/mean/invstd and x2/mean2/invstd2) that share the same g.
+__global__ void bn_bwd_reduce_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ ymask,
+                                     const __bf16* __restrict__ x, const float* __restrict__ mean,
+                                     const float* __restrict__ invstd, const __bf16* __restrict__ x2,
+                                     const float* __restrict__ mean2, const float* __restrict__ invstd2,
+                                     float* __restrict__ part, float* __restrict__ part2, int M, int C,
+                                     int rows_per_block, RowMap rm) {
+  extern __shared__ float sh[];  // [rpp][4][C]
+  const int tid = threadIdx.x;
+  const int tr = tid / rm.tpr, tc = tid % rm.tpr;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  const int NS = x2 ? 4 : 2;
+  for (int k = 0; k < rm.vpt; ++k) {
+    const int cv = tc + k * rm.tpr;
+    float sg[8] = {0}, sgx[8] = {0}, sgx2[8] = {0};
+    float mu[8], is[8], mu2[8], is2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = mean[cv * 8 + e]; is[e] = invstd[cv * 8 + e];
+      mu2[e] = x2 ? mean2[cv * 8 + e] : 0.f; is2[e] = x2 ? invstd2[cv * 8 + e] : 0.f;
+    }
+    for (int r = r0 + tr; r < r1; r += rm.rpp) {
+      const size_t o = (size_t)r * C + cv * 8;
+      float g[8], xv[8];
+      load8(dy + o, g);
+      if (ymask) {
+        const u16x8 ym = *reinterpret_cast<const u16x8*>(ymask + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = (bf2f(ym[e]) > 0.f) ? g[e] : 0.f;
+      }
+      load8(x + o, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sg[e] += g[e]; sgx[e] += g[e] * (xv[e] - mu[e]) * is[e]; }
+      if (x2) {
+        load8(x2 + o, xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sgx2[e] += g[e] * (xv[e] - mu2[e]) * is2[e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sh[(tr * NS + 0) * C + cv * 8 + e] = sg[e];
+      sh[(tr * NS + 1) * C + cv * 8 + e] = sgx[e];
+      if (x2) sh[(tr * NS + 3) * C + cv * 8 + e] = sgx2[e];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * C; i += blockDim.x) {
+    const int which = i / C, c = i % C;
+    float s = 0.f;
+    for (int r = 0; r < rm.rpp; ++r) s += sh[(r * NS + which) * C + c];
+    part[(size_t)blockIdx.x * 2 * C + i] = s;
+    if (x2) {
+      float s2 = 0.f;
+      const int w2 = which == 0 ? 0 : 3;
+      for (int r = 0; r < rm.rpp; ++r) s2 += sh[(r * NS + w2) * C + c];
+      part2[(size_t)blockIdx.x * 2 * C + i] = s2;
+    }
+  }
+}
+
+// partials [T][2][C] -> dgamma/dbeta (written/accumulated into dgamma_out/dbeta_out, optional) and
+// per-channel dx coefficients coef[3][C]: dx = k1*g + k2*x + k3
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ dgamma_out,
+                                       float* __restrict__ dbeta_out, int accumulate, float* __restrict__ coef) {
+  __shared__ double sh[2][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  double sg = 0, sgx = 0;
+  if (c < C) {
+    for (int t = g; t < T; t += 4) {
+      sg += part[(size_t)t * 2 * C + c];
+      sgx += part[(size_t)t * 2 * C + C + c];
+    }
+  }
+  sh[0][g][threadIdx.x & 63] = sg;
+  sh[1][g][threadIdx.x & 63] = sgx;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    for (int k = 1; k < 4; ++k) { sg += sh[0][k][threadIdx.x]; sgx += sh[1][k][threadIdx.x]; }
+    const float dbeta = (float)sg, dgamma = (float)sgx;
+    if (dgamma_out) dgamma_out[c] = accumulate ? dgamma_out[c] + dgamma : dgamma;
+    if (dbeta_out) dbeta_out[c] = accumulate ? dbeta_out[c] + dbeta : dbeta;
+    const float gm = gamma ? gamma[c] : 1.f;
+    const float is = invstd[c], mu = mean[c];
+    const float k1 = gm * is;
+    const float k2 = -(float)(gm * (double)is * is * sgx / count);
+    const float k3 = -(float)(gm * (double)is * sg / count) - k2 * mu;
+    coef[c] = k1;
+    coef[C + c] = k2;
+    coef[2 * C + c] = k3;
+  }
+}
+
+// dx = k1*g + k2*x + k3 (g = dy*(y>0) if ymask); optional second BN (x2, coef2 -> dx2) sharing g;
+// optional g_out (bf16) for the identity path of a residual block.
+__global__ void bn_bwd_apply_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ ymask,
+                                    const __bf16* __restrict__ x, const float* __restrict__ coef,
+                                    __bf16* __restrict__ dx, const __bf16* __restrict__ x2,
+                                    const float* __restrict__ coef2, __bf16* __restrict__ dx2,
+                                    __bf16* __restrict__ g_out, int64_t nvec, int CV) {
+  const int C = CV * 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    float g[8], xv[8], o[8];
+    load8(dy + i * 8, g);
+    if (ymask) {
+      const u16x8 ym = *reinterpret_cast<const u16x8*>(ymask + i * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = (bf2f(ym[e]) > 0.f) ? g[e] : 0.f;
+    }
+    if (g_out) store8(g_out + i * 8, g);
+    load8(x + i * 8, xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = cv * 8 + e;
+      o[e] = coef[c] * g[e] + coef[C + c] * xv[e] + coef[2 * C + c];
+    }
+    store8(dx + i * 8, o);
+    if (x2) {
+      load8(x2 + i * 8, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cv * 8 + e;
+        o[e] = coef2[c] * g[e] + coef2[C + c] * xv[e] + coef2[2 * C + c];
+      }
+      store8(dx2 + i * 8, o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+static int rows_per_block_for(int M, const RowMap& rm, int target_blocks = 2048) {
+  int rpb = std::max(rm.rpp, ceil_div(M, target_blocks));
+  rpb = ceil_div(rpb, rm.rpp) * rm.rpp;
+  return rpb;
+}
+
+static void check_act(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous(), name,
+              ": contiguous bf16 GPU tensor expected");
+  TORCH_CHECK(t.size(-1) % 8 == 0, name, ": channels must be a multiple of 8");
+}
+
+// x: [..., C] bf16 -> partial stats [T][2][C]
+at::Tensor bn_partials(const at::Tensor& x) {
+  check_act(x, "bn_partials");
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  const RowMap rm = make_rowmap(C);
+  const int rpb = rows_per_block_for(M, rm);
+  const int T = ceil_div(M, rpb);
+  auto part = at::empty({T, 2, C}, x.options().dtype(at::kFloat));
+  const size_t shm = (size_t)rm.rpp * 2 * C * sizeof(float);
+  hipLaunchKernelGGL(bn_partials_kernel, dim3(T), dim3(256), shm, cur_stream(), ptr<__bf16>(x),
+                     ptr<float>(part), M, C, rpb, rm);
+  PCMP_LAUNCH_CHECK();
+  return part;
+}
+
+// partials -> (mean, invstd, scale, shift) ; updates running stats in place when given.
+std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const c10::optional<at::Tensor>& gamma,
+                                    const c10::optional<at::Tensor>& beta,
+                                    const c10::optional<at::Tensor>& running_mean,
+                                    const c10::optional<at::Tensor>& running_var, double momentum, double eps) {
+  PCMP_CHECK_F32(part);
+  const int T = part.size(0), C = part.size(2);
+  auto opts = part.options();
+  auto out = at::empty({4, C}, opts);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<float>(part), T,
+                     C, (double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
+                     optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
+                     ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C);
+  PCMP_LAUNCH_CHECK();
+  return {out[0], out[1], out[2], out[3]};
+}
+
+std::vector<at::Tensor> bn_eval_coeff(const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta,
+                                      const at::Tensor& running_mean, const at::Tensor& running_var, double eps) {
+  const int C = running_mean.numel();
+  auto out = at::empty({2, C}, running_mean.options());
+  hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, cur_stream(), C,
+                     optr<float>(gamma), optr<float>(beta), ptr<float>(running_mean), ptr<float>(running_var),
+                     (float)eps, ptr<float>(out), ptr<float>(out) + C);
+  PCMP_LAUNCH_CHECK();
+  return {out[0], out[1]};
+}
+
+static int ew_blocks(int64_t nvec) { return (int)std::min<int64_t>(4096, (nvec + 255) / 256); }
+
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
+                    const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
+                    const c10::optional<at::Tensor>& shift2, bool relu) {
+  check_act(x, "bn_apply");
+  const int C = x.size(-1);
+  auto y = at::empty_like(x);
+  const int64_t nvec = x.numel() / 8;
+  const __bf16* x2p = nullptr;
+  if (x2.has_value() && x2->defined()) {
+    check_act(*x2, "bn_apply x2");
+    TORCH_CHECK(x2->numel() == x.numel(), "bn_apply: x2 shape");
+    x2p = ptr<__bf16>(*x2);
+  }
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                     ptr<float>(scale), ptr<float>(shift), x2p, optr<float>(scale2), optr<float>(shift2),
+                     ptr<__bf16>(y), nvec, C / 8, (int)relu);
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+// returns partials for BN1 (and BN2 when x2 given)
+std::vector<at::Tensor> bn_bwd_reduce(const at::Tensor& dy, const c10::optional<at::Tensor>& ymask,
+                                      const at::Tensor& x, const at::Tensor& mean, const at::Tensor& invstd,
+                                      const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                                      const c10::optional<at::Tensor>& invstd2) {
+  check_act(dy, "bn_bwd dy");
+  check_act(x, "bn_bwd x");
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  const RowMap rm = make_rowmap(C);
+  const int rpb = rows_per_block_for(M, rm);
+  const int T = ceil_div(M, rpb);
+  auto part = at::empty({T, 2, C}, x.options().dtype(at::kFloat));
+  const bool two = x2.has_value() && x2->defined();
+  at::Tensor part2 = two ? at::empty({T, 2, C}, part.options()) : at::Tensor();
+  const size_t shm = (size_t)rm.rpp * (two ? 4 : 2) * C * sizeof(float);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(T), dim3(256), shm, cur_stream(), ptr<__bf16>(dy),
+                     optr<__bf16>(ymask), ptr<__bf16>(x), ptr<float>(mean), ptr<float>(invstd),
+                     two ? ptr<__bf16>(*x2) : nullptr, optr<float>(mean2), optr<float>(invstd2), ptr<float>(part),
+                     two ? ptr<float>(part2) : nullptr, M, C, rpb, rm);
+  PCMP_LAUNCH_CHECK();
+  if (two) return {part, part2};
+  return {part};
+}
+
+// returns coef [3][C]; writes dgamma/dbeta into the given fp32 buffers (flat grad views)
+at::Tensor bn_bwd_finalize(const at::Tensor& part, int64_t count, const c10::optional<at::Tensor>& gamma,
+                           const at::Tensor& mean, const at::Tensor& invstd,
+                           const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
+                           bool accumulate) {
+  const int T = part.size(0), C = part.size(2);
+  auto coef = at::empty({3, C}, part.options());
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<float>(part),
+                     T, C, (double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
+                     optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef));
+  PCMP_LAUNCH_CHECK();
+  return coef;
+}
+
+// returns [dx] (+ dx2) (+ g)
+std::vector<at::Tensor> bn_bwd_apply(const at::Tensor& dy, const c10::optional<at::Tensor>& ymask,
+                                     const at::Tensor& x, const at::Tensor& coef,
+                                     const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& coef2,
+                                     bool want_g) {
+  check_act(dy, "bn_bwd_apply dy");
+  const int C = x.size(-1);
+  auto dx = at::empty_like(x);
+  const bool two = x2.has_value() && x2->defined();
+  at::Tensor dx2 = two ? at::empty_like(*x2) : at::Tensor();
+  at::Tensor g = want_g ? at::empty_like(dy) : at::Tensor();
+  const int64_t nvec = x.numel() / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, cur_stream(), ptr<__bf16>(dy),
+                     optr<__bf16>(ymask), ptr<__bf16>(x), ptr<float>(coef), ptr<__bf16>(dx),
+                     two ? ptr<__bf16>(*x2) : nullptr, optr<float>(coef2), two ? ptr<__bf16>(dx2) : nullptr,
+                     want_g ? ptr<__bf16>(g) : nullptr, nvec, C / 8);
+  PCMP_LAUNCH_CHECK();
+  std::vector<at::Tensor> r{dx};
+  if (two) r.push_back(dx2);
+  if (want_g) r.push_back(g);
+  return r;
+}
+
+}  // namespace pcmp
+
+TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("bn_partials(Tensor x) -> Tensor", &pcmp::bn_partials);
+  m.def("bn_finalize(Tensor part, int count, Tensor? gamma, Tensor? beta, Tensor(a!)? running_mean, "
+        "Tensor(b!)? running_var, float momentum, float eps) -> Tensor[]",
+        &pcmp::bn_finalize);
+  m.def("bn_eval_coeff(Tensor? gamma, Tensor? beta, Tensor running_mean, Tensor running_var, float eps) -> Tensor[]",
+        &pcmp::bn_eval_coeff);
+  m.def("bn_apply(Tensor x, Tensor scale, Tensor shift, Tensor? x2, Tensor? scale2, Tensor? shift2, bool relu) -> Tensor",
+        &pcmp::bn_apply);
+  m.def("bn_bwd_reduce(Tensor dy, Tensor? ymask, Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, "
+        "Tensor? invstd2) -> Tensor[]",
+        &pcmp::bn_bwd_reduce);
+  m.def("bn_bwd_finalize(Tensor part, int count, Tensor? gamma, Tensor mean, Tensor invstd, Tensor(a!)? dgamma, "
+        "Tensor(b!)? dbeta, bool accumulate) -> Tensor",
+        &pcmp::bn_bwd_finalize);
+  m.def("bn_bwd_apply(Tensor dy, Tensor? ymask, Tensor x, Tensor coef, Tensor? x2, Tensor? coef2, bool want_g) -> Tensor[]",
+        &pcmp::bn_bwd_apply);
+}

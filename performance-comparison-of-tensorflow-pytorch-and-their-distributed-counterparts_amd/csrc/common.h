@@ -1,0 +1,92 @@
+// Shared device/host helpers for every CDNA4 (gfx950) kernel in this framework.
+//
+// Conventions used across csrc/:
+//   * activations are NHWC (channels-last) bf16, weights KRSC ([Cout][kh][kw][Cin]) bf16 for
+//     compute with an fp32 master copy owned by the optimizer;
+//   * per-channel statistics / gradients are fp32;
+//   * every launch goes on the current PyTorch HIP stream so ops compose with torch's own
+//     kernels, RCCL and hipGraph capture (no host syncs, no allocation inside launches other
+//     than through the torch caching allocator).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <cstdint>
+
+namespace pcmp {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(unsigned short u) {
+  return __uint_as_float(((unsigned)u) << 16);
+}
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN: quiet bit forced)
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `sh` needs >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = warp_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+
+// Counter-based hash RNG (stateless): used for dropout so backward regenerates the mask
+// from (seed, offset, index) instead of storing it.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed ^ (idx * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)z;
+}
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
+  return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
+}
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+#define PCMP_CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define PCMP_CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define PCMP_CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
+#define PCMP_CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be fp32")
+#define PCMP_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
+
+template <typename T>
+inline T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+inline T* optr(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+}  // namespace pcmp

@@ -1,0 +1,447 @@
+// Pooling, loss, dropout, activation-backward, bias-gradient and input-conversion kernels (NHWC,
+// bf16, 16-B vectors over channels).
+//
+// Reference parity:
+//   * MaxPool2d(3,2,1) of the ResNet stem and the 5 MaxPool2d(2,2) of VGG16
+//     (pytorch_training_inference_on_image.ipynb:458,1991-2041)
+//   * AdaptiveAvgPool2d(1) (ResNet) — global average pool
+//   * LogSoftmax(dim=1) + NLLLoss of the transfer heads (another_neural_net.py:108-113,250-257)
+//     and CrossEntropy of BertForSequenceClassification — one fused row kernel
+//   * Dropout(0.2/0.4/0.5/0.1) — counter-based hash RNG, mask regenerated in backward
+//   * ToTensor/normalise of the image pipeline — fused NCHW f32/u8 -> NHWC bf16
+//     with zero channel padding to a multiple of 8 (the stem conv's MFMA K granularity)
+#include "common.h"
+
+namespace pcmp {
+
+__device__ __forceinline__ void ld8(const __bf16* p, float* v) {
+  const u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = bf2f(u[e]);
+}
+__device__ __forceinline__ void st8(__bf16* p, const float* v) {
+  u16x8 u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+  *reinterpret_cast<u16x8*>(p) = u;
+}
+static int grid_for(int64_t n, int block = 256, int cap = 4096) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + block - 1) / block));
+}
+
+// ---------------------------------------------------------------- max pool (NHWC) -------------
+// y[n,p,q,c] = max over window; idx[n,p,q,c] = argmax position inside the window (uint8)
+__global__ void maxpool_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+                                   uint8_t* __restrict__ idx, int N, int H, int W, int C, int P, int Q,
+                                   int k, int s, int pad) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * P * Q * CV;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = i % CV;
+    int64_t t = i / CV;
+    const int q = t % Q; t /= Q;
+    const int p = t % P;
+    const int n = t / P;
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < k; ++r) {
+      const int h = p * s - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int c = 0; c < k; ++c) {
+        const int w = q * s - pad + c;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float v[8];
+        ld8(x + (((size_t)n * H + h) * W + w) * C + cv * 8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e] || (v[e] != v[e])) { best[e] = v[e]; bi[e] = r * k + c; }
+      }
+    }
+    st8(y + i * 8, best);
+    if (idx) {
+      uint64_t packed = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) packed |= (uint64_t)(bi[e] & 0xff) << (8 * e);
+      *reinterpret_cast<uint64_t*>(idx + i * 8) = packed;
+    }
+  }
+}
+
+// gather-form backward: dx[n,h,w,c] = sum of dy over the windows whose argmax is (h,w)
+__global__ void maxpool_bwd_kernel(const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                   __bf16* __restrict__ dx, int N, int H, int W, int C, int P, int Q,
+                                   int k, int s, int pad) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * H * W * CV;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = i % CV;
+    int64_t t = i / CV;
+    const int w = t % W; t /= W;
+    const int h = t % H;
+    const int n = t / H;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // candidate output rows p with p*s - pad <= h <= p*s - pad + k - 1
+    const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
+    const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * s - pad);
+      if (r < 0 || r >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int c = w - (q * s - pad);
+        if (c < 0 || c >= k) continue;
+        const size_t o = (((size_t)n * P + p) * Q + q) * C + cv * 8;
+        const uint64_t packed = *reinterpret_cast<const uint64_t*>(idx + o);
+        float g[8];
+        ld8(dy + o, g);
+        const int pos = r * k + c;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((packed >> (8 * e)) & 0xff) == pos) acc[e] += g[e];
+      }
+    }
+    st8(dx + i * 8, acc);
+  }
+}
+
+// ---------------------------------------------------------------- global average pool ----------
+// x [N, HW, C] -> y [N, C]  (one block per (n, 64*8-channel slab))
+__global__ void gap_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y, int HW, int C) {
+  const int n = blockIdx.y;
+  const int CV = C / 8;
+  const int cv = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;  // 4 row groups
+  __shared__ float sh[4][64][8];
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (cv < CV) {
+    for (int r = g; r < HW; r += 4) {
+      float v[8];
+      ld8(x + ((size_t)n * HW + r) * C + cv * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sh[g][threadIdx.x & 63][e] = acc[e];
+  __syncthreads();
+  if (g == 0 && cv < CV) {
+    const float inv = 1.f / HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = (acc[e] + sh[1][threadIdx.x][e] + sh[2][threadIdx.x][e] + sh[3][threadIdx.x][e]) * inv;
+    st8(y + (size_t)n * C + cv * 8, acc);
+  }
+}
+
+__global__ void gap_bwd_kernel(const __bf16* __restrict__ dy, __bf16* __restrict__ dx, int N, int HW, int C) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * HW * CV;
+  const float inv = 1.f / HW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = i % CV;
+    const int n = (int)(i / ((int64_t)HW * CV));
+    float v[8];
+    ld8(dy + (size_t)n * C + cv * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= inv;
+    st8(dx + i * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------- softmax cross-entropy --------
+// one wave per row: logits [B][V] (bf16 or f32) -> logp (f32, optional), dlogits (bf16/f32,
+// optional, = (softmax - onehot) * grad_scale), per-row loss (f32) -> loss_rows[B]
+template <typename T>
+__device__ __forceinline__ float ldv(const T* p, int i);
+template <>
+__device__ __forceinline__ float ldv<float>(const float* p, int i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldv<__bf16>(const __bf16* p, int i) {
+  return bf2f(reinterpret_cast<const unsigned short*>(p)[i]);
+}
+
+template <typename T>
+__global__ void xent_kernel(const T* __restrict__ logits, const int64_t* __restrict__ labels, int B, int V,
+                            float* __restrict__ logp, T* __restrict__ dlogits, float* __restrict__ loss_rows,
+                            float grad_scale, int ignore_index) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const T* z = logits + (size_t)row * V;
+  float mx = -INFINITY;
+  for (int i = lane; i < V; i += 64) mx = fmaxf(mx, ldv<T>(z, i));
+  mx = warp_max(mx);
+  float se = 0.f;
+  for (int i = lane; i < V; i += 64) se += __expf(ldv<T>(z, i) - mx);
+  se = warp_sum(se);
+  const float lse = mx + __logf(se);
+  const int64_t y = labels ? labels[row] : -1;
+  const bool valid = labels && y != ignore_index && y >= 0 && y < V;
+  if (logp)
+    for (int i = lane; i < V; i += 64) logp[(size_t)row * V + i] = ldv<T>(z, i) - lse;
+  if (dlogits) {
+    for (int i = lane; i < V; i += 64) {
+      float g = valid ? (__expf(ldv<T>(z, i) - lse) - (i == y ? 1.f : 0.f)) * grad_scale : 0.f;
+      if constexpr (std::is_same<T, float>::value) dlogits[(size_t)row * V + i] = g;
+      else reinterpret_cast<unsigned short*>(dlogits)[(size_t)row * V + i] = f2bf(g);
+    }
+  }
+  if (lane == 0 && loss_rows) loss_rows[row] = valid ? (lse - ldv<T>(z, (int)y)) : 0.f;
+}
+
+// ---------------------------------------------------------------- dropout ----------------------
+// y = x * keep / (1-p), keep = uniform(seed, offset+i) >= p ; same call in backward on dy.
+__global__ void dropout_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y, int64_t n, float p,
+                               uint64_t seed, uint64_t offset) {
+  const float scale = 1.f / (1.f - p);
+  const int64_t nv = n / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    ld8(x + i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = uniform01(seed, offset + i * 8 + e) >= p ? v[e] * scale : 0.f;
+    st8(y + i * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------- relu backward ----------------
+__global__ void relu_bwd_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ y,
+                                __bf16* __restrict__ dx, int64_t nv) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const u16x8 g = reinterpret_cast<const u16x8*>(dy)[i];
+    const u16x8 v = reinterpret_cast<const u16x8*>(y)[i];
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bf2f(v[e]) > 0.f ? g[e] : (unsigned short)0;
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+  }
+}
+
+// ---------------------------------------------------------------- column sums (bias grad) -------
+// x [M][C] bf16 -> out[C] f32 (+= if accumulate). grid.x over 64-vector column slabs,
+// grid.y over row chunks -> partial f32 atomics (few rows chunks; deterministic when grid.y==1)
+__global__ void colsum_kernel(const __bf16* __restrict__ x, float* __restrict__ out, int M, int C,
+                              int rows_per_block) {
+  const int CV = C / 8;
+  const int cv = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  __shared__ float sh[4][64][8];
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (cv < CV) {
+    for (int r = r0 + g; r < r1; r += 4) {
+      float v[8];
+      ld8(x + (size_t)r * C + cv * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sh[g][threadIdx.x & 63][e] = acc[e];
+  __syncthreads();
+  if (g == 0 && cv < CV) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = acc[e] + sh[1][threadIdx.x][e] + sh[2][threadIdx.x][e] + sh[3][threadIdx.x][e];
+      if (gridDim.y == 1) out[cv * 8 + e] = v;
+      else atomicAdd(out + cv * 8 + e, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- input conversion -------------
+// x: [N, Cin, H, W] (f32 or u8) -> y: [N, H, W, Cpad] bf16, y = (x*scale - mean[c]) / std[c]
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const T* __restrict__ x, __bf16* __restrict__ y, int N, int Cin, int HW,
+                                    int Cpad, float scale, const float* __restrict__ mean,
+                                    const float* __restrict__ stdv) {
+  const int64_t total = (int64_t)N * HW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = i / HW, hw = i % HW;
+    for (int c0 = 0; c0 < Cpad; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        if (c < Cin) {
+          float a = (float)x[((size_t)n * Cin + c) * HW + hw] * scale;
+          if (mean) a = (a - mean[c]) / stdv[c];
+          v[e] = a;
+        } else {
+          v[e] = 0.f;
+        }
+      }
+      st8(y + (size_t)i * Cpad + c0, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- host ---------------------------
+std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k * k <= 255, "maxpool: C%8 / k");
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  auto y = at::empty({N, P, Q, C}, x.options());
+  at::Tensor idx = want_idx ? at::empty({N, P, Q, C}, x.options().dtype(at::kByte)) : at::Tensor();
+  const int64_t total = (int64_t)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                     ptr<__bf16>(y), want_idx ? ptr<uint8_t>(idx) : nullptr, N, H, W, C, P, Q, (int)k, (int)s,
+                     (int)pad);
+  PCMP_LAUNCH_CHECK();
+  if (want_idx) return {y, idx};
+  return {y};
+}
+
+at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s,
+                       int64_t pad) {
+  PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, cur_stream(), ptr<__bf16>(dy),
+                     ptr<uint8_t>(idx), ptr<__bf16>(dx), N, (int)H, (int)W, C, P, Q, (int)k, (int)s, (int)pad);
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+at::Tensor gap_fwd(const at::Tensor& x) {
+  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
+  const int N = x.size(0), C = x.size(-1);
+  const int HW = x.numel() / ((int64_t)N * C);
+  TORCH_CHECK(C % 8 == 0, "gap: C%8");
+  auto y = at::empty({N, C}, x.options());
+  dim3 grid(ceil_div(C / 8, 64), N);
+  hipLaunchKernelGGL(gap_fwd_kernel, grid, dim3(256), 0, cur_stream(), ptr<__bf16>(x), ptr<__bf16>(y), HW, C);
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
+  PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy);
+  const int N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, cur_stream(), ptr<__bf16>(dy),
+                     ptr<__bf16>(dx), N, (int)(H * W), C);
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+// returns [loss_rows(f32 [B]), logp(f32) if want_logp, dlogits if want_grad]
+std::vector<at::Tensor> softmax_xent(const at::Tensor& logits, const c10::optional<at::Tensor>& labels,
+                                     bool want_logp, bool want_grad, double grad_scale, int64_t ignore_index) {
+  PCMP_CHECK_CUDA(logits); PCMP_CHECK_CONTIG(logits);
+  TORCH_CHECK(logits.dim() == 2, "softmax_xent: [B,V] logits");
+  const int B = logits.size(0), V = logits.size(1);
+  auto f32 = logits.options().dtype(at::kFloat);
+  auto loss_rows = at::empty({B}, f32);
+  at::Tensor logp = want_logp ? at::empty({B, V}, f32) : at::Tensor();
+  at::Tensor dl = want_grad ? at::empty_like(logits) : at::Tensor();
+  const int64_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    TORCH_CHECK(labels->scalar_type() == at::kLong, "labels must be int64");
+    lab = labels->data_ptr<int64_t>();
+  }
+  dim3 grid(ceil_div(B, 4)), block(256);
+  if (logits.scalar_type() == at::kFloat) {
+    hipLaunchKernelGGL(xent_kernel<float>, grid, block, 0, cur_stream(), ptr<float>(logits), lab, B, V,
+                       want_logp ? ptr<float>(logp) : nullptr, want_grad ? ptr<float>(dl) : nullptr,
+                       ptr<float>(loss_rows), (float)grad_scale, (int)ignore_index);
+  } else {
+    PCMP_CHECK_BF16(logits);
+    hipLaunchKernelGGL(xent_kernel<__bf16>, grid, block, 0, cur_stream(), ptr<__bf16>(logits), lab, B, V,
+                       want_logp ? ptr<float>(logp) : nullptr, want_grad ? ptr<__bf16>(dl) : nullptr,
+                       ptr<float>(loss_rows), (float)grad_scale, (int)ignore_index);
+  }
+  PCMP_LAUNCH_CHECK();
+  std::vector<at::Tensor> r{loss_rows};
+  if (want_logp) r.push_back(logp);
+  if (want_grad) r.push_back(dl);
+  return r;
+}
+
+at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
+  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
+  TORCH_CHECK(x.numel() % 8 == 0, "dropout: numel % 8");
+  auto y = at::empty_like(x);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(x.numel() / 8)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                     ptr<__bf16>(y), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset);
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y) {
+  PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(y);
+  TORCH_CHECK(dy.numel() % 8 == 0, "relu_bwd: numel % 8");
+  auto dx = at::empty_like(dy);
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(dy.numel() / 8)), dim3(256), 0, cur_stream(),
+                     ptr<__bf16>(dy), ptr<__bf16>(y), ptr<__bf16>(dx), dy.numel() / 8);
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+void colsum(const at::Tensor& x, at::Tensor out, bool accumulate) {
+  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out);
+  const int C = x.size(-1);
+  const int M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && out.numel() == C, "colsum: shapes");
+  int chunks = std::max(1, std::min(64, M / 2048));
+  if (accumulate && chunks == 1) {
+    // keep deterministic single pass; accumulate via temp
+    auto tmp = at::empty_like(out);
+    hipLaunchKernelGGL(colsum_kernel, dim3(ceil_div(C / 8, 64), 1), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                       ptr<float>(tmp), M, C, M);
+    PCMP_LAUNCH_CHECK();
+    out.add_(tmp);
+    return;
+  }
+  if (chunks > 1 && !accumulate) out.zero_();
+  const int rpb = ceil_div(M, chunks);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ceil_div(C / 8, 64), chunks), dim3(256), 0, cur_stream(),
+                     ptr<__bf16>(x), ptr<float>(out), M, C, rpb);
+  PCMP_LAUNCH_CHECK();
+}
+
+at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad, double scale, const c10::optional<at::Tensor>& mean,
+                        const c10::optional<at::Tensor>& stdv) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_CONTIG(x);
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(cpad % 8 == 0 && cpad >= Cin, "nchw_to_nhwc: cpad");
+  auto y = at::empty({N, H, W, cpad}, x.options().dtype(at::kBFloat16));
+  const int64_t total = (int64_t)N * H * W;
+  if (x.scalar_type() == at::kFloat) {
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+                       ptr<float>(x), ptr<__bf16>(y), N, Cin, H * W, (int)cpad, (float)scale, optr<float>(mean),
+                       optr<float>(stdv));
+  } else {
+    TORCH_CHECK(x.scalar_type() == at::kByte, "nchw_to_nhwc: f32 or u8 input");
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<uint8_t>, dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+                       ptr<uint8_t>(x), ptr<__bf16>(y), N, Cin, H * W, (int)cpad, (float)scale, optr<float>(mean),
+                       optr<float>(stdv));
+  }
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+}  // namespace pcmp
+
+TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("maxpool_fwd(Tensor x, int k, int s, int pad, bool want_idx) -> Tensor[]", &pcmp::maxpool_fwd);
+  m.def("maxpool_bwd(Tensor dy, Tensor idx, int H, int W, int k, int s, int pad) -> Tensor", &pcmp::maxpool_bwd);
+  m.def("gap_fwd(Tensor x) -> Tensor", &pcmp::gap_fwd);
+  m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &pcmp::gap_bwd);
+  m.def("softmax_xent(Tensor logits, Tensor? labels, bool want_logp, bool want_grad, float grad_scale, "
+        "int ignore_index) -> Tensor[]",
+        &pcmp::softmax_xent);
+  m.def("dropout(Tensor x, float p, int seed, int offset) -> Tensor", &pcmp::dropout);
+  m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &pcmp::relu_bwd);
+  m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()", &pcmp::colsum);
+  m.def("nchw_to_nhwc(Tensor x, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor", &pcmp::nchw_to_nhwc);
+}

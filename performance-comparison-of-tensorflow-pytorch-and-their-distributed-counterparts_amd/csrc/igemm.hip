@@ -1,0 +1,651 @@
+// Implicit-GEMM convolution / linear kernels on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16).
+//
+// One kernel template covers the three GEMMs of a convolution (and of a Linear layer, which is
+// a 1x1 conv over [M,1,1,Cin]):
+//   FWD   : Y[m=(n,p,q)][co]      = sum_{k=(r,s,ci)}  X[n,p*st-pad+r,q*st-pad+s,ci] * W[co][r][s][ci]
+//   DGRAD : dX[m=(n,h,w)][ci]     = sum_{k=(r,s,co)} dY[n,(h+pad-r)/st,(w+pad-s)/st,co] * Wt[ci][r][s][co]
+//   WGRAD : dW[co][j=(r,s,ci)]    = sum_{m=(n,p,q)}  dY[m][co] * X[n,p*st-pad+r,q*st-pad+s,ci]   (split-K)
+// Layouts: activations NHWC bf16, weights KRSC bf16, accumulation fp32.
+//
+// Reference parity: these replace the cuDNN/MKL-DNN convolutions and Linear layers executed by
+// torchvision ResNet-50 / VGG16 and the HF BERT / transfer heads in the reference
+// (another_neural_net.py:95-112,244-255;
+// pytorch_training_inference_on_image.ipynb:454-635).
+//
+// Structure (cdna_hip_programming.md §5): 256 threads = 4 waves (2x2), block tile BMxBN, BK=64,
+// register-staged double-buffered LDS (global loads for tile t+1 are issued before the MFMAs of
+// tile t and written to the other LDS buffer after them: one barrier per K-step), XOR-swizzled
+// LDS images (ds_read_b128 row reads for FWD/DGRAD; ds_read_b64_tr_b16 transposed reads for
+// WGRAD whose operands are both reduction-index-major), XCD-aware bijective block remap, and an
+// LDS-staged epilogue that writes 16-byte coalesced rows and emits per-column BatchNorm partial
+// statistics of the stored (bf16-rounded) output.
+#include "common.h"
+
+namespace pcmp {
+
+// ----------------------------------------------------------------------------------------------
+// Fast unsigned division by a runtime-invariant divisor (round-up multiply method), n < 2^31.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+enum IgemmMode { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct IgemmParams {
+  const __bf16* a;    // FWD: x[N,H,W,C]; DGRAD: dy[N,P,Q,K]; WGRAD: dy[N,P,Q,K]
+  const __bf16* b;    // FWD: w[K][R][S][C]; DGRAD: wt[C][R][S][K]; WGRAD: x[N,H,W,C]
+  void* out;          // FWD/DGRAD: bf16 [gm][gn]; WGRAD: f32 [split][gm][gn]
+  const float* bias;  // FWD: [gn] (optional)
+  const __bf16* resid;  // FWD/DGRAD: bf16 [gm][gn] added before activation (optional)
+  float* stats;       // FWD/DGRAD: [gridM][2][gn] per-block column sum / sum of squares (optional)
+  int gm, gn, gk;
+  int N, H, W, C, K, R, S, P, Q, stride, pad;
+  FastDiv fd_PQ, fd_Q, fd_HW, fd_W;
+  int relu;
+  int ksplit;       // K elements per split (multiple of BK)
+  int nsplit;
+  int tiles_m, tiles_n;
+  float alpha;
+  int accumulate;   // WGRAD with nsplit==1: out += result
+};
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+// XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD so they share its L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg <= 8) return bid;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// Row-read LDS image for FWD/DGRAD operands: [rows][BK] bf16, 128-B rows, 16-B chunks swizzled
+// chunk ^ (row & 7) -> conflict-free ds_read_b128 for the 16x16x32 fragment pattern.
+__device__ __forceinline__ int rr_off(int row, int chunk) {  // byte offset
+  return row * (BK * 2) + ((chunk ^ (row & 7)) << 4);
+}
+
+// Transposed-read LDS image for WGRAD operands: [BK rows (reduction)][COLS] bf16.
+template <int COLS>
+__device__ __forceinline__ int tr_off(int row, int col) {  // byte offset of element (row,col), col%4==0 ok
+  constexpr int RB = COLS * 2;  // row bytes
+  int f;
+  if constexpr (RB >= 256) {
+    f = (row & 3) | (((row >> 3) & 1) << 2);            // 8 distinct 32-B slots per half-wave
+  } else if constexpr (RB == 128) {
+    f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  } else {
+    f = 0;
+  }
+  const int chunk = (col >> 3) ^ (2 * f);  // 16-B chunk, XOR keeps 32-B pairs intact
+  return row * RB + (chunk << 4) + ((col & 7) << 1);
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NVA = BM * BK / 8 / NT;  // 16-B vectors per thread per stage
+  constexpr int NVB = BN * BK / 8 / NT;
+  static_assert(NVA >= 1 && NVB >= 1, "tile too small");
+  static_assert(WM * WN == 4, "4 waves");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+
+  // ---- tile coordinates ---------------------------------------------------------------------
+  const int nwg = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x, nwg);
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = lin / tiles_mn;
+  const int t = lin - split * tiles_mn;
+  const int tile_n = t % p.tiles_n;
+  const int tile_m = t / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = split * p.ksplit;
+  const int kend = min(p.gk, kbeg + p.ksplit);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[NVA], rb[NVB];
+
+  // ---- per-thread loader state ----------------------------------------------------------------
+  // FWD / DGRAD: thread owns rows (tid>>3)+32*i of the A and B tiles and k-chunk (tid&7).
+  const int lchunk = tid & 7;
+  const int lrow = tid >> 3;
+  // A rows
+  int a_valid[NVA];
+  int a_base[NVA];   // element offset of (n) image base
+  int a_y[NVA], a_x[NVA];  // FWD: p*st-pad, q*st-pad ; DGRAD: h+pad, w+pad
+  // WGRAD: tile A' [BK][BM] rows = reduction index m, cols = co; tile B' [BK][BN] cols = j
+  constexpr int CPR_A = BM / 8, CPR_B = BN / 8;       // 16-B chunks per WGRAD tile row
+  int wa_col = 0, wb_col = 0;
+  int wb_r = 0, wb_s = 0, wb_c = 0, wb_ok = 0;
+  // k -> (r, s, c) incremental state for FWD/DGRAD (chunk fixed per thread)
+  int kr = 0, ks = 0, kc = 0;
+  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;  // innermost channel of the A source
+
+  if constexpr (MODE != MODE_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < NVA; ++i) {
+      const int m = m0 + lrow + 32 * i;
+      a_valid[i] = m < p.gm;
+      const int mm = a_valid[i] ? m : 0;
+      if constexpr (MODE == MODE_FWD) {
+        const int n = fdiv(mm, p.fd_PQ);
+        const int rem = mm - n * p.P * p.Q;
+        const int pp = fdiv(rem, p.fd_Q);
+        const int qq = rem - pp * p.Q;
+        a_base[i] = n * p.H * p.W * p.C;
+        a_y[i] = pp * p.stride - p.pad;
+        a_x[i] = qq * p.stride - p.pad;
+      } else {
+        const int n = fdiv(mm, p.fd_HW);
+        const int rem = mm - n * p.H * p.W;
+        const int hh = fdiv(rem, p.fd_W);
+        const int ww = rem - hh * p.W;
+        a_base[i] = n * p.P * p.Q * p.K;
+        a_y[i] = hh + p.pad;
+        a_x[i] = ww + p.pad;
+      }
+    }
+    const int k = kbeg + lchunk * 8;
+    kc = k % CIN;
+    const int rs = k / CIN;
+    ks = rs % p.S;
+    kr = rs / p.S;
+  } else {
+    wa_col = (tid % CPR_A) * 8;
+    wb_col = (tid % CPR_B) * 8;
+    const int j = n0 + wb_col;
+    wb_ok = j < p.gn;
+    const int jj = wb_ok ? j : 0;
+    wb_c = jj % p.C;
+    const int rs = jj / p.C;
+    wb_s = rs % p.S;
+    wb_r = rs / p.S;
+  }
+
+  auto load_stage = [&](int kt) {
+    const int k0 = kbeg + kt * BK;
+    if constexpr (MODE != MODE_WGRAD) {
+      const int k = k0 + lchunk * 8;
+      const bool kok = k < kend;
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        int yy, xx;
+        bool ok = a_valid[i] && kok;
+        int off;
+        if constexpr (MODE == MODE_FWD) {
+          yy = a_y[i] + kr;
+          xx = a_x[i] + ks;
+          ok = ok && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+          off = a_base[i] + (yy * p.W + xx) * p.C + kc;
+        } else {
+          int ph = a_y[i] - kr, pw = a_x[i] - ks;
+          if (p.stride != 1) {
+            ok = ok && ph >= 0 && pw >= 0 && (ph % p.stride) == 0 && (pw % p.stride) == 0;
+            ph /= p.stride;
+            pw /= p.stride;
+          }
+          ok = ok && (unsigned)ph < (unsigned)p.P && (unsigned)pw < (unsigned)p.Q;
+          off = a_base[i] + (ph * p.Q + pw) * p.K + kc;
+        }
+        ra[i] = ok ? *reinterpret_cast<const uint4*>(p.a + off) : uint4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) {
+        const int n = n0 + lrow + 32 * i;
+        const bool ok = kok && n < p.gn;
+        rb[i] = ok ? *reinterpret_cast<const uint4*>(p.b + (size_t)n * p.gk + k) : uint4{0, 0, 0, 0};
+      }
+      // advance k -> (r,s,c) by BK for the next stage
+      kc += BK;
+      while (kc >= CIN) {
+        kc -= CIN;
+        if (++ks == p.S) { ks = 0; ++kr; }
+      }
+    } else {
+      // A': rows = reduction index m, cols = output channel co (dy rows are contiguous in co)
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        const int v = tid + NT * i;
+        const int row = v / CPR_A;
+        const int m = k0 + row;
+        const int co = m0 + wa_col;
+        const bool ok = m < kend && co < p.gm;
+        ra[i] = ok ? *reinterpret_cast<const uint4*>(p.a + (size_t)m * p.K + co) : uint4{0, 0, 0, 0};
+      }
+      // B': rows = m, cols = j=(r,s,c): im2col gather of x
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) {
+        const int v = tid + NT * i;
+        const int row = v / CPR_B;
+        const int m = k0 + row;
+        bool ok = wb_ok && m < kend;
+        const int mm = ok ? m : 0;
+        const int n = fdiv(mm, p.fd_PQ);
+        const int rem = mm - n * p.P * p.Q;
+        const int pp = fdiv(rem, p.fd_Q);
+        const int qq = rem - pp * p.Q;
+        const int yy = pp * p.stride - p.pad + wb_r;
+        const int xx = qq * p.stride - p.pad + wb_s;
+        ok = ok && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        const size_t off = ((size_t)(n * p.H + yy) * p.W + xx) * p.C + wb_c;
+        rb[i] = ok ? *reinterpret_cast<const uint4*>(p.b + off) : uint4{0, 0, 0, 0};
+      }
+    }
+  };
+
+  auto store_stage = [&](int buf) {
+    char* sA = smem + buf * STAGE;
+    char* sB = sA + A_BYTES;
+    if constexpr (MODE != MODE_WGRAD) {
+#pragma unroll
+      for (int i = 0; i < NVA; ++i)
+        *reinterpret_cast<uint4*>(sA + rr_off(lrow + 32 * i, lchunk)) = ra[i];
+#pragma unroll
+      for (int i = 0; i < NVB; ++i)
+        *reinterpret_cast<uint4*>(sB + rr_off(lrow + 32 * i, lchunk)) = rb[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) {
+        const int v = tid + NT * i;
+        *reinterpret_cast<uint4*>(sA + tr_off<BM>(v / CPR_A, wa_col)) = ra[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) {
+        const int v = tid + NT * i;
+        *reinterpret_cast<uint4*>(sB + tr_off<BN>(v / CPR_B, wb_col)) = rb[i];
+      }
+    }
+  };
+
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+
+  auto compute_stage = [&](int buf) {
+    const char* sA = smem + buf * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+      if constexpr (MODE != MODE_WGRAD) {
+        const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wr * WTM + i * 16 + (lane & 15);
+          fa[i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(row, chunk));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wc * WTN + j * 16 + (lane & 15);
+          fb[j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(row, chunk));
+        }
+      } else {
+        // ds_read_b64_tr_b16: 16-lane group g reads rows kk*32+8g+{0..3} (then +4..7),
+        // lane 4q+p supplies row q, columns 4p..4p+3 of its 16-column block.
+        const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
+        const int rowb = kk * 32 + 8 * g + q;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int col = wr * WTM + i * 16 + pc;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          fa[i] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wc * WTN + j * 16 + pc;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          fb[j] = __builtin_bit_cast(bf16x8, v);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---- main loop: register-staged double buffer, one barrier per K-step ------------------------
+  if (nk > 0) {
+    load_stage(0);
+    store_stage(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load_stage(kt + 1);
+      compute_stage(cur);
+      if (kt + 1 < nk) store_stage(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue -------------------------------------------------------------------------------
+  const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (MODE == MODE_WGRAD) {
+    float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wc * WTN + j * 16 + fr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wr * WTM + i * 16 + fq * 4 + e;
+          if (row < p.gm && col < p.gn) {
+            float v = acc[i][j][e] * p.alpha;
+            float* dst = out + (size_t)row * p.gn + col;
+            if (p.accumulate) v += *dst;
+            *dst = v;
+          }
+        }
+      }
+    return;
+  } else {
+    // stage fp32 wave tile in LDS (row stride WTN+4 floats), then coalesced 16-B row stores.
+    constexpr int LD = WTN + 4;
+    float* sC = reinterpret_cast<float*>(smem) + wid * WTM * LD;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          sC[(i * 16 + fq * 4 + e) * LD + j * 16 + fr] = acc[i][j][e];
+    __syncthreads();  // (also protects the smem reuse below for stats)
+    constexpr int CPR = WTN / 8;        // 8-wide chunks per row
+    constexpr int RPP = 64 / CPR;       // rows per pass
+    const int ch = lane % CPR, rp = lane / CPR;
+    const int col0 = n0 + wc * WTN + ch * 8;
+    const bool col_ok = col0 < p.gn;   // gn % 8 == 0 required by host
+    float bias[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = (p.bias && col_ok) ? p.bias[col0 + e] : 0.f;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+    __bf16* out = reinterpret_cast<__bf16*>(p.out);
+    for (int r = rp; r < WTM; r += RPP) {
+      const int row = m0 + wr * WTM + r;
+      if (row >= p.gm || !col_ok) continue;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(sC + r * LD + ch * 8);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(sC + r * LD + ch * 8 + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const size_t o = (size_t)row * p.gn + col0;
+      u16x8 rv;
+      if (p.resid) rv = *reinterpret_cast<const u16x8*>(p.resid + o);
+      u16x8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = v[e] * p.alpha + bias[e];
+        if (p.resid) x += bf2f(rv[e]);
+        if (p.relu) x = fmaxf(x, 0.f);
+        const unsigned short b = f2bf(x);
+        ov[e] = b;
+        const float xr = bf2f(b);
+        s1[e] += xr;
+        s2[e] += xr * xr;
+      }
+      *reinterpret_cast<u16x8*>(out + o) = ov;
+    }
+    if (p.stats) {
+      // reduce over lanes sharing the same chunk (lane % CPR), then across WM waves via LDS.
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int o = CPR; o < 64; o <<= 1) {
+          s1[e] += __shfl_xor(s1[e], o, 64);
+          s2[e] += __shfl_xor(s2[e], o, 64);
+        }
+      }
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);  // [2][BN]
+      for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
+      __syncthreads();
+      if (rp == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(&red[wc * WTN + ch * 8 + e], s1[e]);
+          atomicAdd(&red[BN + wc * WTN + ch * 8 + e], s2[e]);
+        }
+      }
+      __syncthreads();
+      float* st = p.stats + (size_t)tile_m * 2 * p.gn;
+      for (int i = tid; i < BN; i += NT) {
+        const int c = n0 + i;
+        if (c < p.gn) {
+          st[c] = red[i];
+          st[p.gn + c] = red[BN + i];
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// split-K reduction: dst[i] (+)= sum_s ws[s][i]   (fp32, float4)
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dst,
+                                     int64_t n, int nsplit, int accumulate) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 s = reinterpret_cast<const f32x4*>(ws)[i];
+    for (int k = 1; k < nsplit; ++k) s += reinterpret_cast<const f32x4*>(ws + (size_t)k * n)[i];
+    if (accumulate) s += reinterpret_cast<f32x4*>(dst)[i];
+    reinterpret_cast<f32x4*>(dst)[i] = s;
+  }
+}
+
+// weight transpose for DGRAD: wt[c][r][s][k] = w[k][r][s][c]  (bf16)
+__global__ void wt_transpose_kernel(const unsigned short* __restrict__ w, unsigned short* __restrict__ wt,
+                                    int K, int RS, int C) {
+  __shared__ unsigned short tile[64][65];
+  const int rs = blockIdx.z;
+  const int k0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 4 rows per pass
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + tx;
+    tile[r][tx] = (k < K && c < C) ? w[((size_t)k * RS + rs) * C + c] : 0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + tx;
+    if (c < C && k < K) wt[((size_t)c * RS + rs) * K + k] = tile[tx][r];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+template <int MODE, int BM, int BN, int WM, int WN>
+static void launch_cfg(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  constexpr size_t stage_bytes = 2 * (size_t)(BM + BN) * BK * 2;
+  constexpr size_t epi_bytes = 4 * (size_t)(BM / WM) * (BN / WN + 4) * 4;
+  const size_t smem = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), dim3(grid), dim3(NT), smem, st, p);
+  PCMP_LAUNCH_CHECK();
+}
+
+template <int MODE>
+static void dispatch(IgemmParams& p, hipStream_t st) {
+  // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)
+  if (p.gm <= 32) {
+    if (p.gn <= 64) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
+    else launch_cfg<MODE, 32, 128, 1, 4>(p, st);
+  } else if (p.gm <= 64) {
+    if (p.gn <= 64) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
+    else launch_cfg<MODE, 64, 128, 2, 2>(p, st);
+  } else {
+    if (p.gn <= 64) launch_cfg<MODE, 128, 64, 2, 2>(p, st);
+    else launch_cfg<MODE, 128, 128, 2, 2>(p, st);
+  }
+}
+
+static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int R, int S,
+                          int stride, int pad) {
+  p.N = N; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S;
+  p.stride = stride; p.pad = pad;
+  p.P = (H + 2 * pad - R) / stride + 1;
+  p.Q = (W + 2 * pad - S) / stride + 1;
+  p.fd_PQ = make_fastdiv(p.P * p.Q);
+  p.fd_Q = make_fastdiv(p.Q);
+  p.fd_HW = make_fastdiv(H * W);
+  p.fd_W = make_fastdiv(W);
+  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr;
+  p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
+}
+
+// x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
+// (bf16 [N,P,Q,K]) and ReLU fused; optional stats output [tiles_m,2,K] f32 (returned).
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias,
+                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_BF16(w);
+  PCMP_CHECK_CONTIG(x); PCMP_CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: NHWC x and KRSC w expected");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "conv_fwd: channel mismatch");
+  TORCH_CHECK(C % 8 == 0 && K % 8 == 0, "conv_fwd: C and K must be multiples of 8");
+  IgemmParams p;
+  fill_geometry(p, N, H, W, C, K, R, S, stride, pad);
+  p.gm = N * p.P * p.Q; p.gn = K; p.gk = R * S * C;
+  TORCH_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)p.gm * K < (1ll << 31), "conv_fwd: tensor too large");
+  auto y = at::empty({N, p.P, p.Q, K}, x.options());
+  p.a = ptr<__bf16>(x); p.b = ptr<__bf16>(w); p.out = y.data_ptr();
+  if (bias.has_value() && bias->defined()) { PCMP_CHECK_F32(*bias); p.bias = ptr<float>(*bias); }
+  if (resid.has_value() && resid->defined()) {
+    PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->numel() == y.numel(), "conv_fwd: residual shape");
+    p.resid = ptr<__bf16>(*resid);
+  }
+  p.relu = relu;
+  p.ksplit = p.gk; p.nsplit = 1;
+  const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
+  at::Tensor stats;
+  if (want_stats) {
+    stats = at::empty({ceil_div(p.gm, BMsel), 2, K}, x.options().dtype(at::kFloat));
+    p.stats = ptr<float>(stats);
+  }
+  dispatch<MODE_FWD>(p, cur_stream());
+  if (want_stats) return {y, stats};
+  return {y};
+}
+
+// dy: [N,P,Q,K], w: [K,R,S,C] -> dx [N,H,W,C] (H, W given).  Optional bf16 residual gradient
+// added in the epilogue (the identity path of a residual block).
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride,
+                      int64_t pad, const c10::optional<at::Tensor>& resid) {
+  PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(w);
+  PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(w);
+  const int N = dy.size(0), K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
+  IgemmParams p;
+  fill_geometry(p, N, H, W, C, K, R, S, stride, pad);
+  TORCH_CHECK(dy.size(1) == p.P && dy.size(2) == p.Q && dy.size(3) == K, "conv_dgrad: dy shape");
+  auto st = cur_stream();
+  at::Tensor wt = at::empty({C, R, S, K}, w.options());
+  {
+    dim3 grid(ceil_div(C, 64), ceil_div(K, 64), R * S);
+    hipLaunchKernelGGL(wt_transpose_kernel, grid, dim3(256), 0, st,
+                       ptr<unsigned short>(w), ptr<unsigned short>(wt), K, R * S, C);
+    PCMP_LAUNCH_CHECK();
+  }
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  p.gm = N * H * W; p.gn = C; p.gk = R * S * K;
+  p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(wt); p.out = dx.data_ptr();
+  if (resid.has_value() && resid->defined()) {
+    PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->numel() == dx.numel(), "conv_dgrad: residual shape");
+    p.resid = ptr<__bf16>(*resid);
+  }
+  p.ksplit = p.gk;
+  dispatch<MODE_DGRAD>(p, st);
+  return dx;
+}
+
+// dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
+                int64_t stride, int64_t pad, bool accumulate) {
+  PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(x);
+  PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = dy.size(3);
+  IgemmParams p;
+  fill_geometry(p, N, H, W, C, K, R, S, stride, pad);
+  TORCH_CHECK(dy.size(1) == p.P && dy.size(2) == p.Q, "conv_wgrad: dy shape");
+  TORCH_CHECK(out.numel() == (int64_t)K * R * S * C, "conv_wgrad: out numel");
+  p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
+  p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(x);
+  const int BM = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
+  const int BN = p.gn <= 64 ? 64 : 128;
+  const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
+  const int ksteps = ceil_div(p.gk, BK);
+  int nsplit = std::max(1, std::min(ceil_div(1024, tiles), ksteps / 4));
+  const int steps_per = ceil_div(ksteps, nsplit);
+  nsplit = ceil_div(ksteps, steps_per);
+  p.ksplit = steps_per * BK;
+  p.nsplit = nsplit;
+  auto st = cur_stream();
+  if (nsplit == 1) {
+    p.out = out.data_ptr();
+    p.accumulate = accumulate;
+    dispatch<MODE_WGRAD>(p, st);
+    return;
+  }
+  auto ws = at::empty({(int64_t)nsplit, (int64_t)p.gm * p.gn}, out.options());
+  p.out = ws.data_ptr();
+  dispatch<MODE_WGRAD>(p, st);
+  const int64_t n = (int64_t)p.gm * p.gn;
+  TORCH_CHECK(n % 4 == 0, "conv_wgrad: numel % 4");
+  const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<float>(out),
+                     n, nsplit, (int)accumulate);
+  PCMP_LAUNCH_CHECK();
+}
+
+}  // namespace pcmp
+
+TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu, bool want_stats) -> Tensor[]",
+        &pcmp::conv_fwd);
+  m.def("conv_dgrad(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid) -> Tensor",
+        &pcmp::conv_dgrad);
+  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
+        &pcmp::conv_wgrad);
+}

@@ -1,0 +1,208 @@
+"""ResNet-18/34/50/101/152 (torchvision v1.5 topology; Keras v1 variant) on the fused HIP blocks.
+
+Reference parity:
+  * ``models.resnet50(pretrained=True)`` of another_neural_net.py:95 /
+    pytorch_training_inference_on_image.ipynb:389 — 16 Bottlenecks (3/4/6/3), stride on the 3x3,
+    architecture printout at nb :454-635; 25,557,032 params with the 1000-way fc.
+  * transfer-learning mode: ``freeze_backbone()`` sets requires_grad=False on every
+    backbone parameter while BatchNorm stays in train mode (running stats keep updating, batch
+    statistics are used — the reference's behaviour), and ``replace_head(MLPHead(...))`` swaps
+    ``fc`` (another_neural_net.py:105-112).
+  * ``variant="keras"`` puts the stride on the first 1x1 conv of each downsampling bottleneck
+    (Keras ResNet50 v1, resnet.py:17).  Keras' conv biases are omitted: in front of
+    a train-mode BatchNorm a per-channel bias is cancelled exactly by the mean subtraction (its
+    gradient is identically zero), so they change neither outputs nor training.
+  * ResNet-18 (BasicBlock) is the north-star minimum slice.
+
+Input: NCHW float images (as produced by ``ToTensor``) or NHWC bf16 already padded to 8 channels;
+``prepare_input`` runs the fused NCHW->NHWC/bf16/pad kernel.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ..ops.conv_blocks import ResidualBlockFn, StemFn
+from ..ops.kernels import K
+from .layers import ConvBN, GlobalAvgPool, Linear, MLPHead
+
+STEM_CIN_PAD = 8
+
+
+class Stem(nn.Module):
+    def __init__(self, cin=3):
+        super().__init__()
+        self.conv = ConvBN(cin, 64, 7, stride=2, pad=3, cin_pad=STEM_CIN_PAD)
+
+    def param_list(self):
+        return self.conv.params()
+
+    def forward(self, x):
+        return StemFn.apply(x, self, *self.param_list())
+
+
+class _Block(nn.Module):
+    def param_list(self):
+        ps = []
+        for L in self.main_layers():
+            ps += L.params()
+        if self.down_layer() is not None:
+            ps += self.down_layer().params()
+        return ps
+
+    def down_layer(self):
+        return self.downsample
+
+    def forward(self, x):
+        return ResidualBlockFn.apply(x, self, *self.param_list())
+
+
+class BasicBlock(_Block):
+    expansion = 1
+
+    def __init__(self, cin, planes, stride=1, zero_init_residual=False, stride_in_1x1=False):
+        super().__init__()
+        self.conv1 = ConvBN(cin, planes, 3, stride, 1)
+        self.conv2 = ConvBN(planes, planes, 3, 1, 1, zero_init_gamma=zero_init_residual)
+        self.downsample = ConvBN(cin, planes, 1, stride, 0) if (stride != 1 or cin != planes) else None
+
+    def main_layers(self):
+        return [self.conv1, self.conv2]
+
+
+class Bottleneck(_Block):
+    expansion = 4
+
+    def __init__(self, cin, planes, stride=1, zero_init_residual=False, stride_in_1x1=False):
+        super().__init__()
+        out = planes * 4
+        s1, s3 = (stride, 1) if stride_in_1x1 else (1, stride)
+        self.conv1 = ConvBN(cin, planes, 1, s1, 0)
+        self.conv2 = ConvBN(planes, planes, 3, s3, 1)
+        self.conv3 = ConvBN(planes, out, 1, 1, 0, zero_init_gamma=zero_init_residual)
+        self.downsample = ConvBN(cin, out, 1, stride, 0) if (stride != 1 or cin != out) else None
+
+    def main_layers(self):
+        return [self.conv1, self.conv2, self.conv3]
+
+
+_CFG = {
+    "resnet18": (BasicBlock, [2, 2, 2, 2]),
+    "resnet34": (BasicBlock, [3, 4, 6, 3]),
+    "resnet50": (Bottleneck, [3, 4, 6, 3]),
+    "resnet101": (Bottleneck, [3, 4, 23, 3]),
+    "resnet152": (Bottleneck, [3, 8, 36, 3]),
+}
+
+
+class ResNet(nn.Module):
+    def __init__(self, arch="resnet50", num_classes=1000, variant="torchvision", zero_init_residual=False,
+                 compute_dtype=None):
+        super().__init__()
+        block, layers = _CFG[arch]
+        self.arch = arch
+        self.stem = Stem()
+        stride_in_1x1 = variant == "keras"
+        cin = 64
+        stages = []
+        for i, (planes, n) in enumerate(zip([64, 128, 256, 512], layers)):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(block(cin, planes, stride, zero_init_residual, stride_in_1x1))
+                cin = planes * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.avgpool = GlobalAvgPool()
+        self.feature_dim = cin
+        self.fc = Linear(cin, num_classes)
+        self.compute_dtype = compute_dtype
+
+    # ---- dtype / input ---------------------------------------------------------------------
+    def _cdtype(self, device):
+        if self.compute_dtype is not None:
+            return self.compute_dtype
+        return torch.bfloat16 if device.type == "cuda" else torch.float32
+
+    def prepare_input(self, x):
+        """NCHW float/uint8 images -> NHWC compute-dtype, channels padded to 8."""
+        dt = self._cdtype(x.device)
+        if x.dim() == 4 and x.shape[-1] == STEM_CIN_PAD and x.shape[1] != STEM_CIN_PAD:
+            h = x
+        elif dt == torch.bfloat16:
+            scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+            h = K.nchw_to_nhwc(x.contiguous(), STEM_CIN_PAD, scale, None, None)
+        else:  # fp32 parity path (CPU): no bf16 rounding of the input
+            h = x.float().permute(0, 2, 3, 1)
+            h = torch.nn.functional.pad(h, (0, STEM_CIN_PAD - h.shape[-1])).contiguous()
+            if x.dtype == torch.uint8:
+                h = h / 255.0
+        return h if h.dtype == dt else h.to(dt)
+
+    # ---- forward ----------------------------------------------------------------------------
+    def features(self, x):
+        h = self.prepare_input(x)
+        h = self.stem(h)
+        h = self.layer4(self.layer3(self.layer2(self.layer1(h))))
+        return self.avgpool(h)
+
+    def forward_logits(self, x):
+        f = self.features(x)
+        if hasattr(self.fc, "forward_logits"):
+            return self.fc.forward_logits(f)
+        return self.fc(f)
+
+    def forward(self, x):
+        f = self.features(x)
+        return self.fc(f)
+
+    # ---- transfer learning ------------------------------------------------------------------
+    def freeze_backbone(self):
+        """another_neural_net.py:105-106 — every backbone param frozen; BN stays in train mode."""
+        for n, p in self.named_parameters():
+            if not n.startswith("fc."):
+                p.requires_grad_(False)
+        return self
+
+    def replace_head(self, head: nn.Module):
+        self.fc = head
+        return self
+
+    def backbone_modules(self):
+        return [self.stem, self.layer1, self.layer2, self.layer3, self.layer4]
+
+
+def resnet18(num_classes=1000, **kw):
+    return ResNet("resnet18", num_classes, **kw)
+
+
+def resnet34(num_classes=1000, **kw):
+    return ResNet("resnet34", num_classes, **kw)
+
+
+def resnet50(num_classes=1000, **kw):
+    return ResNet("resnet50", num_classes, **kw)
+
+
+def resnet101(num_classes=1000, **kw):
+    return ResNet("resnet101", num_classes, **kw)
+
+
+def resnet50_transfer(num_classes=10, hidden=512, p=0.2, **kw):
+    """The reference's ResNet-50 TL model (another_neural_net.py:95-112)."""
+    m = resnet50(1000, **kw).freeze_backbone()
+    return m.replace_head(MLPHead(m.feature_dim, hidden, num_classes, p))
+
+
+def count_params(model, logical=True):
+    """Parameter count; ``logical`` subtracts the zero padding of Linear rows and stem channels."""
+    total = 0
+    for mod in model.modules():
+        for name, p in mod.named_parameters(recurse=False):
+            n = p.numel()
+            if logical and isinstance(mod, Linear):
+                n = n // mod.out_pad * mod.out_features if name == "weight" else mod.out_features
+            elif logical and isinstance(mod, ConvBN) and name == "weight" and p.shape[-1] != mod.cin:
+                n = n // p.shape[-1] * mod.cin
+            total += n
+    return total

@@ -1,0 +1,80 @@
+"""Native library loading and backend selection.
+
+Rule: an op on a GPU tensor runs the hand-written HIP kernel from ``_native/libpcmp_hip.so``
+and raises loudly if that library is missing or failed to load (no silent eager fallback);
+an op on a CPU tensor runs the PyTorch reference implementation in :mod:`pcmp.ops.ref`
+(CPU plumbing config + numerics tests).  ``PCMP_KERNELS=torch`` (or
+:func:`set_backend`) forces the reference path on GPU too — used only for A/B parity runs.
+"""
+from __future__ import annotations
+
+import os
+import pathlib
+import threading
+
+import torch
+
+_PKG = pathlib.Path(__file__).resolve().parent.parent
+LIB_PATH = _PKG / "_native" / "libpcmp_hip.so"
+
+_lock = threading.Lock()
+_loaded = False
+_load_error: str | None = None
+_backend = os.environ.get("PCMP_KERNELS", "hip").lower()
+
+
+def load(build_if_missing: bool = False) -> bool:
+    """Load the native op library into ``torch.ops.pcmp``.  Returns True on success."""
+    global _loaded, _load_error
+    with _lock:
+        if _loaded:
+            return True
+        if not LIB_PATH.exists() and build_if_missing:
+            from .. import _build
+            _build.build(verbose=False)
+        if not LIB_PATH.exists():
+            _load_error = f"{LIB_PATH} not built (run __graft_entry__.build() or pcmp._build.build())"
+            return False
+        try:
+            torch.ops.load_library(str(LIB_PATH))
+            _loaded = True
+            _load_error = None
+        except Exception as e:  # pragma: no cover - depends on the environment
+            _load_error = f"failed to load {LIB_PATH}: {e}"
+        return _loaded
+
+
+def available() -> bool:
+    return load()
+
+
+def load_error() -> str | None:
+    return _load_error
+
+
+def set_backend(name: str) -> None:
+    """'hip' (default) or 'torch' (reference ops on every device)."""
+    global _backend
+    assert name in ("hip", "torch"), name
+    _backend = name
+
+
+def backend() -> str:
+    return _backend
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True if ops on ``t`` must run the HIP kernels.  Raises if they are required but absent."""
+    if not t.is_cuda or _backend == "torch":
+        return False
+    if not load():
+        raise RuntimeError(
+            "pcmp: GPU tensor given but the native HIP library is unavailable: "
+            f"{_load_error}.  Refusing to fall back silently (set PCMP_KERNELS=torch to use the "
+            "PyTorch reference path deliberately).")
+    return True
+
+
+def ops():
+    load()
+    return torch.ops.pcmp

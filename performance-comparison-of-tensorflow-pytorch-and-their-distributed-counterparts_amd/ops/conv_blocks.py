@@ -1,0 +1,266 @@
+"""Fused conv+BN(+ReLU) block executors with hand-scheduled backward.
+
+A whole residual block (BasicBlock / Bottleneck, with or without a downsample branch) or the
+ResNet stem is ONE autograd node.  Its forward runs the implicit-GEMM conv kernels (BN partial
+statistics emitted by the conv epilogue), the BN finalize kernel and the fused
+``bn_apply`` (scale/shift + residual branch + ReLU).  Its backward is scheduled by hand so that:
+  * the block tail's ReLU mask, the BN backward of the last conv AND of the downsample branch
+    share one reduction pass and one apply pass;
+  * the identity-path gradient and the downsample dgrad are added inside the dgrad epilogue
+    of the first conv (no separate add kernel, no autograd accumulation);
+  * every weight gradient is written by the wgrad kernel straight into the flat DDP bucket
+    (``pcmp.ops.params.emit_grad``) and announced to the data-parallel engine immediately.
+
+Reference parity: torchvision ResNet-50 Bottleneck (conv1x1-bn-relu-conv3x3(stride)-bn-relu-
+conv1x1-bn (+downsample conv1x1/s + bn) -> add -> relu), printed at
+pytorch_training_inference_on_image.ipynb:454-626; BasicBlock for the ResNet-18 north-star slice;
+stem conv7x7/2-bn-relu-maxpool3x3/2 (:455-458).
+"""
+from __future__ import annotations
+
+import torch
+
+from .kernels import K
+from .params import compute_weight, emit_grad, sink_or_temp
+
+
+def _conv_bn_train(x, L, dtype):
+    """conv (+stats) -> finalize.  Returns c, mean, invstd, scale, shift."""
+    w = compute_weight(L.weight, dtype)
+    c, part = K.conv_fwd(x, w, L.stride, L.pad, None, None, False, True)
+    count = c.numel() // c.shape[-1]
+    track = L.track_running_stats
+    mean, invstd, scale, shift = K.bn_finalize(part, count, L.gamma, L.beta,
+                                               L.running_mean if track else None,
+                                               L.running_var if track else None, L.momentum, L.eps)
+    return c, mean, invstd, scale, shift
+
+
+def _conv_bn_eval(x, L, dtype):
+    w = compute_weight(L.weight, dtype)
+    c = K.conv_fwd(x, w, L.stride, L.pad, None, None, False, False)[0]
+    scale, shift = K.bn_eval_coeff(L.gamma, L.beta, L.running_mean, L.running_var, L.eps)
+    return c, scale, shift
+
+
+def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=None, L2=None, want_g=False):
+    """Backward of one BN (or two BNs sharing the incoming gradient) -> list of dx (+g)."""
+    parts = K.bn_bwd_reduce(dy, ymask, x, mean, invstd, x2, mean2, invstd2)
+    count = x.numel() // x.shape[-1]
+    gout, acc, fin = sink_or_temp(L.gamma)
+    bout, bacc, bfin = sink_or_temp(L.beta)
+    coef = K.bn_bwd_finalize(parts[0], count, L.gamma, mean, invstd, gout, bout, acc or bacc)
+    grads = {L.gamma: fin(), L.beta: bfin()}
+    coef2 = None
+    if x2 is not None:
+        gout2, acc2, fin2 = sink_or_temp(L2.gamma)
+        bout2, bacc2, bfin2 = sink_or_temp(L2.beta)
+        coef2 = K.bn_bwd_finalize(parts[1], count, L2.gamma, mean2, invstd2, gout2, bout2, acc2 or bacc2)
+        grads[L2.gamma] = fin2()
+        grads[L2.beta] = bfin2()
+    outs = K.bn_bwd_apply(dy, ymask, x, coef, x2, coef2, want_g)
+    return outs, grads
+
+
+def _wgrad(L, dy, x, grads):
+    g = emit_grad(L.weight, lambda out, acc: K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad, acc))
+    grads[L.weight] = g
+
+
+class ResidualBlockFn(torch.autograd.Function):
+    """out = relu( BN_L(conv_L(...relu(BN_1(conv_1(x)))...)) + shortcut(x) )."""
+
+    @staticmethod
+    def forward(ctx, x, blk, *params):
+        dtype = x.dtype
+        main, down = blk.main_layers(), blk.down_layer()
+        if not blk.training:
+            h = x
+            for i, L in enumerate(main):
+                c, sc, sh = _conv_bn_eval(h, L, dtype)
+                if i < len(main) - 1:
+                    h = K.bn_apply(c, sc, sh, None, None, None, True)
+                else:
+                    last = (c, sc, sh)
+            if down is not None:
+                cd, scd, shd = _conv_bn_eval(x, down, dtype)
+                return K.bn_apply(last[0], last[1], last[2], cd, scd, shd, True)
+            return K.bn_apply(last[0], last[1], last[2], x, None, None, True)
+
+        acts, cs, stats = [x], [], []
+        h = x
+        for i, L in enumerate(main):
+            c, mean, invstd, sc, sh = _conv_bn_train(h, L, dtype)
+            cs.append(c)
+            stats.append((mean, invstd))
+            if i < len(main) - 1:
+                h = K.bn_apply(c, sc, sh, None, None, None, True)
+                acts.append(h)
+            else:
+                last = (sc, sh)
+        if down is not None:
+            cd, meand, invstdd, scd, shd = _conv_bn_train(x, down, dtype)
+            out = K.bn_apply(cs[-1], last[0], last[1], cd, scd, shd, True)
+        else:
+            cd = meand = invstdd = None
+            out = K.bn_apply(cs[-1], last[0], last[1], x, None, None, True)
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(x, out)
+            ctx.main = main
+            ctx.down = down
+            ctx.acts = acts[1:]          # intermediates only; x and out go through save_for_backward
+            ctx.cs = cs
+            ctx.stats = stats
+            ctx.dstate = (cd, meand, invstdd)
+            ctx.params = params
+            ctx.saved_ok = True
+        else:
+            ctx.saved_ok = False
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        assert ctx.saved_ok, "ResidualBlockFn.backward without saved state"
+        main, down = ctx.main, ctx.down
+        x, out = ctx.saved_tensors
+        acts, cs, stats = [x] + ctx.acts, ctx.cs, ctx.stats
+        cd, meand, invstdd = ctx.dstate
+        dout = dout.contiguous()
+        H, W = x.shape[1], x.shape[2]
+        grads = {}
+        Ll = main[-1]
+        mean, invstd = stats[-1]
+        if down is not None:
+            outs, gr = _bn_backward(dout, out, cs[-1], mean, invstd, Ll, cd, meand, invstdd, down)
+            dh, dcd = outs[0], outs[1]
+            gid = None
+        else:
+            outs, gr = _bn_backward(dout, out, cs[-1], mean, invstd, Ll, want_g=True)
+            dh, gid = outs[0], outs[1]
+            dcd = None
+        grads.update(gr)
+        need_dx = ctx.needs_input_grad[0]
+        dx = None
+        for i in range(len(main) - 1, -1, -1):
+            L = main[i]
+            _wgrad(L, dh, acts[i], grads)
+            wcomp = compute_weight(L.weight, dh.dtype)
+            if i > 0:
+                Hi, Wi = acts[i].shape[1], acts[i].shape[2]
+                da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None)
+                m_prev, is_prev = stats[i - 1]
+                outs, gr = _bn_backward(da, acts[i], cs[i - 1], m_prev, is_prev, main[i - 1])
+                grads.update(gr)
+                dh = outs[0]
+            else:
+                if down is not None:
+                    _wgrad(down, dcd, acts[0], grads)
+                    if need_dx:
+                        t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None)
+                        wd = compute_weight(down.weight, dh.dtype)
+                        dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t)
+                elif need_dx:
+                    dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid)
+        # free saved activations early
+        ctx.acts = ctx.cs = ctx.dstate = None
+        pgrads = tuple(grads.get(p) for p in ctx.params)
+        return (dx, None) + pgrads
+
+
+class StemFn(torch.autograd.Function):
+    """y = maxpool3x3/2( relu( BN( conv7x7/2(x) ) ) )."""
+
+    @staticmethod
+    def forward(ctx, x, stem, *params):
+        L = stem.conv
+        dtype = x.dtype
+        if not stem.training:
+            c, sc, sh = _conv_bn_eval(x, L, dtype)
+            a = K.bn_apply(c, sc, sh, None, None, None, True)
+            return K.maxpool_fwd(a, 3, 2, 1, False)[0]
+        c, mean, invstd, sc, sh = _conv_bn_train(x, L, dtype)
+        a = K.bn_apply(c, sc, sh, None, None, None, True)
+        y, idx = K.maxpool_fwd(a, 3, 2, 1, True)
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(x)
+            ctx.state = (c, a, idx, mean, invstd)
+            ctx.stem = stem
+            ctx.params = params
+        else:
+            ctx.state = None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        c, a, idx, mean, invstd = ctx.state
+        L = ctx.stem.conv
+        grads = {}
+        da = K.maxpool_bwd(dy.contiguous(), idx, a.shape[1], a.shape[2], 3, 2, 1)
+        outs, gr = _bn_backward(da, a, c, mean, invstd, L)
+        grads.update(gr)
+        dc = outs[0]
+        _wgrad(L, dc, x, grads)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.conv_dgrad(dc, compute_weight(L.weight, dc.dtype), x.shape[1], x.shape[2], L.stride, L.pad, None)
+        ctx.state = None
+        return (dx, None) + tuple(grads.get(p) for p in ctx.params)
+
+
+class ConvBiasActFn(torch.autograd.Function):
+    """y = act(conv(x, W) + b) -- VGG16 conv3x3+bias+ReLU and the Keras-style biased convs."""
+
+    @staticmethod
+    def forward(ctx, x, conv, weight, bias):
+        w = compute_weight(weight, x.dtype)
+        y = K.conv_fwd(x, w, conv.stride, conv.pad, bias.float() if bias is not None else None, None,
+                       conv.relu, False)[0]
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(x, y)
+            ctx.conv = conv
+            ctx.weight, ctx.bias = weight, bias
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        conv, weight, bias = ctx.conv, ctx.weight, ctx.bias
+        dy = dy.contiguous()
+        if conv.relu:
+            dy = K.relu_bwd(dy, y)
+        gw = emit_grad(weight, lambda out, acc: K.conv_wgrad(dy, x, out, conv.R, conv.S, conv.stride, conv.pad, acc))
+        gb = emit_grad(bias, lambda out, acc: K.colsum(dy, out, acc)) if bias is not None else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = K.conv_dgrad(dy, compute_weight(weight, dy.dtype), x.shape[1], x.shape[2], conv.stride, conv.pad,
+                              None)
+        return dx, None, gw, gb
+
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, pad):
+        need = ctx.needs_input_grad[0]
+        r = K.maxpool_fwd(x, k, s, pad, need)
+        if need:
+            ctx.save_for_backward(r[1])
+            ctx.cfg = (x.shape[1], x.shape[2], k, s, pad)
+        return r[0]
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        H, W, k, s, pad = ctx.cfg
+        return K.maxpool_bwd(dy.contiguous(), idx, H, W, k, s, pad), None, None, None
+
+
+class GapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[1], x.shape[2])
+        return K.gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return K.gap_bwd(dy.contiguous(), *ctx.hw)

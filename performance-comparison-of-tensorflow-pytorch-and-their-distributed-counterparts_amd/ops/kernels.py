@@ -1,0 +1,51 @@
+"""Device dispatch for the native op set.
+
+``K.<op>(*args)`` runs ``torch.ops.pcmp.<op>`` when the first tensor argument lives on the GPU
+(raising if the HIP library is missing — see :mod:`pcmp.ops._lib`) and the PyTorch reference
+:mod:`pcmp.ops.ref` otherwise.  Both return the same structure.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib, ref
+
+OP_NAMES = (
+    "conv_fwd", "conv_dgrad", "conv_wgrad",
+    "bn_partials", "bn_finalize", "bn_eval_coeff", "bn_apply", "bn_bwd_reduce", "bn_bwd_finalize",
+    "bn_bwd_apply",
+    "maxpool_fwd", "maxpool_bwd", "gap_fwd", "gap_bwd", "softmax_xent", "dropout", "relu_bwd", "colsum",
+    "nchw_to_nhwc",
+    "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16",
+    "embedding_fwd", "embedding_bwd", "lstm_cell_fwd", "lstm_cell_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
+    "masked_mean_fwd", "masked_mean_bwd",
+    "layernorm_fwd", "layernorm_bwd", "gelu_fwd", "gelu_bwd", "bias_act_fwd",
+    "attention_fwd", "attention_bwd", "tanh_fwd", "tanh_bwd", "add_bf16",
+)
+
+
+def _first_tensor(args):
+    for a in args:
+        if isinstance(a, torch.Tensor):
+            return a
+    raise TypeError("no tensor argument")
+
+
+class _Dispatch:
+    def __getattr__(self, name):
+        refimpl = getattr(ref, name, None)
+
+        def call(*args):
+            t = _first_tensor(args)
+            if _lib.use_native(t):
+                return getattr(torch.ops.pcmp, name)(*args)
+            if refimpl is None:
+                raise NotImplementedError(f"no reference implementation for {name}")
+            return refimpl(*args)
+
+        call.__name__ = name
+        setattr(self, name, call)
+        return call
+
+
+K = _Dispatch()

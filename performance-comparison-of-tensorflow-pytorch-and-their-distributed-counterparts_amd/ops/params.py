@@ -1,0 +1,77 @@
+"""Parameter plumbing shared by every autograd Function of the framework.
+
+* **Compute weights.**  Parameters are fp32 masters.  Kernels consume a compute-dtype copy
+  (bf16 on the GPU).  When the model's parameters are flattened (:class:`pcmp.utils.flat.FlatParams`),
+  ``p._shadow`` is a view into one contiguous bf16 buffer that the fused optimizer kernel
+  rewrites in the same pass as the fp32 update; otherwise the copy is cached per ``p._version``.
+
+* **Gradient sinks.**  With flattened parameters each parameter carries ``p.main_grad``, an fp32
+  view into the flat gradient buffer (whose slices are the DDP all-reduce buckets).  Backward
+  kernels write weight gradients straight into that view (overwrite on the first write of a
+  step, accumulate afterwards) and then fire ``p._grad_ready_hook`` so the data-parallel
+  engine can launch the bucket's all-reduce while the rest of backward runs.  Without a sink
+  the gradient is returned to autograd as usual.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+
+def compute_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    sh = getattr(p, "_shadow", None)
+    if sh is not None and sh.dtype == dtype:
+        return sh
+    if p.dtype == dtype:
+        return p.detach()
+    cache = getattr(p, "_shadow_cache", None)
+    if cache is None or cache[0] != p._version or cache[1].dtype != dtype or cache[1].device != p.device:
+        cache = (p._version, p.detach().to(dtype).contiguous())
+        p._shadow_cache = cache
+    return cache[1]
+
+
+def emit_grad(p: torch.Tensor | None, compute: Callable[[torch.Tensor, bool], None]):
+    """Produce the gradient of ``p``.  ``compute(out, accumulate)`` fills an fp32 tensor.
+
+    Returns the tensor to hand back to autograd, or None when it went into a sink.
+    """
+    if p is None or not p.requires_grad:
+        return None
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        fresh = getattr(p, "_grad_fresh", True)
+        compute(mg, not fresh)
+        p._grad_fresh = False
+        hook = getattr(p, "_grad_ready_hook", None)
+        if hook is not None:
+            hook(p)
+        return None
+    out = torch.empty(p.shape, dtype=torch.float32, device=p.device)
+    compute(out, False)
+    return out if p.dtype == torch.float32 else out.to(p.dtype)
+
+
+def needs_grad(p) -> bool:
+    return p is not None and isinstance(p, torch.Tensor) and p.requires_grad
+
+
+def sink_or_temp(p: torch.Tensor | None):
+    """For kernels that write a small gradient (BN gamma/beta) directly: returns
+    (out_tensor_or_None, accumulate, finish) where ``finish()`` returns the autograd value."""
+    if p is None or not p.requires_grad:
+        return None, False, (lambda: None)
+    mg = getattr(p, "main_grad", None)
+    if mg is not None:
+        acc = not getattr(p, "_grad_fresh", True)
+
+        def finish():
+            p._grad_fresh = False
+            hook = getattr(p, "_grad_ready_hook", None)
+            if hook is not None:
+                hook(p)
+            return None
+        return mg, acc, finish
+    tmp = torch.empty(p.shape, dtype=torch.float32, device=p.device)
+    return tmp, False, (lambda: tmp)

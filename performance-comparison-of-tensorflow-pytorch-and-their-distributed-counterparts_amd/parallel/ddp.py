@@ -1,0 +1,157 @@
+"""Data-parallel gradient synchronisation over RCCL (xGMI), bucketed and overlapped with backward.
+
+Reference: the reference's DDP wrap is commented out (pytorch_on_language_distr.py:220-221), so
+its "distributed" runs are independent replicas.  This module is the gradient-
+synchronised data parallelism the north star asks for:
+
+* gradients live in ONE flat fp32 buffer (:class:`pcmp.utils.flat.FlatParams`, reverse
+  registration order), so a bucket is a contiguous slice — the all-reduce runs in place on it,
+  no pack/unpack copies;
+* the wgrad kernels announce each finished parameter (``p._grad_ready_hook``); when the last
+  parameter of a bucket is written, the bucket's ``all_reduce(SUM, async_op=True)`` is issued.
+  ProcessGroupNCCL (RCCL on ROCm) orders its internal stream after the compute stream at the
+  moment of the call, so the collective overlaps with the remaining backward kernels;
+* buckets are launched strictly in index order on every rank (collective order must match);
+* bucket sizing for 7 point-to-point xGMI links per MI355X: a small first bucket (default 4 MB)
+  so communication starts early in backward, then 32 MB buckets so each of RCCL's per-link
+  channel chunks stays >= ~256 KB at world 8;
+* the 1/world averaging is folded into the optimizer kernel's gradient scale (no extra pass);
+* initial parameters and buffers are broadcast from rank 0 (DDP constructor semantics).
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+
+from ..utils.flat import FlatParams
+
+
+class _Bucket:
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched")
+
+    def __init__(self, index, start, end, params):
+        self.index, self.start, self.end, self.params = index, start, end, params
+        self.pending = len(params)
+        self.work = None
+        self.launched = False
+
+
+def plan_buckets(sizes, first_bucket_elems, bucket_elems):
+    """Greedy contiguous bucketing of consecutive slices -> list of [i0, i1) param index ranges."""
+    out, i0, acc = [], 0, 0
+    cap = first_bucket_elems
+    for i, n in enumerate(sizes):
+        acc += n
+        if acc >= cap:
+            out.append((i0, i + 1))
+            i0, acc, cap = i + 1, 0, bucket_elems
+    if i0 < len(sizes):
+        out.append((i0, len(sizes)))
+    return out
+
+
+class DistributedDataParallel(torch.nn.Module):
+    def __init__(self, module: torch.nn.Module, flat: FlatParams, process_group=None, bucket_cap_mb: float = 32.0,
+                 first_bucket_mb: float = 4.0, broadcast_buffers: bool = True, average: bool = True):
+        super().__init__()
+        self.module = module
+        self.flat = flat
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.average = average
+        self.require_sync = True
+        esz = flat.grad.element_size()
+        sizes = []
+        offs = flat.offsets + [flat.numel]
+        for i in range(len(flat.params)):
+            sizes.append(offs[i + 1] - offs[i])
+        ranges = plan_buckets(sizes, int(first_bucket_mb * 2 ** 20 / esz), int(bucket_cap_mb * 2 ** 20 / esz))
+        self.buckets = []
+        self._bucket_of = {}
+        for bi, (i0, i1) in enumerate(ranges):
+            ps = flat.params[i0:i1]
+            b = _Bucket(bi, offs[i0], offs[i1], ps)
+            self.buckets.append(b)
+            for p in ps:
+                self._bucket_of[id(p)] = b
+        for p in flat.params:
+            p._grad_ready_hook = self._on_grad_ready
+        self._next_launch = 0
+        if self.world > 1:
+            self._broadcast_state(broadcast_buffers)
+
+    # ------------------------------------------------------------------------------------------
+    def _broadcast_state(self, buffers: bool):
+        src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+        dist.broadcast(self.flat.master, src, group=self.pg)
+        self.flat.refresh_shadows()
+        if buffers:
+            self.sync_buffers()
+
+    def sync_buffers(self):
+        if self.world <= 1:
+            return
+        src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+        for b in self.module.buffers():
+            if b.is_floating_point() or b.dtype in (torch.int64, torch.int32):
+                dist.broadcast(b, src, group=self.pg)
+
+    def forward(self, *a, **kw):
+        self._reset()
+        return self.module(*a, **kw)
+
+    def _reset(self):
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+            b.launched = False
+        self._next_launch = 0
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation window: buckets are not all-reduced."""
+        old = self.require_sync
+        self.require_sync = False
+        try:
+            yield
+        finally:
+            self.require_sync = old
+
+    # ------------------------------------------------------------------------------------------
+    def _on_grad_ready(self, p):
+        b = self._bucket_of.get(id(p))
+        if b is None:
+            return
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch_ready()
+
+    def _launch_ready(self):
+        while self._next_launch < len(self.buckets) and self.buckets[self._next_launch].pending <= 0:
+            self._launch(self.buckets[self._next_launch])
+            self._next_launch += 1
+
+    def _launch(self, b: _Bucket):
+        b.launched = True
+        if self.world <= 1 or not self.require_sync:
+            return
+        view = self.flat.grad[b.start:b.end]
+        b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def finish_gradient_sync(self):
+        """Call after ``loss.backward()``: launches buckets whose params produced no gradient
+        (their slices hold zeros from ``zero_grad``), then joins every outstanding all-reduce
+        (the compute stream waits on RCCL's stream; the host does not block for NCCL)."""
+        for b in self.buckets:
+            b.pending = 0
+        self._launch_ready()
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+                b.work = None
+        self._reset()
+
+    def grad_scale(self) -> float:
+        return 1.0 / self.world if (self.average and self.world > 1) else 1.0

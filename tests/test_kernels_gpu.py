@@ -1,0 +1,207 @@
+"""Numerics of every HIP kernel against the PyTorch fp32 reference of the same op (GPU only).
+
+Inputs are bf16 (what the kernels consume); the reference computes in fp32 from the same bf16
+values, so differences are accumulation order + output rounding.  Shapes cover the classes of
+SURVEY.md §2.4.1 (stem 7x7/2 with Cin padded to 8, 1x1, 3x3, strided 3x3 and 1x1 downsample,
+narrow and wide Cout, small-M linear).
+"""
+import pytest
+import torch
+
+import pcmp  # noqa: F401
+from pcmp.ops import ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    return torch.ops.pcmp
+
+
+def rnd(*shape, dev, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*shape, device=dev) * scale).to(dtype)
+
+
+def close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    lim = atol + rtol * b.abs().max().item()
+    assert err <= lim, f"max err {err} > {lim}"
+
+
+CONV_SHAPES = [
+    # N, H, W, C, K, R, stride, pad
+    (2, 32, 32, 8, 64, 7, 2, 3),      # stem (Cin padded 3->8)
+    (2, 14, 14, 64, 64, 1, 1, 0),     # 1x1
+    (2, 14, 14, 64, 256, 1, 1, 0),    # 1x1 expand
+    (2, 14, 14, 64, 64, 3, 1, 1),     # 3x3
+    (2, 14, 14, 128, 128, 3, 2, 1),   # 3x3 stride 2
+    (2, 14, 14, 256, 512, 1, 2, 0),   # 1x1 stride-2 downsample
+    (3, 7, 7, 512, 512, 3, 1, 1),     # layer4 3x3 (M not a multiple of the tile)
+    (5, 1, 1, 2048, 16, 1, 1, 0),     # linear, tiny M, N
+    (64, 1, 1, 512, 1000 + 8, 1, 1, 0),  # linear 1000(+pad) classes
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd(gpu, shape):
+    N, H, W, C, K, R, s, p = shape
+    x = rnd(N, H, W, C, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+    bias = torch.randn(K, device=gpu)
+    y, st = _ops().conv_fwd(x, w, s, p, None, None, False, True)
+    yr, str_ = ref.conv_fwd(x, w, s, p, None, None, False, True)
+    close(y, yr)
+    close(st.sum(0), str_.sum(0), rtol=2e-2, atol=1e-1)
+    # fused bias + residual + relu epilogue
+    res = rnd(*yr.shape, dev=gpu)
+    y2 = _ops().conv_fwd(x, w, s, p, bias, res, True, False)[0]
+    y2r = ref.conv_fwd(x, w, s, p, bias, res, True, False)[0]
+    close(y2, y2r)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_dgrad(gpu, shape):
+    N, H, W, C, K, R, s, p = shape
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    dy = rnd(N, P, Q, K, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * K)) ** 0.5)
+    dx = _ops().conv_dgrad(dy, w, H, W, s, p, None)
+    dxr = ref.conv_dgrad(dy, w, H, W, s, p, None)
+    close(dx, dxr)
+    res = rnd(N, H, W, C, dev=gpu)
+    close(_ops().conv_dgrad(dy, w, H, W, s, p, res), ref.conv_dgrad(dy, w, H, W, s, p, res))
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_wgrad(gpu, shape):
+    N, H, W, C, K, R, s, p = shape
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    dy = rnd(N, P, Q, K, dev=gpu)
+    x = rnd(N, H, W, C, dev=gpu)
+    out = torch.empty(K, R, R, C, device=gpu)
+    outr = torch.empty_like(out)
+    _ops().conv_wgrad(dy, x, out, R, R, s, p, False)
+    ref.conv_wgrad(dy, x, outr, R, R, s, p, False)
+    close(out, outr, rtol=1e-2, atol=1e-2)
+    _ops().conv_wgrad(dy, x, out, R, R, s, p, True)
+    close(out, 2 * outr, rtol=1e-2, atol=2e-2)
+
+
+def test_conv_wgrad_large_k_splitk(gpu):
+    # reduction over N*P*Q = 32*28*28 = 25088 rows -> split-K path
+    x = rnd(32, 28, 28, 128, dev=gpu)
+    dy = rnd(32, 28, 28, 128, dev=gpu)
+    out = torch.empty(128, 3, 3, 128, device=gpu)
+    outr = torch.empty_like(out)
+    _ops().conv_wgrad(dy, x, out, 3, 3, 1, 1, False)
+    ref.conv_wgrad(dy, x, outr, 3, 3, 1, 1, False)
+    close(out, outr, rtol=1e-2, atol=1e-1)
+
+
+@pytest.mark.parametrize("C", [8, 64, 256, 2048])
+def test_bn_forward_backward(gpu, C):
+    M = 3000
+    x = rnd(M, C, dev=gpu) * 2 + 0.5
+    x2 = rnd(M, C, dev=gpu)
+    g = torch.rand(C, device=gpu) + 0.5
+    b = torch.randn(C, device=gpu)
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    rm2, rv2 = rm.clone(), rv.clone()
+    part = _ops().bn_partials(x)
+    partr = ref.bn_partials(x)
+    close(part.sum(0), partr.sum(0), rtol=1e-3, atol=1e-1)
+    mean, invstd, sc, sh = _ops().bn_finalize(part, M, g, b, rm, rv, 0.1, 1e-5)
+    meanr, invstdr, scr, shr = ref.bn_finalize(partr, M, g, b, rm2, rv2, 0.1, 1e-5)
+    close(mean, meanr, 1e-4, 1e-4)
+    close(invstd, invstdr, 1e-3, 1e-4)
+    close(rm, rm2, 1e-4, 1e-5)
+    close(rv, rv2, 1e-3, 1e-4)
+    y = _ops().bn_apply(x, sc, sh, x2, None, None, True)
+    yr = ref.bn_apply(x, scr, shr, x2, None, None, True)
+    close(y, yr)
+    dy = rnd(M, C, dev=gpu)
+    p1 = _ops().bn_bwd_reduce(dy, y, x, mean, invstd, None, None, None)[0]
+    p1r = ref.bn_bwd_reduce(dy, yr, x, meanr, invstdr, None, None, None)[0]
+    close(p1.sum(0), p1r.sum(0), 1e-2, 1e-1)
+    dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+    dgr, dbr = torch.empty_like(dg), torch.empty_like(db)
+    coef = _ops().bn_bwd_finalize(p1, M, g, mean, invstd, dg, db, False)
+    coefr = ref.bn_bwd_finalize(p1r, M, g, meanr, invstdr, dgr, dbr, False)
+    close(dg, dgr, 1e-2, 1e-1)
+    close(db, dbr, 1e-2, 1e-1)
+    dx, gg = _ops().bn_bwd_apply(dy, y, x, coef, None, None, True)
+    dxr, ggr = ref.bn_bwd_apply(dy, yr, x, coefr, None, None, True)
+    close(dx, dxr)
+    close(gg, ggr)
+
+
+def test_maxpool_gap(gpu):
+    x = rnd(2, 17, 17, 64, dev=gpu)
+    y, idx = _ops().maxpool_fwd(x, 3, 2, 1, True)
+    yr, idxr = ref.maxpool_fwd(x, 3, 2, 1, True)
+    close(y, yr, 0, 0)
+    dy = rnd(*y.shape, dev=gpu)
+    close(_ops().maxpool_bwd(dy, idx, 17, 17, 3, 2, 1), ref.maxpool_bwd(dy, idxr, 17, 17, 3, 2, 1))
+    g = _ops().gap_fwd(x)
+    close(g, ref.gap_fwd(x))
+    dg = rnd(2, 64, dev=gpu)
+    close(_ops().gap_bwd(dg, 17, 17), ref.gap_bwd(dg, 17, 17))
+
+
+@pytest.mark.parametrize("V", [10, 2, 1000])
+def test_softmax_xent(gpu, V):
+    z = torch.randn(37, V, device=gpu)
+    y = torch.randint(0, V, (37,), device=gpu)
+    y[3] = -100
+    r = _ops().softmax_xent(z, y, True, True, 0.5, -100)
+    rr = ref.softmax_xent(z, y, True, True, 0.5, -100)
+    for a, b in zip(r, rr):
+        close(a, b, 1e-4, 1e-5)
+
+
+def test_dropout_matches_reference_rng(gpu):
+    x = rnd(4096, dev=gpu)
+    y = _ops().dropout(x, 0.2, 1234, 77 << 32)
+    yr = ref.dropout(x, 0.2, 1234, 77 << 32)
+    close(y, yr, 0, 1e-2)
+    keep = (y != 0).float().mean().item()
+    assert 0.75 < keep < 0.85
+
+
+def test_optimizers(gpu):
+    n = 4096 * 3
+    w = torch.randn(n, device=gpu)
+    g = torch.randn(n, device=gpu)
+    lr = torch.tensor([0.1], device=gpu)
+    gs = torch.tensor([0.5], device=gpu)
+    for first in (True, False):
+        w1, w2 = w.clone(), w.clone()
+        m1, m2 = torch.randn(n, device=gpu), None
+        m2 = m1.clone()
+        s1 = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+        s2 = s1.clone()
+        _ops().sgd_flat(w1, g, m1, s1, None, lr, gs, 0.9, 0.0, 1e-4, True, first)
+        ref.sgd_flat(w2, g, m2, s2, None, lr, gs, 0.9, 0.0, 1e-4, True, first)
+        close(w1, w2, 1e-5, 1e-6)
+        close(m1, m2, 1e-5, 1e-6)
+        close(s1, s2, 1e-2, 1e-2)
+    step = torch.tensor([3.0], device=gpu)
+    for dec in (False, True):
+        w1, w2 = w.clone(), w.clone()
+        a1, b1 = torch.randn(n, device=gpu), torch.rand(n, device=gpu)
+        a2, b2 = a1.clone(), b1.clone()
+        _ops().adam_flat(w1, g, a1, b1, None, None, lr, gs, step, 0.9, 0.999, 1e-8, 0.01, dec)
+        ref.adam_flat(w2, g, a2, b2, None, None, lr, gs, step.cpu(), 0.9, 0.999, 1e-8, 0.01, dec)
+        close(w1, w2, 1e-5, 1e-5)
+    norm, coef = _ops().grad_clip_coef(g, 1.0, 1.0, 0.25)
+    normr, coefr = ref.grad_clip_coef(g, 1.0, 1.0, 0.25)
+    close(norm, normr, 1e-5, 1e-4)
+    close(coef, coefr, 1e-5, 1e-7)
+
+
+def test_input_conversion(gpu):
+    x = torch.rand(2, 3, 9, 11, device=gpu)
+    close(_ops().nchw_to_nhwc(x, 8, 1.0, None, None), ref.nchw_to_nhwc(x, 8, 1.0), 0, 1e-2)
+    xu = (torch.rand(2, 3, 9, 11, device=gpu) * 255).to(torch.uint8)
+    close(_ops().nchw_to_nhwc(xu, 8, 1 / 255, None, None), ref.nchw_to_nhwc(xu, 8, 1 / 255), 0, 1e-2)
