@@ -78,9 +78,26 @@ __global__ void bn_partials_kernel(const __bf16* __restrict__ x, float* __restri
   }
 }
 
+// ---- stage-1 column reduction of partials: part [T][L] f32 -> red [G][L] f64 ----------------
+// grid (ceil(L/64), G), 256 threads = 64 columns x 4 row lanes; each block sums `rpb` rows.
+__global__ void partials_reduce_kernel(const float* __restrict__ part, int T, int L, int rpb,
+                                       double* __restrict__ red) {
+  __shared__ double sh[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rpb, r1 = min(T, r0 + rpb);
+  double s = 0;
+  if (col < L)
+    for (int r = r0 + g; r < r1; r += 4) s += part[(size_t)r * L + col];
+  sh[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && col < L) red[(size_t)blockIdx.y * L + col] = s + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+}
+
 // ---- finalize: partials [T][2][C] -> mean, invstd, scale, shift; running stats update --------
 // block = 256 threads handles 64 channels (4 row-groups of partials).
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int T, int C, double count,
+template <typename PT>
+__global__ void bn_finalize_kernel(const PT* __restrict__ part, int T, int C, double count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                    float* __restrict__ rmean, float* __restrict__ rvar, float momentum,
                                    float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
@@ -229,7 +246,8 @@ __global__ void bn_bwd_reduce_kernel(const __bf16* __restrict__ dy, const __bf16
 
 // partials [T][2][C] -> dgamma/dbeta (written/accumulated into dgamma_out/dbeta_out, optional) and
 // per-channel dx coefficients coef[3][C]: dx = k1*g + k2*x + k3
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int T, int C, double count,
+template <typename PT>
+__global__ void bn_bwd_finalize_kernel(const PT* __restrict__ part, int T, int C, double count,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ dgamma_out,
                                        float* __restrict__ dbeta_out, int accumulate, float* __restrict__ coef) {
@@ -329,6 +347,20 @@ at::Tensor bn_partials(const at::Tensor& x) {
   return part;
 }
 
+// Reduce [T][2][C] f32 partials to at most ~64 rows of f64 when T is large (parallel stage 1).
+static at::Tensor reduce_partials(const at::Tensor& part, int& T_out) {
+  const int T = part.size(0), L = 2 * part.size(2);
+  if (T <= 64) { T_out = T; return at::Tensor(); }
+  const int rpb = std::max(16, ceil_div(T, 64));
+  const int G = ceil_div(T, rpb);
+  auto red = at::empty({G, L}, part.options().dtype(at::kDouble));
+  hipLaunchKernelGGL(partials_reduce_kernel, dim3(ceil_div(L, 64), G), dim3(256), 0, cur_stream(), ptr<float>(part),
+                     T, L, rpb, ptr<double>(red));
+  PCMP_LAUNCH_CHECK();
+  T_out = G;
+  return red;
+}
+
 // partials -> (mean, invstd, scale, shift) ; updates running stats in place when given.
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const c10::optional<at::Tensor>& gamma,
                                     const c10::optional<at::Tensor>& beta,
@@ -338,10 +370,18 @@ std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const
   const int T = part.size(0), C = part.size(2);
   auto opts = part.options();
   auto out = at::empty({4, C}, opts);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<float>(part), T,
-                     C, (double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
-                     optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
-                     ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C);
+  int T2;
+  at::Tensor red = reduce_partials(part, T2);
+  if (red.defined())
+    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<double>(red),
+                       T2, C, (double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
+                       optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
+                       ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<float>(part),
+                       T, C, (double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
+                       optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
+                       ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C);
   PCMP_LAUNCH_CHECK();
   return {out[0], out[1], out[2], out[3]};
 }
@@ -411,9 +451,16 @@ at::Tensor bn_bwd_finalize(const at::Tensor& part, int64_t count, const c10::opt
                            bool accumulate) {
   const int T = part.size(0), C = part.size(2);
   auto coef = at::empty({3, C}, part.options());
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<float>(part),
-                     T, C, (double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
-                     optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef));
+  int T2;
+  at::Tensor red = reduce_partials(part, T2);
+  if (red.defined())
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(),
+                       ptr<double>(red), T2, C, (double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
+                       optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef));
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<float>, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(),
+                       ptr<float>(part), T, C, (double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
+                       optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef));
   PCMP_LAUNCH_CHECK();
   return coef;
 }

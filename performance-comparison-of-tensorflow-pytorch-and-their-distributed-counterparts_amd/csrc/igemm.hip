@@ -53,6 +53,8 @@ struct IgemmParams {
   int gm, gn, gk;
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   FastDiv fd_PQ, fd_Q, fd_HW, fd_W;
+  // DGRAD decode: rows m -> (n, hh, ww) over [N][dH][dW]; h = hh*ostep + oph (sub-pixel class)
+  int dH, dW, offy, offx, sub, oph, opw;
   int relu;
   int ksplit;       // K elements per split (multiple of BK)
   int nsplit;
@@ -164,12 +166,12 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
         a_x[i] = qq * p.stride - p.pad;
       } else {
         const int n = fdiv(mm, p.fd_HW);
-        const int rem = mm - n * p.H * p.W;
+        const int rem = mm - n * p.dH * p.dW;
         const int hh = fdiv(rem, p.fd_W);
-        const int ww = rem - hh * p.W;
+        const int ww = rem - hh * p.dW;
         a_base[i] = n * p.P * p.Q * p.K;
-        a_y[i] = hh + p.pad;
-        a_x[i] = ww + p.pad;
+        a_y[i] = hh + p.offy;
+        a_x[i] = ww + p.offx;
       }
     }
     const int k = kbeg + lchunk * 8;
@@ -206,7 +208,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
           off = a_base[i] + (yy * p.W + xx) * p.C + kc;
         } else {
           int ph = a_y[i] - kr, pw = a_x[i] - ks;
-          if (p.stride != 1) {
+          if (p.stride != 1 && !p.sub) {
             ok = ok && ph >= 0 && pw >= 0 && (ph % p.stride) == 0 && (pw % p.stride) == 0;
             ph /= p.stride;
             pw /= p.stride;
@@ -406,7 +408,17 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       const f32x4 v0 = *reinterpret_cast<const f32x4*>(sC + r * LD + ch * 8);
       const f32x4 v1 = *reinterpret_cast<const f32x4*>(sC + r * LD + ch * 8 + 4);
       float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      const size_t o = (size_t)row * p.gn + col0;
+      size_t orow = row;
+      if constexpr (MODE == MODE_DGRAD) {
+        if (p.sub) {
+          const int n = fdiv(row, p.fd_HW);
+          const int rem = row - n * p.dH * p.dW;
+          const int hh = fdiv(rem, p.fd_W);
+          const int ww = rem - hh * p.dW;
+          orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
+        }
+      }
+      const size_t o = orow * p.gn + col0;
       u16x8 rv;
       if (p.resid) rv = *reinterpret_cast<const u16x8*>(p.resid + o);
       u16x8 ov;
@@ -465,27 +477,37 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
     f32x4 s = reinterpret_cast<const f32x4*>(ws)[i];
-    for (int k = 1; k < nsplit; ++k) s += reinterpret_cast<const f32x4*>(ws + (size_t)k * n)[i];
+    int k = 1;
+    for (; k + 4 <= nsplit; k += 4) {
+      const f32x4 a = reinterpret_cast<const f32x4*>(ws + (size_t)k * n)[i];
+      const f32x4 b = reinterpret_cast<const f32x4*>(ws + (size_t)(k + 1) * n)[i];
+      const f32x4 c = reinterpret_cast<const f32x4*>(ws + (size_t)(k + 2) * n)[i];
+      const f32x4 d = reinterpret_cast<const f32x4*>(ws + (size_t)(k + 3) * n)[i];
+      s += (a + b) + (c + d);
+    }
+    for (; k < nsplit; ++k) s += reinterpret_cast<const f32x4*>(ws + (size_t)k * n)[i];
     if (accumulate) s += reinterpret_cast<f32x4*>(dst)[i];
     reinterpret_cast<f32x4*>(dst)[i] = s;
   }
 }
 
-// weight transpose for DGRAD: wt[c][r][s][k] = w[k][r][s][c]  (bf16)
+// weight transpose for DGRAD: wt[c][t][k] = w[k][r(t)][s(t)][c]  (bf16), taps t over a
+// (possibly strided) sub-grid r = r0 + rstep*(t / subS), s = s0 + rstep*(t % subS).
 __global__ void wt_transpose_kernel(const unsigned short* __restrict__ w, unsigned short* __restrict__ wt,
-                                    int K, int RS, int C) {
+                                    int K, int R, int S, int C, int r0, int s0, int rstep, int subS, int T) {
   __shared__ unsigned short tile[64][65];
-  const int rs = blockIdx.z;
+  const int t = blockIdx.z;
+  const int rsrc = (r0 + rstep * (t / subS)) * S + s0 + rstep * (t % subS);
   const int k0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 4 rows per pass
   for (int r = ty; r < 64; r += 4) {
     const int k = k0 + r, c = c0 + tx;
-    tile[r][tx] = (k < K && c < C) ? w[((size_t)k * RS + rs) * C + c] : 0;
+    tile[r][tx] = (k < K && c < C) ? w[((size_t)k * R * S + rsrc) * C + c] : 0;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
     const int c = c0 + r, k = k0 + tx;
-    if (c < C && k < K) wt[((size_t)c * RS + rs) * K + k] = tile[tx][r];
+    if (c < C && k < K) wt[((size_t)c * T + t) * K + k] = tile[tx][r];
   }
 }
 
@@ -528,6 +550,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.fd_Q = make_fastdiv(p.Q);
   p.fd_HW = make_fastdiv(H * W);
   p.fd_W = make_fastdiv(W);
+  p.dH = H; p.dW = W; p.offy = pad; p.offx = pad; p.sub = 0; p.oph = 0; p.opw = 0;
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
 }
@@ -569,8 +592,21 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   return {y};
 }
 
-// dy: [N,P,Q,K], w: [K,R,S,C] -> dx [N,H,W,C] (H, W given).  Optional bf16 residual gradient
-// added in the epilogue (the identity path of a residual block).
+static at::Tensor transpose_taps(const at::Tensor& w, int r0, int s0, int rstep, int subR, int subS,
+                                 hipStream_t st) {
+  const int K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
+  auto wt = at::empty({C, subR, subS, K}, w.options());
+  dim3 grid(ceil_div(C, 64), ceil_div(K, 64), subR * subS);
+  hipLaunchKernelGGL(wt_transpose_kernel, grid, dim3(256), 0, st, ptr<unsigned short>(w), ptr<unsigned short>(wt), K,
+                     R, S, C, r0, s0, rstep, subS, subR * subS);
+  PCMP_LAUNCH_CHECK();
+  return wt;
+}
+
+// dy: [N,P,Q,K], w: [K,R,S,C] -> dx [N,H,W,C] (H, W given) = dgrad + resid (resid optional).
+// Stride 2 runs as up to 4 sub-pixel (parity-class) GEMMs, each over only the taps that reach
+// that class of output pixels (no MFMA work on structural zeros); their epilogues accumulate in
+// place into the residual buffer, which is CONSUMED (its memory becomes dx).
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride,
                       int64_t pad, const c10::optional<at::Tensor>& resid) {
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(w);
@@ -579,22 +615,42 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
   IgemmParams p;
   fill_geometry(p, N, H, W, C, K, R, S, stride, pad);
   TORCH_CHECK(dy.size(1) == p.P && dy.size(2) == p.Q && dy.size(3) == K, "conv_dgrad: dy shape");
-  auto st = cur_stream();
-  at::Tensor wt = at::empty({C, R, S, K}, w.options());
-  {
-    dim3 grid(ceil_div(C, 64), ceil_div(K, 64), R * S);
-    hipLaunchKernelGGL(wt_transpose_kernel, grid, dim3(256), 0, st,
-                       ptr<unsigned short>(w), ptr<unsigned short>(wt), K, R * S, C);
-    PCMP_LAUNCH_CHECK();
+  const bool has_res = resid.has_value() && resid->defined();
+  if (has_res) {
+    PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->numel() == (int64_t)N * H * W * C, "conv_dgrad: residual shape");
   }
+  auto st = cur_stream();
+  if (stride == 2) {
+    at::Tensor dx = has_res ? *resid : at::zeros({N, H, W, C}, dy.options());
+    for (int oph = 0; oph < 2; ++oph)
+      for (int opw = 0; opw < 2; ++opw) {
+        const int r0 = (oph + pad) & 1, s0 = (opw + pad) & 1;
+        const int subR = r0 < R ? (R - r0 + 1) / 2 : 0, subS = s0 < S ? (S - s0 + 1) / 2 : 0;
+        const int dH = (H - oph + 1) / 2, dW = (W - opw + 1) / 2;
+        if (subR == 0 || subS == 0 || dH <= 0 || dW <= 0) continue;
+        at::Tensor wt = transpose_taps(w, r0, s0, 2, subR, subS, st);
+        IgemmParams q = p;
+        q.R = subR; q.S = subS;
+        q.sub = 1; q.oph = oph; q.opw = opw;
+        q.dH = dH; q.dW = dW;
+        q.fd_HW = make_fastdiv(dH * dW);
+        q.fd_W = make_fastdiv(dW);
+        q.offy = (oph + pad - r0) / 2;
+        q.offx = (opw + pad - s0) / 2;
+        q.gm = N * dH * dW; q.gn = C; q.gk = subR * subS * K;
+        q.a = ptr<__bf16>(dy); q.b = ptr<__bf16>(wt); q.out = dx.data_ptr();
+        q.resid = ptr<__bf16>(dx);   // in-place accumulate
+        q.ksplit = q.gk;
+        dispatch<MODE_DGRAD>(q, st);
+      }
+    return dx;
+  }
+  at::Tensor wt = transpose_taps(w, 0, 0, 1, R, S, st);
   auto dx = at::empty({N, H, W, C}, dy.options());
   p.gm = N * H * W; p.gn = C; p.gk = R * S * K;
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(wt); p.out = dx.data_ptr();
-  if (resid.has_value() && resid->defined()) {
-    PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
-    TORCH_CHECK(resid->numel() == dx.numel(), "conv_dgrad: residual shape");
-    p.resid = ptr<__bf16>(*resid);
-  }
+  if (has_res) p.resid = ptr<__bf16>(*resid);
   p.ksplit = p.gk;
   dispatch<MODE_DGRAD>(p, st);
   return dx;
@@ -616,7 +672,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   const int BN = p.gn <= 64 ? 64 : 128;
   const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
   const int ksteps = ceil_div(p.gk, BK);
-  int nsplit = std::max(1, std::min(ceil_div(1024, tiles), ksteps / 4));
+  int nsplit = std::max(1, std::min(std::min(ceil_div(1024, tiles), ksteps / 8), 256));
   const int steps_per = ceil_div(ksteps, nsplit);
   nsplit = ceil_div(ksteps, steps_per);
   p.ksplit = steps_per * BK;

@@ -6,9 +6,14 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib, ref
+
+# PCMP_TRACE_OPS=1 records (op, [shapes]) of every dispatched op in TRACE (profiling aid)
+TRACE = [] if os.environ.get("PCMP_TRACE_OPS") else None
 
 OP_NAMES = (
     "conv_fwd", "conv_dgrad", "conv_wgrad",
@@ -37,6 +42,8 @@ class _Dispatch:
 
         def call(*args):
             t = _first_tensor(args)
+            if TRACE is not None:
+                TRACE.append((name, [tuple(a.shape) if isinstance(a, torch.Tensor) else a for a in args]))
             if _lib.use_native(t):
                 return getattr(torch.ops.pcmp, name)(*args)
             if refimpl is None:
