@@ -1,0 +1,476 @@
+// BiLSTM text-classifier kernels: embedding gather / scatter-add, masked mean pooling and a
+// persistent bidirectional LSTM recurrence (forward and backward-through-time).
+//
+// North-star text path (BASELINE.json config 5): token ids [B,128] (vocab 30522,
+// id 0 = padding, mask = id > 0 exactly as pytorch_on_language_distr.py:84-103 builds it),
+// embedding -> BiLSTM layers -> masked mean pool -> Linear -> CE.
+//
+// Recurrence design (MI355X): the input projection x_t W_ih^T for all t and both directions is
+// ONE MFMA GEMM outside the recurrence (igemm linear).  The recurrence h_{t-1} W_hh^T runs in ONE
+// persistent launch per layer: each workgroup owns J=16 hidden units of one direction and keeps
+// its 4J x H slice of W_hh resident in LDS for all 128 timesteps; per step it reads h_{t-1} of
+// its direction (16 KB), does the 32x64x256 product on MFMA, applies the fused gate
+// nonlinearities + cell update and publishes its h_t slice.  Workgroups of a direction meet once
+// per step at an agent-scope counter barrier (cdna_hip_programming.md §6 Guideline 16: producer
+// vmcnt(0) -> barrier -> release fence -> vmcnt(0) -> relaxed atomic; consumer relaxed poll ->
+// acquire fence -> vmcnt(0) -> barrier).  2*H/J = 32 workgroups are trivially co-resident on
+// 256 CUs; every spin is bounded and a timeout sets an error word instead of hanging.
+//
+// Masking = packed-sequence semantics: at a padded step (mask 0) the state is carried unchanged
+// (h_t = h_{t-1}, c_t = c_{t-1}); the reverse direction therefore starts at the last real token.
+// Backward: the same layout in reverse time computes dgates and dh_rec = dgates W_hh
+// (workgroup j owns columns j of dh_rec and the W_hh[:, j] slice); weight gradients are then
+// plain MFMA GEMMs over all timesteps (igemm wgrad), outside the recurrence.
+#include "common.h"
+
+namespace pcmp {
+
+// ------------------------------------------------------------------------------- embedding
+// out[r][:] = W[ids[r]][:]   (W bf16 [V][E], E % 8 == 0)
+__global__ void embedding_fwd_kernel(const int64_t* __restrict__ ids, const __bf16* __restrict__ W,
+                                     __bf16* __restrict__ out, int64_t rows, int E) {
+  const int EV = E / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * EV;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / EV;
+    const int v = i % EV;
+    const int64_t id = ids[r];
+    reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(W + id * E)[v];
+  }
+}
+
+// dW[ids[r]][:] += dy[r][:]  (fp32 atomics; rows with id == padding_idx skipped)
+__global__ void embedding_bwd_kernel(const int64_t* __restrict__ ids, const __bf16* __restrict__ dy,
+                                     float* __restrict__ dW, int64_t rows, int E, int64_t padding_idx) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows * E;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / E;
+    const int e = i % E;
+    const int64_t id = ids[r];
+    if (id == padding_idx) continue;
+    atomicAdd(dW + id * E + e, bf2f(reinterpret_cast<const unsigned short*>(dy)[i]));
+  }
+}
+
+// ------------------------------------------------------------------------------- masked mean
+// x [B][S][D] bf16, mask [B][S] (int64 ids > 0 or bool/uint8) -> y [B][D] bf16 = mean over valid t
+__global__ void masked_mean_fwd_kernel(const __bf16* __restrict__ x, const int64_t* __restrict__ ids, int B, int S,
+                                       int D, __bf16* __restrict__ y) {
+  const int b = blockIdx.x;
+  __shared__ float cnt_sh;
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int t = 0; t < S; ++t) c += ids[(size_t)b * S + t] > 0;
+    cnt_sh = (float)max(c, 1);
+  }
+  __syncthreads();
+  const float inv = 1.f / cnt_sh;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float s = 0.f;
+    for (int t = 0; t < S; ++t)
+      if (ids[(size_t)b * S + t] > 0) s += bf2f(reinterpret_cast<const unsigned short*>(x)[((size_t)b * S + t) * D + d]);
+    reinterpret_cast<unsigned short*>(y)[(size_t)b * D + d] = f2bf(s * inv);
+  }
+}
+
+__global__ void masked_mean_bwd_kernel(const __bf16* __restrict__ dy, const int64_t* __restrict__ ids, int B, int S,
+                                       int D, __bf16* __restrict__ dx) {
+  const int b = blockIdx.x;
+  __shared__ float cnt_sh;
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int t = 0; t < S; ++t) c += ids[(size_t)b * S + t] > 0;
+    cnt_sh = (float)max(c, 1);
+  }
+  __syncthreads();
+  const float inv = 1.f / cnt_sh;
+  for (int i = threadIdx.x; i < S * D; i += blockDim.x) {
+    const int t = i / D, d = i % D;
+    const float g = ids[(size_t)b * S + t] > 0 ? bf2f(reinterpret_cast<const unsigned short*>(dy)[(size_t)b * D + d]) * inv : 0.f;
+    reinterpret_cast<unsigned short*>(dx)[((size_t)b * S + t) * D + d] = f2bf(g);
+  }
+}
+
+// ------------------------------------------------------------------------------- LSTM
+constexpr int LJ = 16;         // hidden units per workgroup
+constexpr int LB = 32;         // batch rows handled per launch (B must be <= 32; host tiles larger B)
+constexpr int LT = 256;        // threads
+constexpr unsigned kSpinLimit = 1u << 26;
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  const float r = (1.f - e) / (1.f + e);
+  return copysignf(r, x);
+}
+
+// grid barrier among the workgroups of one direction: arrive + wait for `target` arrivals
+__device__ __forceinline__ bool dir_barrier(unsigned* counter, unsigned target, unsigned* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add((gu32*)counter, 1u, RLX_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load((gu32*)counter, RLX_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store((gu32*)err, 1u, RLX_AGENT);
+        ok = false;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return ok;
+}
+
+struct LstmFwdParams {
+  const __bf16* gx;      // [B][S][2][4H] bf16 input projections (+ both biases), dir-major gates i,f,g,o
+  const __bf16* whh;     // [2][4H][H] bf16
+  const int64_t* ids;    // [B][S] token ids (mask = id > 0)
+  __bf16* hout;          // [B][S][2H] bf16 layer output (dir 0 = cols 0..H-1)
+  float* gates;          // [B][S][2][4H] fp32 saved activations (i,f,g,o after nonlinearity)
+  float* cst;            // [B][S][2][H] fp32 cell state c_t
+  __bf16* hbuf;          // [2][2][LB][H] bf16 ping-pong h exchange buffer
+  unsigned* counters;    // [2] per-direction arrival counters (zeroed by host)
+  unsigned* err;
+  int B, S, H;
+};
+
+// grid = 2 * (H / LJ) workgroups; wg -> (dir = wg / (H/LJ), unit block ub = wg % (H/LJ))
+__global__ void __launch_bounds__(LT) lstm_fwd_persistent(const LstmFwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = p.H, nub = H / LJ;
+  const int dir = blockIdx.x / nub, ub = blockIdx.x % nub, j0 = ub * LJ;
+  // LDS: W slice [4*LJ rows][H] bf16 (row r = gate*LJ + jj), h tile [LB][H] bf16, pre-acts [LB][4LJ] f32
+  __bf16* sW = reinterpret_cast<__bf16*>(smem);
+  __bf16* sH = sW + 4 * LJ * H;
+  float* sG = reinterpret_cast<float*>(sH + LB * H);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int i = tid; i < 4 * LJ * H / 8; i += LT) {
+    const int r = i / (H / 8), c8 = i % (H / 8);
+    const int gate = r / LJ, jj = r % LJ;
+    reinterpret_cast<uint4*>(sW)[i] =
+        reinterpret_cast<const uint4*>(p.whh + ((size_t)dir * 4 * H + gate * H + j0 + jj) * H)[c8];
+  }
+  // cell state for (b, jj) pairs owned by this thread: 2 pairs per thread (LB*LJ = 512)
+  float creg[2] = {0.f, 0.f};
+  float hreg[2] = {0.f, 0.f};
+  __syncthreads();
+  unsigned* cnt = p.counters + dir;
+  const int nwg_dir = nub;
+  for (int step = 0; step < p.S; ++step) {
+    const int t = dir == 0 ? step : p.S - 1 - step;
+    const int cur = step & 1;
+    // ---- load h_{t-1} [LB][H] of this direction into LDS (zeros at step 0)
+    if (step == 0) {
+      for (int i = tid; i < LB * H / 8; i += LT) reinterpret_cast<uint4*>(sH)[i] = uint4{0, 0, 0, 0};
+    } else {
+      const __bf16* src = p.hbuf + ((size_t)(cur ^ 1) * 2 + dir) * LB * H;
+      for (int i = tid; i < LB * H / 8; i += LT) reinterpret_cast<uint4*>(sH)[i] = reinterpret_cast<const uint4*>(src)[i];
+    }
+    __syncthreads();
+    // ---- pre-activations [LB=32][4LJ=64] = h @ Wslice^T : wave w -> m-tile (w&1), n-tiles 2*(w>>1)+{0,1}
+    {
+      const int mt = wid & 1;
+      f32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+      for (int k0 = 0; k0 < H; k0 += 32) {
+        const int kk = k0 + 8 * (lane >> 4);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(sH + (mt * 16 + (lane & 15)) * H + kk);
+        const int n0 = (2 * (wid >> 1)) * 16 + (lane & 15);
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(sW + n0 * H + kk);
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(sW + (n0 + 16) * H + kk);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b1, acc1, 0, 0, 0);
+      }
+      const int col = (2 * (wid >> 1)) * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = mt * 16 + (lane >> 4) * 4 + e;
+        sG[row * 4 * LJ + col] = acc0[e];
+        sG[row * 4 * LJ + col + 16] = acc1[e];
+      }
+    }
+    __syncthreads();
+    // ---- cell update for (b, jj): pair q = tid + LT*k
+    __bf16* hdst = p.hbuf + ((size_t)cur * 2 + dir) * LB * H;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = tid + LT * k;
+      const int b = q / LJ, jj = q % LJ, j = j0 + jj;
+      float hn = 0.f;
+      if (b < p.B) {
+        const bool valid = p.ids[(size_t)b * p.S + t] > 0;
+        const size_t gbase = (((size_t)b * p.S + t) * 2 + dir) * 4 * H;
+        float pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          pre[g] = sG[b * 4 * LJ + g * LJ + jj] + bf2f(reinterpret_cast<const unsigned short*>(p.gx)[gbase + g * H + j]);
+        const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanh_f(pre[2]), og = sigm(pre[3]);
+        float cn, hv;
+        if (valid) {
+          cn = fg * creg[k] + ig * gg;
+          hv = og * tanh_f(cn);
+        } else {
+          cn = creg[k];
+          hv = hreg[k];
+        }
+        creg[k] = cn;
+        hreg[k] = hv;
+        hn = hv;
+        p.gates[gbase + 0 * H + j] = ig;
+        p.gates[gbase + 1 * H + j] = fg;
+        p.gates[gbase + 2 * H + j] = gg;
+        p.gates[gbase + 3 * H + j] = og;
+        p.cst[(((size_t)b * p.S + t) * 2 + dir) * H + j] = cn;
+        reinterpret_cast<unsigned short*>(p.hout)[((size_t)b * p.S + t) * 2 * H + dir * H + j] = f2bf(hv);
+      }
+      reinterpret_cast<unsigned short*>(hdst)[b * H + j] = f2bf(hn);
+    }
+    if (step + 1 < p.S) {
+      if (!dir_barrier(cnt, (unsigned)(step + 1) * nwg_dir, p.err)) return;
+    }
+  }
+}
+
+struct LstmBwdParams {
+  const float* gates;    // [B][S][2][4H] activations i,f,g,o
+  const float* cst;      // [B][S][2][H]
+  const __bf16* whh;     // [2][4H][H] bf16
+  const int64_t* ids;
+  const __bf16* dhout;   // [B][S][2H] bf16 gradient w.r.t. layer output
+  __bf16* dgates;        // [B][S][2][4H] bf16 gradient w.r.t. gate pre-activations
+  __bf16* dgbuf;         // [2][2][LB][4H] bf16 ping-pong dgates exchange
+  unsigned* counters;
+  unsigned* err;
+  int B, S, H;
+};
+
+// wg owns hidden units j0..j0+LJ of its direction: cell backward for those units and
+// columns j0..j0+LJ of dh_rec = dgates_{t} @ W_hh  (needs W_hh[:, j0:j0+LJ], all 4H rows)
+__global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = p.H, nub = H / LJ;
+  const int dir = blockIdx.x / nub, ub = blockIdx.x % nub, j0 = ub * LJ;
+  const int G4 = 4 * H;
+  // LDS: Wt slice [LJ cols][4H] bf16 (transposed: row jj holds W_hh[:, j0+jj]), dgates tile [LB][4H] bf16,
+  //      dh_rec [LB][LJ] f32
+  __bf16* sWt = reinterpret_cast<__bf16*>(smem);
+  __bf16* sD = sWt + LJ * G4;
+  float* sR = reinterpret_cast<float*>(sD + LB * G4);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int i = tid; i < LJ * G4; i += LT) {
+    const int jj = i / G4, r = i % G4;
+    reinterpret_cast<unsigned short*>(sWt)[i] =
+        reinterpret_cast<const unsigned short*>(p.whh)[((size_t)dir * G4 + r) * H + j0 + jj];
+  }
+  float dcreg[2] = {0.f, 0.f};
+  float dhcarry[2] = {0.f, 0.f};  // dh flowing to the previous step (recurrent part)
+  __syncthreads();
+  unsigned* cnt = p.counters + dir;
+  for (int step = 0; step < p.S; ++step) {
+    const int t = dir == 0 ? p.S - 1 - step : step;      // reverse of the forward order
+    const int tprev = dir == 0 ? t - 1 : t + 1;          // forward predecessor of t
+    const int cur = step & 1;
+    __bf16* dst = p.dgbuf + ((size_t)cur * 2 + dir) * LB * G4;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = tid + LT * k;
+      const int b = q / LJ, jj = q % LJ, j = j0 + jj;
+      float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
+      if (b < p.B) {
+        const bool valid = p.ids[(size_t)b * p.S + t] > 0;
+        const size_t gbase = (((size_t)b * p.S + t) * 2 + dir) * 4 * H;
+        const float dh = bf2f(reinterpret_cast<const unsigned short*>(p.dhout)[((size_t)b * p.S + t) * 2 * H + dir * H + j]) +
+                         dhcarry[k];
+        if (valid) {
+          const float ig = p.gates[gbase + j], fg = p.gates[gbase + H + j], gg = p.gates[gbase + 2 * H + j],
+                      og = p.gates[gbase + 3 * H + j];
+          const float c = p.cst[(((size_t)b * p.S + t) * 2 + dir) * H + j];
+          const bool has_prev = tprev >= 0 && tprev < p.S;
+          const float cprev = has_prev ? p.cst[(((size_t)b * p.S + tprev) * 2 + dir) * H + j] : 0.f;
+          const float tc = tanh_f(c);
+          const float dc = dcreg[k] + dh * og * (1.f - tc * tc);
+          dgo = dh * tc * og * (1.f - og);
+          dgi = dc * gg * ig * (1.f - ig);
+          dgg = dc * ig * (1.f - gg * gg);
+          dgf = dc * cprev * fg * (1.f - fg);
+          dcreg[k] = dc * fg;
+          dhcarry[k] = 0.f;  // replaced by dgates @ W_hh below
+        } else {
+          // carried state: dh and dc pass through unchanged
+          dhcarry[k] = dh;
+        }
+        __bf16* dg = p.dgates + gbase;
+        reinterpret_cast<unsigned short*>(dg)[j] = f2bf(dgi);
+        reinterpret_cast<unsigned short*>(dg)[H + j] = f2bf(dgf);
+        reinterpret_cast<unsigned short*>(dg)[2 * H + j] = f2bf(dgg);
+        reinterpret_cast<unsigned short*>(dg)[3 * H + j] = f2bf(dgo);
+      }
+      unsigned short* d16 = reinterpret_cast<unsigned short*>(dst) + b * G4;
+      d16[j] = f2bf(dgi);
+      d16[H + j] = f2bf(dgf);
+      d16[2 * H + j] = f2bf(dgg);
+      d16[3 * H + j] = f2bf(dgo);
+    }
+    if (step + 1 == p.S) break;
+    if (!dir_barrier(cnt, (unsigned)(step + 1) * nub, p.err)) return;
+    // ---- gather dgates_t of all units of this direction [LB][4H] into LDS
+    for (int i = tid; i < LB * G4 / 8; i += LT) reinterpret_cast<uint4*>(sD)[i] = reinterpret_cast<const uint4*>(dst)[i];
+    __syncthreads();
+    // ---- dh_rec[b][jj] = sum_r dgates[b][r] * W[r][j0+jj] : M=32 (2 tiles), N=16 (1 tile), K=4H
+    //      waves 0,1 -> m-tile 0,1 with K split in two halves (waves 2,3 take the upper K half)
+    {
+      const int mt = wid & 1, kh = wid >> 1;
+      f32x4 acc = {0, 0, 0, 0};
+      const int kbeg = kh * (G4 / 2), kend = kbeg + G4 / 2;
+      for (int k0 = kbeg; k0 < kend; k0 += 32) {
+        const int kk = k0 + 8 * (lane >> 4);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(sD + (mt * 16 + (lane & 15)) * G4 + kk);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(sWt + (lane & 15) * G4 + kk);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+      }
+      if (kh == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sR[(mt * 16 + (lane >> 4) * 4 + e) * LJ + (lane & 15)] = acc[e];
+      }
+      __syncthreads();
+      if (kh == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sR[(mt * 16 + (lane >> 4) * 4 + e) * LJ + (lane & 15)] += acc[e];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = tid + LT * k;
+      const int b = q / LJ, jj = q % LJ;
+      if (b < p.B) dhcarry[k] += sR[b * LJ + jj];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------- host
+static int ew_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256)); }
+
+at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
+  PCMP_CHECK_CUDA(ids); PCMP_CHECK_BF16(W); PCMP_CHECK_CONTIG(W);
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
+  const int E = W.size(1);
+  TORCH_CHECK(E % 8 == 0, "embedding dim % 8");
+  auto idc = ids.contiguous();
+  auto sizes = idc.sizes().vec();
+  sizes.push_back(E);
+  auto out = at::empty(sizes, W.options());
+  const int64_t rows = idc.numel();
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3(ew_grid(rows * E / 8)), dim3(256), 0, cur_stream(), idc.data_ptr<int64_t>(),
+                     ptr<__bf16>(W), ptr<__bf16>(out), rows, E);
+  PCMP_LAUNCH_CHECK();
+  return out;
+}
+
+void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, int64_t padding_idx, bool accumulate) {
+  PCMP_CHECK_BF16(dy); PCMP_CHECK_F32(dW);
+  auto idc = ids.contiguous();
+  auto dyc = dy.contiguous();
+  const int E = dW.size(-1);
+  if (!accumulate) dW.zero_();
+  const int64_t rows = idc.numel();
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(ew_grid(rows * E)), dim3(256), 0, cur_stream(), idc.data_ptr<int64_t>(),
+                     ptr<__bf16>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  PCMP_LAUNCH_CHECK();
+}
+
+at::Tensor masked_mean_fwd(const at::Tensor& x, const at::Tensor& ids) {
+  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
+  const int B = x.size(0), S = x.size(1), D = x.size(2);
+  auto y = at::empty({B, D}, x.options());
+  auto idc = ids.contiguous();
+  hipLaunchKernelGGL(masked_mean_fwd_kernel, dim3(B), dim3(256), 0, cur_stream(), ptr<__bf16>(x), idc.data_ptr<int64_t>(),
+                     B, S, D, ptr<__bf16>(y));
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+at::Tensor masked_mean_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t S) {
+  PCMP_CHECK_BF16(dy);
+  const int B = dy.size(0), D = dy.size(1);
+  auto dx = at::empty({B, S, D}, dy.options());
+  auto idc = ids.contiguous();
+  auto dyc = dy.contiguous();
+  hipLaunchKernelGGL(masked_mean_bwd_kernel, dim3(B), dim3(256), 0, cur_stream(), ptr<__bf16>(dyc),
+                     idc.data_ptr<int64_t>(), B, (int)S, D, ptr<__bf16>(dx));
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+static void check_lstm_shapes(int B, int H) {
+  TORCH_CHECK(B <= LB, "lstm: per-launch batch must be <= 32 (host splits larger batches)");
+  TORCH_CHECK(H % LJ == 0 && H % 32 == 0 && H <= 512, "lstm: hidden size must be a multiple of 32, <= 512");
+}
+
+// gx [B][S][2][4H] bf16 (input projection incl. biases), whh [2][4H][H] bf16, ids [B][S]
+// -> [hout bf16 [B][S][2H], gates f32 [B][S][2][4H], c f32 [B][S][2][H]]
+std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh, const at::Tensor& ids) {
+  PCMP_CHECK_BF16(gx); PCMP_CHECK_CONTIG(gx); PCMP_CHECK_BF16(whh); PCMP_CHECK_CONTIG(whh);
+  const int B = gx.size(0), S = gx.size(1), H = whh.size(2);
+  check_lstm_shapes(B, H);
+  TORCH_CHECK(gx.size(2) == 2 && gx.size(3) == 4 * H, "lstm_seq_fwd: gx shape");
+  auto idc = ids.contiguous();
+  auto hout = at::empty({B, S, 2 * H}, whh.options());
+  auto f32 = gx.options().dtype(at::kFloat);
+  auto gates = at::empty({B, S, 2, 4 * H}, f32);
+  auto cst = at::empty({B, S, 2, H}, f32);
+  auto hbuf = at::empty({2, 2, LB, H}, whh.options());
+  auto sync = at::zeros({4}, gx.options().dtype(at::kInt));
+  LstmFwdParams p{ptr<__bf16>(gx), ptr<__bf16>(whh), idc.data_ptr<int64_t>(), ptr<__bf16>(hout), ptr<float>(gates),
+                  ptr<float>(cst), ptr<__bf16>(hbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
+                  reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H};
+  const size_t smem = (size_t)4 * LJ * H * 2 + (size_t)LB * H * 2 + (size_t)LB * 4 * LJ * 4;
+  TORCH_CHECK(smem <= 160 * 1024, "lstm_seq_fwd: LDS budget exceeded");
+  hipLaunchKernelGGL(lstm_fwd_persistent, dim3(2 * (H / LJ)), dim3(LT), smem, cur_stream(), p);
+  PCMP_LAUNCH_CHECK();
+  return {hout, gates, cst, sync};
+}
+
+// -> dgates bf16 [B][S][2][4H]  (and the sync/error words)
+std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& gates, const at::Tensor& cst,
+                                     const at::Tensor& whh, const at::Tensor& ids) {
+  PCMP_CHECK_BF16(dhout); PCMP_CHECK_F32(gates); PCMP_CHECK_F32(cst);
+  const int B = gates.size(0), S = gates.size(1), H = whh.size(2);
+  check_lstm_shapes(B, H);
+  auto idc = ids.contiguous();
+  auto dh = dhout.contiguous();
+  auto dgates = at::empty({B, S, 2, 4 * H}, whh.options());
+  auto dgbuf = at::empty({2, 2, LB, 4 * H}, whh.options());
+  auto sync = at::zeros({4}, gates.options().dtype(at::kInt));
+  LstmBwdParams p{ptr<float>(gates), ptr<float>(cst), ptr<__bf16>(whh), idc.data_ptr<int64_t>(), ptr<__bf16>(dh),
+                  ptr<__bf16>(dgates), ptr<__bf16>(dgbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
+                  reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H};
+  const size_t smem = (size_t)LJ * 4 * H * 2 + (size_t)LB * 4 * H * 2 + (size_t)LB * LJ * 4;
+  TORCH_CHECK(smem <= 160 * 1024, "lstm_seq_bwd: LDS budget exceeded");
+  hipLaunchKernelGGL(lstm_bwd_persistent, dim3(2 * (H / LJ)), dim3(LT), smem, cur_stream(), p);
+  PCMP_LAUNCH_CHECK();
+  return {dgates, sync};
+}
+
+}  // namespace pcmp
+
+TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("embedding_fwd(Tensor ids, Tensor W) -> Tensor", &pcmp::embedding_fwd);
+  m.def("embedding_bwd(Tensor ids, Tensor dy, Tensor(a!) dW, int padding_idx, bool accumulate) -> ()",
+        &pcmp::embedding_bwd);
+  m.def("masked_mean_fwd(Tensor x, Tensor ids) -> Tensor", &pcmp::masked_mean_fwd);
+  m.def("masked_mean_bwd(Tensor dy, Tensor ids, int S) -> Tensor", &pcmp::masked_mean_bwd);
+  m.def("lstm_seq_fwd(Tensor gx, Tensor whh, Tensor ids) -> Tensor[]", &pcmp::lstm_seq_fwd);
+  m.def("lstm_seq_bwd(Tensor dhout, Tensor gates, Tensor cst, Tensor whh, Tensor ids) -> Tensor[]", &pcmp::lstm_seq_bwd);
+}

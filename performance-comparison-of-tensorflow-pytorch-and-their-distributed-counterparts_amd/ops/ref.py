@@ -306,3 +306,194 @@ def grad_clip_coef(g, pre_scale, max_norm, post_scale):
 
 def cast_to_bf16(x, y):
     y.copy_(x.to(y.dtype))
+
+
+# ------------------------------------------------------------------------------ text / LSTM
+def embedding_fwd(ids, W):
+    return W[ids]
+
+
+def embedding_bwd(ids, dy, dW, padding_idx, accumulate):
+    if not accumulate:
+        dW.zero_()
+    E = dW.shape[-1]
+    idf = ids.reshape(-1)
+    g = dy.reshape(-1, E).float()
+    keep = idf != padding_idx
+    dW.index_add_(0, idf[keep], g[keep])
+
+
+def masked_mean_fwd(x, ids):
+    m = (ids > 0).float().unsqueeze(-1)
+    cnt = m.sum(1).clamp_min(1.0)
+    return ((x.float() * m).sum(1) / cnt).to(x.dtype)
+
+
+def masked_mean_bwd(dy, ids, S):
+    m = (ids > 0).float().unsqueeze(-1)
+    cnt = m.sum(1, keepdim=True).clamp_min(1.0)
+    return (dy.float().unsqueeze(1) * m / cnt).to(dy.dtype)
+
+
+def lstm_seq_fwd(gx, whh, ids):
+    """Reference recurrence with packed-sequence masking (state carried at padded steps)."""
+    B, S, _, G4 = gx.shape
+    H = G4 // 4
+    dev = gx.device
+    hout = torch.zeros(B, S, 2 * H, dtype=whh.dtype, device=dev)
+    gates = torch.zeros(B, S, 2, 4 * H, dtype=torch.float32, device=dev)
+    cst = torch.zeros(B, S, 2, H, dtype=torch.float32, device=dev)
+    valid = ids > 0
+    for d in range(2):
+        W = whh[d].float()
+        h = torch.zeros(B, H, device=dev)
+        hq = torch.zeros(B, H, device=dev)  # compute-dtype rounded h used by the recurrence
+        c = torch.zeros(B, H, device=dev)
+        order = range(S) if d == 0 else range(S - 1, -1, -1)
+        for t in order:
+            pre = gx[:, t, d].float() + hq @ W.t()
+            i, f, g, o = pre.split(H, dim=1)
+            i, f, g, o = torch.sigmoid(i), torch.sigmoid(f), torch.tanh(g), torch.sigmoid(o)
+            cn = f * c + i * g
+            hn = o * torch.tanh(cn)
+            v = valid[:, t].unsqueeze(1)
+            c = torch.where(v, cn, c)
+            h = torch.where(v, hn, h)
+            hq = h.to(whh.dtype).float()
+            gates[:, t, d] = torch.cat([i, f, g, o], 1)
+            cst[:, t, d] = c
+            hout[:, t, d * H:(d + 1) * H] = h.to(whh.dtype)
+    return [hout, gates, cst, torch.zeros(4, dtype=torch.int32, device=dev)]
+
+
+def lstm_seq_bwd(dhout, gates, cst, whh, ids):
+    B, S, _, G4 = gates.shape
+    H = G4 // 4
+    dev = gates.device
+    dgates = torch.zeros(B, S, 2, G4, dtype=whh.dtype, device=dev)
+    valid = ids > 0
+    for d in range(2):
+        W = whh[d].float()
+        dh_carry = torch.zeros(B, H, device=dev)
+        dc = torch.zeros(B, H, device=dev)
+        order = range(S - 1, -1, -1) if d == 0 else range(S)
+        for t in order:
+            tprev = t - 1 if d == 0 else t + 1
+            i, f, g, o = gates[:, t, d].split(H, dim=1)
+            c = cst[:, t, d]
+            cprev = cst[:, tprev, d] if 0 <= tprev < S else torch.zeros_like(c)
+            dh = dhout[:, t, d * H:(d + 1) * H].float() + dh_carry
+            tc = torch.tanh(c)
+            dcn = dc + dh * o * (1 - tc * tc)
+            dgo = dh * tc * o * (1 - o)
+            dgi = dcn * g * i * (1 - i)
+            dgg = dcn * i * (1 - g * g)
+            dgf = dcn * cprev * f * (1 - f)
+            dg = torch.cat([dgi, dgf, dgg, dgo], 1)
+            v = valid[:, t].unsqueeze(1)
+            dg = torch.where(v, dg, torch.zeros_like(dg))
+            dgq = dg.to(whh.dtype)
+            dgates[:, t, d] = dgq
+            dc = torch.where(v, dcn * f, dc)
+            dh_carry = torch.where(v, dgq.float() @ W, dh)
+    return [dgates, torch.zeros(4, dtype=torch.int32, device=dev)]
+
+
+# ------------------------------------------------------------------------------ transformer
+def layernorm_fwd(x, r, g, b, eps):
+    xs = x.float() + r.float() if r is not None else x.float()
+    if r is not None:
+        xs = xs.to(x.dtype).float()
+    mean = xs.mean(-1)
+    var = ((xs - mean.unsqueeze(-1)) ** 2).mean(-1)
+    rstd = torch.rsqrt(var + eps)
+    y = (xs - mean.unsqueeze(-1)) * rstd.unsqueeze(-1) * g + b
+    D = x.shape[-1]
+    return [y.to(x.dtype), xs.to(x.dtype), mean.reshape(-1), rstd.reshape(-1)]
+
+
+def layernorm_bwd(dy, xs, mean, rstd, g, dg, db, accumulate):
+    D = xs.shape[-1]
+    dyf = dy.float().reshape(-1, D)
+    xh = (xs.float().reshape(-1, D) - mean.view(-1, 1)) * rstd.view(-1, 1)
+    gy = dyf * g
+    dx = rstd.view(-1, 1) * (gy - gy.mean(-1, keepdim=True) - xh * (gy * xh).mean(-1, keepdim=True))
+    if dg is not None:
+        (dg.add_ if accumulate else dg.copy_)((dyf * xh).sum(0))
+    if db is not None:
+        (db.add_ if accumulate else db.copy_)(dyf.sum(0))
+    return dx.reshape(xs.shape).to(dy.dtype)
+
+
+def gelu_fwd(x):
+    return F.gelu(x.float()).to(x.dtype)
+
+
+def gelu_bwd(dy, x):
+    xf = x.float()
+    cdf = 0.5 * (1 + torch.erf(xf * 0.7071067811865476))
+    pdf = 0.3989422804014327 * torch.exp(-0.5 * xf * xf)
+    return (dy.float() * (cdf + xf * pdf)).to(dy.dtype)
+
+
+def tanh_fwd(x):
+    return torch.tanh(x.float()).to(x.dtype)
+
+
+def tanh_bwd(dy, y):
+    return (dy.float() * (1 - y.float() ** 2)).to(dy.dtype)
+
+
+def add_bf16(a, b):
+    return (a.float() + b.float()).to(a.dtype)
+
+
+def _attn_prep(qkv, ids, B, S, H):
+    D = qkv.shape[-1] // 3
+    t = qkv.float().view(B, S, 3, H, D // H)
+    q, k, v = t[:, :, 0].transpose(1, 2), t[:, :, 1].transpose(1, 2), t[:, :, 2].transpose(1, 2)  # [B,H,S,d]
+    bias = torch.zeros(B, 1, 1, S, device=qkv.device)
+    if ids is not None:
+        bias = torch.where((ids > 0).view(B, 1, 1, S), bias, torch.full_like(bias, -1e30))
+    return q, k, v, bias, D
+
+
+def _attn_drop(B, H, S, p, seed, offset, device):
+    if p <= 0:
+        return None
+    idx = torch.arange(B * H * S * S, device=device, dtype=torch.int64) + offset
+    keep = hash_uniform(seed, idx).view(B, H, S, S) >= p
+    return keep.float() / (1.0 - p)
+
+
+def attention_fwd(qkv, ids, B, S, H, p_drop, seed, offset):
+    q, k, v, bias, D = _attn_prep(qkv, ids, B, S, H)
+    s = q @ k.transpose(-1, -2) * 0.125 + bias
+    lse = torch.logsumexp(s, -1)
+    P = torch.exp(s - lse.unsqueeze(-1))
+    dm = _attn_drop(B, H, S, p_drop, seed, offset, qkv.device)
+    if dm is not None:
+        P = P * dm
+    P = P.to(qkv.dtype).float()
+    ctx = (P @ v).transpose(1, 2).reshape(B * S, D)
+    return [ctx.to(qkv.dtype), lse.reshape(B * H, S)]
+
+
+def attention_bwd(dctx, qkv, ctx, lse, ids, B, S, H, p_drop, seed, offset):
+    q, k, v, bias, D = _attn_prep(qkv, ids, B, S, H)
+    d = D // H
+    dO = dctx.float().view(B, S, H, d).transpose(1, 2)
+    O = ctx.float().view(B, S, H, d).transpose(1, 2)
+    s = q @ k.transpose(-1, -2) * 0.125 + bias
+    P = torch.exp(s - lse.view(B, H, S, 1))
+    dm = _attn_drop(B, H, S, p_drop, seed, offset, qkv.device)
+    Pd = P * dm if dm is not None else P
+    dV = Pd.to(qkv.dtype).float().transpose(-1, -2) @ dO
+    dPd = dO @ v.transpose(-1, -2)
+    dP = dPd * dm if dm is not None else dPd
+    Dd = (dO * O).sum(-1, keepdim=True)
+    dS = (P * (dP - Dd)).to(qkv.dtype).float()
+    dQ = dS @ k * 0.125
+    dK = dS.transpose(-1, -2) @ q * 0.125
+    out = torch.stack([dQ, dK, dV], 2)  # [B,H,3,S,d]
+    return out.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * D).to(qkv.dtype)

@@ -1,0 +1,168 @@
+"""GPU numerics of the BiLSTM / BERT kernels against their PyTorch references, plus model-level
+HIP-vs-reference checks for BiLSTM, BERT and VGG16."""
+import pytest
+import torch
+
+import pcmp  # noqa: F401
+from pcmp.ops import _lib, ref
+
+pytestmark = pytest.mark.gpu
+
+
+def ops():
+    return torch.ops.pcmp
+
+
+def close(a, b, rtol=2e-2, atol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    lim = atol + rtol * b.abs().max().item()
+    assert err <= lim, f"max err {err} > {lim}"
+
+
+def _ids(B, S, V, dev, lens=None):
+    ids = torch.randint(1, V, (B, S), device=dev)
+    lens = lens or [S - (7 * i) % S for i in range(B)]
+    for i, l in enumerate(lens):
+        ids[i, max(1, l):] = 0
+    return ids
+
+
+def test_embedding_and_masked_mean(gpu):
+    ids = _ids(6, 40, 500, gpu)
+    W = torch.randn(500, 64, device=gpu).to(torch.bfloat16)
+    close(ops().embedding_fwd(ids, W), ref.embedding_fwd(ids, W), 0, 0)
+    dy = torch.randn(6, 40, 64, device=gpu).to(torch.bfloat16)
+    d1 = torch.zeros(500, 64, device=gpu)
+    d2 = torch.zeros(500, 64, device=gpu)
+    ops().embedding_bwd(ids, dy, d1, 0, False)
+    ref.embedding_bwd(ids, dy, d2, 0, False)
+    close(d1, d2, 1e-4, 1e-3)
+    x = torch.randn(6, 40, 64, device=gpu).to(torch.bfloat16)
+    close(ops().masked_mean_fwd(x, ids), ref.masked_mean_fwd(x, ids))
+    g = torch.randn(6, 64, device=gpu).to(torch.bfloat16)
+    close(ops().masked_mean_bwd(g, ids, 40), ref.masked_mean_bwd(g, ids, 40))
+
+
+@pytest.mark.parametrize("B,S,H", [(5, 40, 64), (32, 128, 256)])
+def test_lstm_recurrence(gpu, B, S, H):
+    torch.manual_seed(0)
+    ids = _ids(B, S, 1000, gpu)
+    gx = (torch.randn(B, S, 2, 4 * H, device=gpu) * 0.5).to(torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, device=gpu) / H ** 0.5).to(torch.bfloat16)
+    h, g, c, sync = ops().lstm_seq_fwd(gx, whh, ids)
+    hr, gr, cr, _ = ref.lstm_seq_fwd(gx, whh, ids)
+    torch.cuda.synchronize()
+    assert int(sync[2].item()) == 0, "barrier timeout"
+    close(h, hr, 3e-2, 3e-2)
+    close(c, cr, 3e-2, 3e-2)
+    dh = torch.randn(B, S, 2 * H, device=gpu).to(torch.bfloat16)
+    dg, sync2 = ops().lstm_seq_bwd(dh, g, c, whh, ids)
+    dgr, _ = ref.lstm_seq_bwd(dh, gr, cr, whh, ids)
+    torch.cuda.synchronize()
+    assert int(sync2[2].item()) == 0, "barrier timeout"
+    close(dg, dgr, 5e-2, 5e-2)
+
+
+def test_layernorm_act(gpu):
+    x = torch.randn(300, 768, device=gpu).to(torch.bfloat16)
+    r = torch.randn(300, 768, device=gpu).to(torch.bfloat16)
+    g = torch.rand(768, device=gpu) + 0.5
+    b = torch.randn(768, device=gpu)
+    y, xs, m, s = ops().layernorm_fwd(x, r, g, b, 1e-12)
+    yr, xsr, mr, sr = ref.layernorm_fwd(x, r, g, b, 1e-12)
+    close(y, yr)
+    close(xs, xsr, 0, 1e-2)
+    dy = torch.randn(300, 768, device=gpu).to(torch.bfloat16)
+    dg1, db1, dg2, db2 = (torch.zeros(768, device=gpu) for _ in range(4))
+    dx = ops().layernorm_bwd(dy, xs, m, s, g, dg1, db1, False)
+    dxr = ref.layernorm_bwd(dy, xsr, mr, sr, g, dg2, db2, False)
+    close(dx, dxr)
+    close(dg1, dg2, 1e-3, 1e-2)
+    close(db1, db2, 1e-3, 1e-2)
+    z = torch.randn(64, 3072, device=gpu).to(torch.bfloat16)
+    close(ops().gelu_fwd(z), ref.gelu_fwd(z))
+    close(ops().gelu_bwd(dy[:64, :768].repeat(1, 4).contiguous(), z), ref.gelu_bwd(dy[:64, :768].repeat(1, 4), z))
+    t = ops().tanh_fwd(z)
+    close(t, ref.tanh_fwd(z))
+    close(ops().tanh_bwd(z, t), ref.tanh_bwd(z, t))
+
+
+@pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (64, 0.1)])
+def test_attention(gpu, S, p):
+    torch.manual_seed(1)
+    B, H, D = 3, 12, 768
+    qkv = torch.randn(B * S, 3 * D, device=gpu).to(torch.bfloat16)
+    ids = _ids(B, S, 30522, gpu, lens=[S, S // 2, 3])
+    o, lse = ops().attention_fwd(qkv, ids, B, S, H, p, 99, 5 << 32)
+    or_, lser = ref.attention_fwd(qkv, ids, B, S, H, p, 99, 5 << 32)
+    close(o, or_)
+    close(lse, lser, 1e-3, 1e-3)
+    do = torch.randn(B * S, D, device=gpu).to(torch.bfloat16)
+    dq = ops().attention_bwd(do, qkv, o, lse, ids, B, S, H, p, 99, 5 << 32)
+    dqr = ref.attention_bwd(do, qkv, or_, lser, ids, B, S, H, p, 99, 5 << 32)
+    close(dq, dqr, 3e-2, 3e-2)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _grads(model, fn, backend):
+    from pcmp.ops.functions import dropout_rng
+    dropout_rng.reseed(1234)
+    _lib.set_backend(backend)
+    try:
+        for p in model.parameters():
+            p.grad = None
+        loss = fn()
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.item(), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    finally:
+        _lib.set_backend("hip")
+
+
+def test_bilstm_model_native_vs_ref(gpu):
+    from pcmp.models.bilstm import BiLSTMClassifier
+    from pcmp.ops import cross_entropy
+    from pcmp.ops.rnn import check_errors
+    torch.manual_seed(0)
+    m = BiLSTMClassifier(2000, 128, 128, 2, 2, 0.0).to(gpu).train()
+    ids = _ids(40, 64, 2000, gpu)
+    y = torch.randint(0, 2, (40,), device=gpu)
+    l1, g1 = _grads(m, lambda: cross_entropy(m.forward_logits(ids), y), "hip")
+    check_errors()
+    l2, g2 = _grads(m, lambda: cross_entropy(m.forward_logits(ids), y), "torch")
+    assert abs(l1 - l2) < 2e-2
+    for n in g2:
+        assert _rel(g1[n], g2[n]) < 0.08, n
+
+
+def test_bert_model_native_vs_ref(gpu):
+    from pcmp.models.bert import BertConfig, BertForSequenceClassification
+    torch.manual_seed(0)
+    m = BertForSequenceClassification(BertConfig(num_hidden_layers=2, hidden_dropout_prob=0.0,
+                                                 attention_probs_dropout_prob=0.0)).to(gpu).train()
+    ids = _ids(4, 128, 30522, gpu, lens=[128, 100, 50, 7])
+    y = torch.randint(0, 2, (4,), device=gpu)
+    l1, g1 = _grads(m, lambda: m(ids, None, (ids > 0).long(), y)[0], "hip")
+    l2, g2 = _grads(m, lambda: m(ids, None, (ids > 0).long(), y)[0], "torch")
+    assert abs(l1 - l2) < 2e-2
+    bad = [(n, _rel(g1[n], g2[n])) for n in g2 if _rel(g1[n], g2[n]) > 0.1]
+    assert not bad, bad
+
+
+def test_vgg16_step(gpu):
+    from pcmp.models.vgg import vgg16_transfer
+    from pcmp.ops import cross_entropy
+    torch.manual_seed(0)
+    m = vgg16_transfer().to(gpu).train()
+    x = torch.rand(2, 3, 224, 224, device=gpu)
+    y = torch.randint(0, 10, (2,), device=gpu)
+    l1, g1 = _grads(m, lambda: cross_entropy(m.forward_logits(x), y), "hip")
+    l2, g2 = _grads(m, lambda: cross_entropy(m.forward_logits(x), y), "torch")
+    assert set(g1) == {n for n, p in m.named_parameters() if p.requires_grad}
+    assert abs(l1 - l2) < 5e-2 * max(1, abs(l2))
+    for n in g2:
+        assert _rel(g1[n], g2[n]) < 0.15, n
