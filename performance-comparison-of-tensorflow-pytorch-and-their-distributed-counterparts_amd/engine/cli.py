@@ -1,0 +1,79 @@
+"""Shared CLI plumbing for the entry points (SURVEY §5.6 config/flag system).
+
+Every reference constant becomes a flag whose default is the reference value;
+``--preset`` selects the BASELINE.json configs; ``--local_rank`` (legacy launcher) and
+``LOCAL_RANK`` (torchrun) are both honoured; ``--synthetic`` (default) vs ``--data-dir``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+PRESETS = {
+    # BASELINE.json configs
+    "mlp-cpu": dict(model="mlp", device="cpu", epochs=1, batch_size=64),
+    "resnet18-1gpu": dict(model="resnet18", full_train=True, epochs=1, batch_size=256),
+    "resnet50-ddp8": dict(model="resnet50", full_train=True, epochs=1, batch_size=256),
+    "resnet50-tl-infer": dict(model="resnet50", epochs=1, batch_size=64, num_images=1000),
+    "bilstm-ddp8": dict(model="bilstm", epochs=3, batch_size=32),
+    "bert-distr": dict(model="bert", epochs=3, batch_size=32),
+}
+
+
+def common_parser(desc):
+    ap = argparse.ArgumentParser(description=desc)
+    ap.add_argument("--local_rank", "--local-rank", type=int, default=None)
+    ap.add_argument("--preset", choices=sorted(PRESETS), default=None)
+    ap.add_argument("--device", choices=["auto", "cpu", "cuda"], default="auto")
+    ap.add_argument("--synthetic", action="store_true", default=True)
+    ap.add_argument("--data-dir", default=None, help="real dataset path (overrides --synthetic)")
+    ap.add_argument("--epochs", type=int, default=None)
+    ap.add_argument("--batch-size", type=int, default=None)
+    ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--kernels", choices=["hip", "torch"], default="hip",
+                    help="torch = PyTorch reference ops (parity runs only)")
+    ap.add_argument("--json", default=None, help="append a JSON metrics record to this file")
+    ap.add_argument("--profile", default=None, help="torch.profiler chrome trace path")
+    ap.add_argument("--reference-compat", action="store_true",
+                    help="reproduce the reference's printed-value quirks (SURVEY §0.2)")
+    ap.add_argument("--verbose", action="store_true", help="per-step prints (reference behaviour)")
+    ap.add_argument("--watchdog", type=float, default=0.0, help="hang watchdog timeout (s), 0=off")
+    return ap
+
+
+def apply_preset(args, defaults: dict):
+    d = dict(defaults)
+    if args.preset:
+        d.update(PRESETS[args.preset])
+    for k, v in d.items():
+        if getattr(args, k, None) is None:
+            setattr(args, k, v)
+    return args
+
+
+def setup(args):
+    import torch
+
+    import pcmp  # noqa: F401
+    from ..ops import _lib
+    from ..parallel import launch
+    from ..utils.misc import seed_everything
+    _lib.set_backend(args.kernels)
+    use_gpu = torch.cuda.is_available() if args.device == "auto" else args.device == "cuda"
+    env = launch.init(args.local_rank, use_gpu=use_gpu)
+    seed_everything(args.seed + (0 if args.kernels else 0))
+    return env
+
+
+def write_json(args, record):
+    from ..utils.report import emit_json, is_main
+    emit_json(record)
+    if args.json and is_main():
+        with open(args.json, "a") as f:
+            f.write(json.dumps(record, default=float) + "\n")
+
+
+def env_info():
+    return {"world_size": int(os.environ.get("WORLD_SIZE", "1")), "rank": int(os.environ.get("RANK", "0"))}

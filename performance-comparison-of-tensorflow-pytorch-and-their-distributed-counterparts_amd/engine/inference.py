@@ -1,0 +1,98 @@
+"""Inference engine (E1-E5) — batch-1 latency with hipGraph replay.
+
+The reference's ``predict_image`` loop (pytorch_training_inference_on_image.ipynb:855-905,
+another_neural_net.py:180-217) does, per image: transform -> unsqueeze -> ``.to(device)`` ->
+``model(input)`` -> ``.cpu().numpy().argmax()``, and prints only the total
+("Inference time is X seconds").  Here:
+  * ``Batch1Predictor`` captures the eval-mode forward at batch 1 into a hipGraph once (static
+    input buffer; every kernel of the forward replays from one graph launch, so per-image latency
+    is not host-launch bound), then per image: H2D copy into the static buffer, graph replay,
+    argmax on device, one D2H of the index (the reference's host round trip is kept);
+  * ``infer_batch1`` times the whole loop (the reference string) AND records per-image latency
+    (p50/p90/p99) with a device sync per image;
+  * ``predict_topk`` — the single-image sanity prediction (E3) with softmax percentages
+    (x100; the reference's x1000 in one notebook is a bug).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..utils import report as R
+
+
+def _logits(model, x):
+    return model.forward_logits(x) if hasattr(model, "forward_logits") else model(x)
+
+
+class Batch1Predictor:
+    def __init__(self, model, example: torch.Tensor, use_graph=True, warmup=3):
+        self.model = model.eval()
+        self.device = example.device
+        self.static_in = example.clone()
+        self.graph = None
+        self.use_graph = use_graph and self.device.type == "cuda"
+        with torch.no_grad():
+            for _ in range(warmup):
+                self.static_out = _logits(model, self.static_in).argmax(1)
+            if self.use_graph:
+                torch.cuda.synchronize()
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    for _ in range(2):
+                        self.static_out = _logits(model, self.static_in).argmax(1)
+                torch.cuda.current_stream().wait_stream(s)
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self.static_out = _logits(model, self.static_in).argmax(1)
+                torch.cuda.synchronize()
+
+    @torch.no_grad()
+    def __call__(self, x_host_or_dev: torch.Tensor) -> int:
+        self.static_in.copy_(x_host_or_dev, non_blocking=True)
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.static_out = _logits(self.model, self.static_in).argmax(1)
+        return int(self.static_out.item())
+
+
+def infer_batch1(model, images: torch.Tensor, labels=None, device=None, use_graph=True, print_every_image=False,
+                 printer=R.rprint):
+    """images: [N,3,H,W] (host or device).  Returns (total_seconds, stats dict, predictions)."""
+    device = device or next(model.parameters()).device
+    pred = Batch1Predictor(model, images[:1].to(device), use_graph=use_graph)
+    lat, preds = [], []
+    t1 = time.time()
+    for ii in range(images.shape[0]):
+        if print_every_image:
+            printer(ii + 1)
+        ts = time.perf_counter()
+        idx = pred(images[ii:ii + 1])
+        lat.append(time.perf_counter() - ts)
+        preds.append(idx)
+    total = time.time() - t1
+    printer(R.inference_time_line(total))
+    stats = R.latency_stats(lat)
+    if labels is not None:
+        lab = labels.tolist() if hasattr(labels, "tolist") else list(labels)
+        stats["accuracy"] = sum(int(a == b) for a, b in zip(preds, lab)) / max(1, len(lab))
+    stats["images_per_sec"] = images.shape[0] / total
+    stats["graph"] = pred.graph is not None
+    return total, stats, preds
+
+
+@torch.no_grad()
+def predict_topk(model, x: torch.Tensor, labels: dict | list | None = None, k=5):
+    """E3: softmax percentages of the top-k classes for one preprocessed image [1,3,H,W]."""
+    model.eval()
+    z = _logits(model, x).float()
+    pct = torch.softmax(z, dim=1)[0] * 100
+    vals, idx = torch.sort(pct, descending=True)
+    out = []
+    for v, i in zip(vals[:k].tolist(), idx[:k].tolist()):
+        name = labels[i] if labels is not None and i in (labels if isinstance(labels, dict) else range(len(labels))) else i
+        out.append((name, v))
+    return out

@@ -22,11 +22,12 @@ CAFFE_MEAN_BGR = (103.939, 116.779, 123.68)
 
 
 class KerasResNet50TL(nn.Module):
-    def __init__(self, num_classes=10, compute_dtype=None):
+    def __init__(self, num_classes=10, compute_dtype=None, image_size=224):
         super().__init__()
         self.backbone = ResNet("resnet50", 1000, variant="keras", compute_dtype=compute_dtype)
         self.backbone.fc = nn.Identity()
-        self.dense = Linear(7 * 7 * 2048, num_classes)   # "transfer_lr" Dense
+        fm = (image_size + 31) // 32                       # 7 at 224
+        self.dense = Linear(fm * fm * 2048, num_classes)  # "transfer_lr" Dense (100,352 inputs at 224)
         self.num_classes = num_classes
 
     def forward_logits(self, x):
