@@ -66,6 +66,7 @@ class Conv2d(nn.Module):
     def __init__(self, cin, cout, k, stride=1, pad=0, bias=True, relu=False, cin_pad=None):
         super().__init__()
         cin_p = cin_pad or cin
+        self.cin = cin
         self.R = self.S = k
         self.stride, self.pad, self.relu = stride, pad, relu
         w = torch.empty(cout, cin, k, k)

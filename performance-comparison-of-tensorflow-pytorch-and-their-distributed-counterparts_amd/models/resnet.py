@@ -24,7 +24,7 @@ from torch import nn
 
 from ..ops.conv_blocks import ResidualBlockFn, StemFn
 from ..ops.kernels import K
-from .layers import ConvBN, GlobalAvgPool, Linear, MLPHead
+from .layers import Conv2d, ConvBN, GlobalAvgPool, Linear, MLPHead
 
 STEM_CIN_PAD = 8
 
@@ -202,7 +202,7 @@ def count_params(model, logical=True):
             n = p.numel()
             if logical and isinstance(mod, Linear):
                 n = n // mod.out_pad * mod.out_features if name == "weight" else mod.out_features
-            elif logical and isinstance(mod, ConvBN) and name == "weight" and p.shape[-1] != mod.cin:
+            elif logical and isinstance(mod, (ConvBN, Conv2d)) and name == "weight" and p.shape[-1] != mod.cin:
                 n = n // p.shape[-1] * mod.cin
             total += n
     return total

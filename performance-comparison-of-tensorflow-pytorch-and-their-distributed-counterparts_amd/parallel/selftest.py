@@ -1,0 +1,77 @@
+"""Multi-process DDP self-tests (CPU/gloo or GPU/RCCL) used by tests/ and tools/.
+
+``ddp_equivalence_worker``: every rank trains the same model on its shard of a global batch with
+the framework's flat-bucket DDP; the gradient after all-reduce averaging must equal the
+single-process gradient on the concatenated batch, and parameters must stay identical across
+ranks after several optimizer steps ("DDP grads == single-process grads on the
+concatenated batch").
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def _build(kind, seed=0):
+    torch.manual_seed(seed)
+    if kind == "mlp":
+        from ..models.layers import MLPHead
+        return MLPHead(64, 128, 5, p=0.0)
+    if kind == "bilstm":
+        from ..models.bilstm import BiLSTMClassifier
+        return BiLSTMClassifier(300, 32, 16, 1, 2, 0.0)
+    raise ValueError(kind)
+
+
+def _batch(kind, n, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    if kind == "mlp":
+        return torch.randn(n, 64, generator=g), torch.randint(0, 5, (n,), generator=g)
+    ids = torch.randint(1, 300, (n, 10), generator=g)
+    ids[::3, 6:] = 0
+    return ids, torch.randint(0, 2, (n,), generator=g)
+
+
+def _loss(model, kind, x, y):
+    from ..ops import cross_entropy
+    return cross_entropy(model.forward_logits(x), y)
+
+
+def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.01):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from .. import optim
+    from ..utils.flat import FlatParams
+    from .ddp import DistributedDataParallel
+    model = _build(kind, seed=rank)              # different init per rank: DDP must broadcast rank 0's
+    flat = FlatParams(model.parameters(), shadow_dtype=None)
+    ddp = DistributedDataParallel(model, flat, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
+    opt = optim.SGD(flat, lr=0.05, momentum=0.9)
+    opt.set_grad_scale(ddp.grad_scale())
+    N = 8 * world
+    x, y = _batch(kind, N)
+    shard = slice(rank * 8, (rank + 1) * 8)
+    # reference: single-process gradient on the full batch with rank 0's initial weights
+    ref = _build(kind, seed=0)
+    rflat = FlatParams(ref.parameters(), shadow_dtype=None)
+    rflat.zero_grad()
+    _loss(ref, kind, x, y).backward()
+    ref_grad = rflat.grad.clone()
+    opt.zero_grad()
+    _loss(model, kind, x[shard], y[shard]).backward()
+    ddp.finish_gradient_sync()
+    avg = flat.grad * ddp.grad_scale()
+    ok_grad = torch.allclose(avg, ref_grad, atol=1e-5, rtol=1e-4)
+    for _ in range(3):
+        opt.step()
+        opt.zero_grad()
+        _loss(model, kind, x[shard], y[shard]).backward()
+        ddp.finish_gradient_sync()
+    gathered = [torch.zeros_like(flat.master) for _ in range(world)]
+    dist.all_gather(gathered, flat.master)
+    ok_sync = all(torch.equal(gathered[0], g) for g in gathered)
+    torch.save({"ok_grad": ok_grad, "ok_sync": ok_sync, "nbuckets": len(ddp.buckets),
+                "maxdiff": float((avg - ref_grad).abs().max())}, os.path.join(out_dir, f"rank{rank}.pt"))
+    dist.destroy_process_group()

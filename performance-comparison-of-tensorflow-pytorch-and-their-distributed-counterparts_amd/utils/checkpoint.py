@@ -30,7 +30,8 @@ def _atomic_save(obj, path):
 
 
 def rng_state():
-    st = {"torch": torch.get_rng_state(), "numpy": np.random.get_state()[1].copy(),
+    st = {"torch": torch.get_rng_state(),
+          "numpy": torch.from_numpy(np.random.get_state()[1].astype(np.int64)),
           "python": repr(random.getstate())}
     if torch.cuda.is_available():
         st["cuda"] = torch.cuda.get_rng_state_all()

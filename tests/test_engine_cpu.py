@@ -1,0 +1,128 @@
+"""Engine / entry points / checkpoint / text pipeline on CPU (tiny synthetic configs)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import pcmp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(script, *args, timeout=600):
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, script), "--device", "cpu", *args], capture_output=True,
+                       text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def _last_json(out):
+    for line in reversed(out.strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError("no JSON record")
+
+
+def test_another_neural_net_resnet_tl():
+    out = _run("another_neural_net.py", "--model", "resnet50", "--train-size", "24", "--image-size", "64",
+               "--batch-size", "8", "--epochs", "1", "--num-images", "3")
+    assert "No GPU. switching to CPU" in out
+    assert "trainloader done" in out and "Epoch 1/1.. Train loss:" in out
+    assert "Training time per epoch is" in out and "Inference time is" in out
+    rec = _last_json(out)
+    assert rec["batch1_latency"]["n"] == 3 and "p50_ms" in rec["batch1_latency"]
+
+
+def test_mlp_cpu_preset():
+    out = _run("another_neural_net.py", "--preset", "mlp-cpu")
+    assert "Training time per epoch is" in out
+
+
+def test_text_bert_entrypoint():
+    out = _run("pytorch_on_language_distr.py", "--model", "bert", "--layers", "1", "--train-size", "40",
+               "--test-size", "16", "--epochs", "1", "--batch-size", "8")
+    for s in ("======== Epoch 1 / 1 ========", "Training...", "  Average training loss:", "  Training epcoh took:",
+              "Running Validation...", "  Validation took:", "Training complete!", "  Test took:"):
+        assert s in out, s
+
+
+def test_keras_counterpart_entrypoint():
+    out = _run("resnet.py", "--train-size", "8", "--val-size", "8", "--image-size", "64", "--batch-size", "8",
+               "--epochs", "1")
+    assert "the inference takes" in out
+
+
+def test_notebook_flow_save_reload_infer(tmp_path):
+    out = _run("pytorch_training_inference.py", "--models", "resnet50", "--train-size", "24", "--image-size", "64",
+               "--batch-size", "8", "--num-images", "2", "--save-dir", str(tmp_path))
+    assert "Saving Model" in out and "Inference time is" in out
+    assert (tmp_path / "resnet50_model.pt").exists()
+
+
+def test_standalone_inference_entrypoint():
+    out = _run("standalone_inference.py", "--models", "pt-resnet50,keras-resnet50", "--num-images", "2",
+               "--image-size", "64")
+    assert out.count("Inference Time is:") == 2
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    from pcmp.models.resnet import resnet18
+    from pcmp.optim import SGD
+    from pcmp.utils.checkpoint import load_checkpoint, load_model, save_checkpoint, save_model
+    from pcmp.utils.flat import FlatParams
+    m = resnet18(10)
+    flat = FlatParams(m.parameters(), shadow_dtype=None)
+    opt = SGD(flat, lr=0.01, momentum=0.9)
+    from pcmp.ops import cross_entropy
+    cross_entropy(m.forward_logits(torch.rand(4, 3, 32, 32)), torch.tensor([0, 1, 2, 3])).backward()
+    opt.step()
+    save_checkpoint(str(tmp_path / "c.pt"), m, opt, epoch=3)
+    m2 = resnet18(10)
+    flat2 = FlatParams(m2.parameters(), shadow_dtype=None)
+    opt2 = SGD(flat2, lr=0.5, momentum=0.9)
+    ep, _ = load_checkpoint(str(tmp_path / "c.pt"), m2, opt2)
+    assert ep == 3 and opt2.lr == 0.01 and torch.equal(flat.master, flat2.master) and torch.equal(opt.mom, opt2.mom)
+    save_model(str(tmp_path / "m.pt"), m, {"builder": "pcmp.models.resnet:resnet18", "kwargs": {"num_classes": 10}})
+    m3 = load_model(str(tmp_path / "m.pt")).eval()
+    m.eval()
+    x = torch.rand(1, 3, 32, 32)
+    assert torch.allclose(m.forward_logits(x), m3.forward_logits(x))
+
+
+def test_native_text_pipeline_matches_python():
+    from pcmp.data import imdb
+    texts = ["This movie was GREAT!!<br /><br />Loved it, 10/10.", "bad.", "Unseenwordxyz and the end",
+             "a " * 300, ""]
+    vocab = imdb.build_vocab(texts + ["movie great loved the end and a bad"], size=400)
+    ids_n, m_n = imdb.encode(texts, vocab, 16)
+    ids_p, m_p = imdb.encode(texts, vocab, 16, force_python=True)
+    assert torch.equal(ids_n, ids_p) and torch.equal(m_n, m_p)
+    assert ids_n[0, 0].item() == 101 and (ids_n[3] > 0).all()        # [CLS] ... truncated to 16
+    assert ids_n[1].tolist()[:4] == [101, vocab.index("bad"), vocab.index("."), 102]
+    assert ids_n[4].tolist()[:3] == [101, 102, 0]
+    assert torch.equal(m_n, (ids_n > 0).long())
+
+
+def test_rm_tags_and_csv_reader(tmp_path):
+    from pcmp.data import imdb
+    assert imdb.rm_tags("a<br />b<i>c</i>") == "a b c "
+    p = tmp_path / "IMDB Dataset.csv"
+    p.write_text('review,sentiment\n"Good <br/>film",positive\n"Awful",negative\n')
+    texts, labels = imdb.read_files(str(p))
+    assert list(labels) == [1, 0] and "<" not in texts[0]
+
+
+def test_synthetic_datasets_shapes():
+    from pcmp.data.synthetic import BatchLoader, SyntheticIMDB, SyntheticImages
+    ds = SyntheticImages(100, 10, 32)
+    x, y = ds.get_batch([0, 5, 7])
+    assert x.shape == (3, 3, 32, 32) and 0 <= x.min() and x.max() <= 1 and y.max() < 10
+    assert torch.equal(ds.labels(torch.tensor([5])), ds.labels(torch.tensor([5])))
+    t = SyntheticIMDB(50)
+    ids, mask, lab = t.get_batch(list(range(50)))
+    assert ids.shape == (50, 128) and (ids[:, 0] == 101).all() and torch.equal(mask, (ids > 0).long())
+    assert len(BatchLoader(ds, 32)) == 4

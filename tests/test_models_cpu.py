@@ -1,0 +1,135 @@
+"""Model parity on CPU (framework model on the reference-op path vs stock torch.nn / HF)."""
+import pytest
+import torch
+
+import pcmp
+from pcmp.ops import cross_entropy
+
+
+def _rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-20)).item()
+
+
+def test_resnet18_matches_torch_nn():
+    from pcmp.models.resnet import resnet18
+    from pcmp.models.torch_ref import TorchResNet
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).train()
+    t = TorchResNet("resnet18", 10).train().load_from_pcmp(m)
+    x, y = torch.randn(4, 3, 64, 64), torch.randint(0, 10, (4,))
+    l = cross_entropy(m.forward_logits(x), y)
+    l.backward()
+    lt = torch.nn.functional.cross_entropy(t(x), y)
+    lt.backward()
+    assert abs(l.item() - lt.item()) < 1e-4
+    assert _rel(m.stem.conv.weight.grad[..., :3].permute(0, 3, 1, 2), t.conv1.weight.grad) < 1e-3
+    assert _rel(m.layer3[0].downsample.weight.grad.permute(0, 3, 1, 2), t.layer3[0].downsample[0].weight.grad) < 1e-3
+    assert torch.allclose(m.stem.conv.running_mean, t.bn1.running_mean, atol=1e-5)
+
+
+@pytest.mark.parametrize("cin,planes,stride", [(64, 64, 1), (256, 128, 2)])
+def test_bottleneck_matches_torch(cin, planes, stride):
+    from pcmp.models.resnet import Bottleneck
+    from pcmp.models.torch_ref import TBottleneck
+    torch.manual_seed(0)
+    b, t = Bottleneck(cin, planes, stride).train(), TBottleneck(cin, planes, stride).train()
+    with torch.no_grad():
+        for nm, L in zip("123", b.main_layers()):
+            getattr(t, "conv" + nm).weight.copy_(L.weight.permute(0, 3, 1, 2))
+        t.downsample[0].weight.copy_(b.downsample.weight.permute(0, 3, 1, 2))
+    x = torch.randn(2, cin, 8, 8)
+    xp = x.permute(0, 2, 3, 1).contiguous().requires_grad_(True)
+    xt = x.clone().requires_grad_(True)
+    y, yt = b(xp), t(xt)
+    g = torch.randn_like(yt)
+    y.backward(g.permute(0, 2, 3, 1))
+    yt.backward(g)
+    assert torch.allclose(y.permute(0, 3, 1, 2), yt, atol=1e-4)
+    assert _rel(xp.grad.permute(0, 3, 1, 2), xt.grad) < 1e-4
+    assert _rel(b.conv2.weight.grad.permute(0, 3, 1, 2), t.conv2.weight.grad) < 1e-4
+
+
+def test_resnet50_param_count_matches_torchvision():
+    from pcmp.models.resnet import count_params, resnet50, resnet50_transfer
+    assert count_params(resnet50()) == 25557032          # torchvision figure
+    m = resnet50_transfer()
+    head = sum(p.numel() for p in m.fc.parameters())
+    assert count_params(m.fc) == 1054218
+    assert all(not p.requires_grad for n, p in m.named_parameters() if not n.startswith("fc."))
+    assert head >= 1054218
+
+
+def test_vgg16_param_count():
+    from pcmp.models.resnet import count_params
+    from pcmp.models.vgg import vgg16, vgg16_transfer
+    assert count_params(vgg16()) == 138357544            # torchvision VGG16
+    assert count_params(vgg16_transfer()) == 135311946    # SURVEY §2.4.2 (TL head 1,051,402)
+
+
+def test_bilstm_matches_torch_lstm():
+    from pcmp.models.bilstm import BiLSTMClassifier, TorchBiLSTM
+    torch.manual_seed(0)
+    t = TorchBiLSTM(500, 32, 16, 2, 2, 0.0)
+    m = BiLSTMClassifier(500, 32, 16, 2, 2, 0.0).load_torch_lstm(t.embedding, t.lstm, t.fc)
+    ids = torch.randint(1, 500, (4, 12))
+    for i, l in enumerate([12, 7, 3, 1]):
+        ids[i, l:] = 0
+    y = torch.randint(0, 2, (4,))
+    l = cross_entropy(m.forward_logits(ids), y)
+    l.backward()
+    lt = torch.nn.functional.cross_entropy(t(ids), y)
+    lt.backward()
+    assert abs(l.item() - lt.item()) < 1e-5
+    assert _rel(m.layers[0].w_hh.grad[1], t.lstm.weight_hh_l0_reverse.grad) < 1e-4
+    assert _rel(m.embedding.weight.grad, t.embedding.weight.grad) < 1e-4
+
+
+def test_bert_matches_hf():
+    transformers = pytest.importorskip("transformers")
+    from pcmp.models.bert import BertConfig, BertForSequenceClassification
+    torch.manual_seed(0)
+    kw = dict(num_hidden_layers=2, hidden_size=64, num_attention_heads=1, intermediate_size=128)
+    hf = transformers.BertForSequenceClassification(transformers.BertConfig(num_labels=2, hidden_dropout_prob=0.0,
+                                                                            attention_probs_dropout_prob=0.0, **kw))
+    m = BertForSequenceClassification(BertConfig(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0, **kw)).load_hf(hf)
+    ids = torch.randint(1, 30522, (2, 32))
+    ids[1, 10:] = 0
+    y = torch.tensor([0, 1])
+    out = hf(ids, attention_mask=(ids > 0).long(), labels=y)
+    loss, logits = m(ids, None, (ids > 0).long(), y)
+    assert torch.allclose(logits, out.logits, atol=1e-5)
+    out.loss.backward()
+    loss.backward()
+    sd = dict(hf.named_parameters())
+    assert _rel(m.layers[1].ffn1.weight.grad, sd["bert.encoder.layer.1.intermediate.dense.weight"].grad) < 1e-4
+
+
+def test_bert_base_param_count():
+    from pcmp.models.bert import bert_base
+    from pcmp.models.resnet import count_params
+    assert count_params(bert_base()) == 109483778
+
+
+def test_keras_resnet_and_mlp_head_shapes():
+    from pcmp.models.keras_resnet import KerasResNet50TL
+    from pcmp.models.layers import MLPHead
+    m = KerasResNet50TL(10, image_size=64)
+    p = m(torch.rand(2, 3, 64, 64))
+    assert p.shape == (2, 10) and torch.allclose(p.sum(1), torch.ones(2), atol=1e-5)
+    h = MLPHead(2048, 512, 10, 0.2).eval()
+    out = h(torch.randn(3, 2048))
+    assert torch.allclose(out.exp().sum(1), torch.ones(3), atol=1e-5)
+
+
+def test_resnet_eval_mode_uses_running_stats():
+    from pcmp.models.resnet import resnet18
+    from pcmp.models.torch_ref import TorchResNet
+    torch.manual_seed(0)
+    m = resnet18(10).train()
+    for _ in range(2):
+        m.forward_logits(torch.randn(4, 3, 32, 32))
+    t = TorchResNet("resnet18", 10).load_from_pcmp(m).eval()
+    m.eval()
+    x = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        assert torch.allclose(m.forward_logits(x), t(x), atol=1e-4)

@@ -1,0 +1,88 @@
+"""CPU tests of the reference op layer, the dispatcher, FastDiv, RNG and the host parts."""
+import pytest
+import torch
+
+import pcmp
+from pcmp.ops import K, _lib, ref
+
+
+def test_dispatch_cpu_uses_reference():
+    x = torch.randn(2, 5, 5, 8)
+    w = torch.randn(16, 3, 3, 8)
+    y = K.conv_fwd(x, w, 1, 1, None, None, True, False)[0]
+    yr = torch.relu(torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), padding=1)).permute(0, 2, 3, 1)
+    assert torch.allclose(y, yr, atol=1e-5)
+
+
+def test_native_library_builds_and_registers_ops():
+    assert _lib.LIB_PATH.exists(), "run __graft_entry__.build() first"
+    assert _lib.load(), _lib.load_error()
+    for name in ("conv_fwd", "conv_dgrad", "conv_wgrad", "bn_finalize", "lstm_seq_fwd", "attention_fwd",
+                 "sgd_flat", "adam_flat", "text_encode", "layernorm_fwd", "embedding_fwd"):
+        assert hasattr(torch.ops.pcmp, name), name
+
+
+def test_gpu_tensor_without_native_raises(monkeypatch):
+    class FakeT:
+        is_cuda = True
+    monkeypatch.setattr(_lib, "_loaded", False)
+    monkeypatch.setattr(_lib, "LIB_PATH", _lib.LIB_PATH.parent / "missing.so")
+    monkeypatch.setattr(_lib, "_backend", "hip")
+    with pytest.raises(RuntimeError, match="Refusing to fall back"):
+        _lib.use_native(FakeT())
+
+
+def _fastdiv(d):
+    s = 0
+    while (1 << s) < d:
+        s += 1
+    m = ((1 << 32) * ((1 << s) - d)) // d + 1
+    return m & 0xFFFFFFFF, s
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 14, 28, 49, 56, 112, 196, 784, 3136, 12544, 50176])
+def test_fastdiv_formula(d):
+    m, s = _fastdiv(d)
+    import random
+    vals = [0, 1, d - 1, d, d + 1, 2 ** 31 - 1] + [random.randrange(0, 2 ** 31) for _ in range(2000)]
+    for n in vals:
+        t = (n * m) >> 32
+        assert (t + n) >> s == n // d, (n, d)
+
+
+def test_hash_rng_uniform():
+    u = ref.hash_uniform(123, torch.arange(100000))
+    assert 0.49 < u.mean().item() < 0.51 and u.min() >= 0 and u.max() < 1
+    assert torch.equal(u, ref.hash_uniform(123, torch.arange(100000)))
+    assert not torch.equal(u, ref.hash_uniform(124, torch.arange(100000)))
+
+
+def test_bn_reference_roundtrip_vs_autograd():
+    torch.manual_seed(0)
+    x = torch.randn(64, 16) * 3 + 1
+    g, b = torch.rand(16) + 0.5, torch.randn(16)
+    part = ref.bn_partials(x)
+    mean, invstd, sc, sh = ref.bn_finalize(part, 64, g, b, None, None, 0.1, 1e-5)
+    y = ref.bn_apply(x, sc, sh, None, None, None, True)
+    xt = x.clone().requires_grad_(True)
+    gt, bt = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yt = torch.relu(torch.nn.functional.batch_norm(xt, None, None, gt, bt, True, 0.1, 1e-5))
+    assert torch.allclose(y, yt, atol=1e-5)
+    dy = torch.randn_like(x)
+    yt.backward(dy)
+    p = ref.bn_bwd_reduce(dy, y, x, mean, invstd)[0]
+    dg, db = torch.zeros(16), torch.zeros(16)
+    coef = ref.bn_bwd_finalize(p, 64, g, mean, invstd, dg, db, False)
+    dx = ref.bn_bwd_apply(dy, y, x, coef)[0]
+    assert torch.allclose(dx, xt.grad, atol=1e-5)
+    assert torch.allclose(dg, gt.grad, atol=1e-4) and torch.allclose(db, bt.grad, atol=1e-4)
+
+
+def test_maxpool_reference_idx_roundtrip():
+    x = torch.randn(2, 9, 9, 8)
+    y, idx = ref.maxpool_fwd(x, 3, 2, 1, True)
+    xt = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    yt = torch.nn.functional.max_pool2d(xt, 3, 2, 1)
+    dy = torch.randn_like(y)
+    yt.backward(dy.permute(0, 3, 1, 2))
+    assert torch.allclose(ref.maxpool_bwd(dy, idx, 9, 9, 3, 2, 1), xt.grad.permute(0, 2, 3, 1), atol=1e-6)
