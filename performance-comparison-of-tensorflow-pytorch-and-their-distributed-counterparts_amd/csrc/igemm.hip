@@ -56,6 +56,7 @@ struct IgemmParams {
   // DGRAD decode: rows m -> (n, hh, ww) over [N][dH][dW]; h = hh*ostep + oph (sub-pixel class)
   int dH, dW, offy, offx, sub, oph, opw;
   int relu;
+  unsigned a_bytes, b_bytes;   // buffer-resource extents of a / b (hardware OOB -> zero)
   int ksplit;       // K elements per split (multiple of BK)
   int nsplit;
   int tiles_m, tiles_n;
@@ -97,7 +98,31 @@ __device__ __forceinline__ int tr_off(int row, int col) {  // byte offset of ele
   return row * RB + (chunk << 4) + ((col & 7) << 1);
 }
 
-template <int MODE, int BM, int BN, int WM, int WN>
+// Buffer resource over a whole tensor: loads at out-of-range byte offsets return ZERO (hardware
+// range check), which implements conv zero-padding and tile tails without selects or branches.
+constexpr unsigned kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, unsigned voff) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0);
+  return uint4{v[0], v[1], v[2], v[3]};
+}
+
+// LDS row rho of the B tile holds output channel chan_perm(rho): within each group of 32 rows,
+// rho = 16jj + 4q + e  ->  8q + 4jj + e  (so MFMA tile pair (2jp, 2jp+1), lane group q, element e
+// maps to channel 32jp + 8q + 4jj + e).
+template <bool PAIR>
+__device__ __forceinline__ int chan_perm(int rho) {
+  if constexpr (!PAIR) return rho;
+  return (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
+}
+
+// UNIF: the A source channel count (C for FWD, K for DGRAD) is a multiple of BK, so the 8 16-B
+// chunks of a K-step share one filter tap (r,s) and a block-uniform channel base c0: per K-step
+// the address update is one uniform scalar offset plus one add per row.
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF>
 __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -126,59 +151,79 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   const int kend = min(p.gk, kbeg + p.ksplit);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
-  f32x4 acc[TM][TN];
+  // FWD/DGRAD compute D^T tiles (weights as the MFMA A operand) so each lane ends up holding 4
+  // consecutive output channels of one pixel -> direct 8-byte stores, no LDS staging.
+  // PAIR: output-channel permutation inside each 32-channel group of the B (weight) tile so that a
+  // lane's two MFMA column tiles 2jp, 2jp+1 hold 8 CONSECUTIVE channels -> 16-B epilogue stores.
+  constexpr bool PAIR = MODE != MODE_WGRAD && (TN % 2 == 0);
+  constexpr int AT0 = (MODE == MODE_WGRAD) ? TM : TN;
+  constexpr int AT1 = (MODE == MODE_WGRAD) ? TN : TM;
+  f32x4 acc[AT0][AT1];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < AT0; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < AT1; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[NVA], rb[NVB];
 
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+
   // ---- per-thread loader state ----------------------------------------------------------------
-  // FWD / DGRAD: thread owns rows (tid>>3)+32*i of the A and B tiles and k-chunk (tid&7).
   const int lchunk = tid & 7;
   const int lrow = tid >> 3;
-  // A rows
-  int a_valid[NVA];
-  int a_base[NVA];   // element offset of (n) image base
-  int a_y[NVA], a_x[NVA];  // FWD: p*st-pad, q*st-pad ; DGRAD: h+pad, w+pad
-  // WGRAD: tile A' [BK][BM] rows = reduction index m, cols = co; tile B' [BK][BN] cols = j
-  constexpr int CPR_A = BM / 8, CPR_B = BN / 8;       // 16-B chunks per WGRAD tile row
+  int a_off[NVA];            // FWD/DGRAD: element offset of row's (tap 0) base; WGRAD unused
+  int a_y[NVA], a_x[NVA];    // bounds coordinates (invalid rows get a huge negative a_y)
+  int b_off[NVB];            // FWD/DGRAD: n*gk (or -1 for n >= gn)
+  constexpr int CPR_A = BM / 8, CPR_B = BN / 8;
   int wa_col = 0, wb_col = 0;
   int wb_r = 0, wb_s = 0, wb_c = 0, wb_ok = 0;
-  // k -> (r, s, c) incremental state for FWD/DGRAD (chunk fixed per thread)
-  int kr = 0, ks = 0, kc = 0;
-  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;  // innermost channel of the A source
+  int kr = 0, ks = 0, kc = 0;     // tap / channel state (uniform when UNIF)
+  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
 
   if constexpr (MODE != MODE_WGRAD) {
 #pragma unroll
     for (int i = 0; i < NVA; ++i) {
       const int m = m0 + lrow + 32 * i;
-      a_valid[i] = m < p.gm;
-      const int mm = a_valid[i] ? m : 0;
+      const bool v = m < p.gm;
+      const int mm = v ? m : 0;
       if constexpr (MODE == MODE_FWD) {
         const int n = fdiv(mm, p.fd_PQ);
         const int rem = mm - n * p.P * p.Q;
         const int pp = fdiv(rem, p.fd_Q);
         const int qq = rem - pp * p.Q;
-        a_base[i] = n * p.H * p.W * p.C;
-        a_y[i] = pp * p.stride - p.pad;
+        const int yv = pp * p.stride - p.pad;
+        a_y[i] = v ? yv : -(1 << 28);
         a_x[i] = qq * p.stride - p.pad;
+        a_off[i] = ((n * p.H + yv) * p.W + a_x[i]) * p.C;
       } else {
         const int n = fdiv(mm, p.fd_HW);
         const int rem = mm - n * p.dH * p.dW;
         const int hh = fdiv(rem, p.fd_W);
         const int ww = rem - hh * p.dW;
-        a_base[i] = n * p.P * p.Q * p.K;
-        a_y[i] = hh + p.offy;
+        const int yv = hh + p.offy;
+        a_y[i] = v ? yv : -(1 << 28);
         a_x[i] = ww + p.offx;
+        a_off[i] = ((n * p.P + yv) * p.Q + a_x[i]) * p.K;
       }
     }
-    const int k = kbeg + lchunk * 8;
-    kc = k % CIN;
-    const int rs = k / CIN;
-    ks = rs % p.S;
-    kr = rs / p.S;
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int n = n0 + chan_perm<PAIR>(lrow + 32 * i);
+      b_off[i] = n < p.gn ? n * p.gk : -1;
+    }
+    if constexpr (UNIF) {
+      kc = kbeg % CIN;
+      const int rs = kbeg / CIN;
+      ks = rs % p.S;
+      kr = rs / p.S;
+    } else {
+      const int k = kbeg + lchunk * 8;
+      kc = k % CIN;
+      const int rs = k / CIN;
+      ks = rs % p.S;
+      kr = rs / p.S;
+    }
   } else {
     wa_col = (tid % CPR_A) * 8;
     wb_col = (tid % CPR_B) * 8;
@@ -194,41 +239,55 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   auto load_stage = [&](int kt) {
     const int k0 = kbeg + kt * BK;
     if constexpr (MODE != MODE_WGRAD) {
-      const int k = k0 + lchunk * 8;
-      const bool kok = k < kend;
+      int tap, chan;
+      if constexpr (UNIF) {
+        chan = kc + lchunk * 8;
+        if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C;
+        else tap = -(kr * p.Q + ks) * p.K;
+      } else {
+        chan = kc;
+        if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C;
+        else tap = -(kr * p.Q + ks) * p.K;
+      }
+      const bool kok = UNIF ? true : (k0 + lchunk * 8 < kend);
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
-        int yy, xx;
-        bool ok = a_valid[i] && kok;
-        int off;
+        bool ok;
         if constexpr (MODE == MODE_FWD) {
-          yy = a_y[i] + kr;
-          xx = a_x[i] + ks;
-          ok = ok && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-          off = a_base[i] + (yy * p.W + xx) * p.C + kc;
+          ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
         } else {
-          int ph = a_y[i] - kr, pw = a_x[i] - ks;
           if (p.stride != 1 && !p.sub) {
-            ok = ok && ph >= 0 && pw >= 0 && (ph % p.stride) == 0 && (pw % p.stride) == 0;
-            ph /= p.stride;
-            pw /= p.stride;
+            // generic strided dgrad (not used for stride 2: sub-pixel classes) -- exact checks
+            const int ph = a_y[i] - kr, pw = a_x[i] - ks;
+            ok = ph >= 0 && pw >= 0 && (ph % p.stride) == 0 && (pw % p.stride) == 0 &&
+                 ph / p.stride < p.P && pw / p.stride < p.Q;
+          } else {
+            ok = (unsigned)(a_y[i] - kr) < (unsigned)p.P && (unsigned)(a_x[i] - ks) < (unsigned)p.Q;
           }
-          ok = ok && (unsigned)ph < (unsigned)p.P && (unsigned)pw < (unsigned)p.Q;
-          off = a_base[i] + (ph * p.Q + pw) * p.K + kc;
         }
-        ra[i] = ok ? *reinterpret_cast<const uint4*>(p.a + off) : uint4{0, 0, 0, 0};
+        ok = ok && kok;
+        const unsigned voff = ok ? (unsigned)(a_off[i] + tap + chan) * 2u : kOOB;
+        ra[i] = bload16(rsA, voff);
       }
+      const int kk = k0 + lchunk * 8;
 #pragma unroll
       for (int i = 0; i < NVB; ++i) {
-        const int n = n0 + lrow + 32 * i;
-        const bool ok = kok && n < p.gn;
-        rb[i] = ok ? *reinterpret_cast<const uint4*>(p.b + (size_t)n * p.gk + k) : uint4{0, 0, 0, 0};
+        const bool ok = b_off[i] >= 0 && kk < kend;
+        rb[i] = bload16(rsB, ok ? (unsigned)(b_off[i] + kk) * 2u : kOOB);
       }
-      // advance k -> (r,s,c) by BK for the next stage
-      kc += BK;
-      while (kc >= CIN) {
-        kc -= CIN;
-        if (++ks == p.S) { ks = 0; ++kr; }
+      // advance (r,s,c) by BK
+      if constexpr (UNIF) {
+        kc += BK;
+        if (kc >= CIN) {
+          kc = 0;
+          if (++ks == p.S) { ks = 0; ++kr; }
+        }
+      } else {
+        kc += BK;
+        while (kc >= CIN) {
+          kc -= CIN;
+          if (++ks == p.S) { ks = 0; ++kr; }
+        }
       }
     } else {
       // A': rows = reduction index m, cols = output channel co (dy rows are contiguous in co)
@@ -239,7 +298,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
         const int m = k0 + row;
         const int co = m0 + wa_col;
         const bool ok = m < kend && co < p.gm;
-        ra[i] = ok ? *reinterpret_cast<const uint4*>(p.a + (size_t)m * p.K + co) : uint4{0, 0, 0, 0};
+        ra[i] = bload16(rsA, ok ? (unsigned)(m * p.K + co) * 2u : kOOB);
       }
       // B': rows = m, cols = j=(r,s,c): im2col gather of x
 #pragma unroll
@@ -256,8 +315,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
         const int yy = pp * p.stride - p.pad + wb_r;
         const int xx = qq * p.stride - p.pad + wb_s;
         ok = ok && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-        const size_t off = ((size_t)(n * p.H + yy) * p.W + xx) * p.C + wb_c;
-        rb[i] = ok ? *reinterpret_cast<const uint4*>(p.b + off) : uint4{0, 0, 0, 0};
+        rb[i] = bload16(rsB, ok ? (unsigned)(((n * p.H + yy) * p.W + xx) * p.C + wb_c) * 2u : kOOB);
       }
     }
   };
@@ -288,6 +346,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
 
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
 
   auto compute_stage = [&](int buf) {
     const char* sA = smem + buf * STAGE;
@@ -307,39 +366,34 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
           const int row = wc * WTN + j * 16 + (lane & 15);
           fb[j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(row, chunk));
         }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
       } else {
-        // ds_read_b64_tr_b16: 16-lane group g reads rows kk*32+8g+{0..3} (then +4..7),
-        // lane 4q+p supplies row q, columns 4p..4p+3 of its 16-column block.
         const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
         const int rowb = kk * 32 + 8 * g + q;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int col = wr * WTM + i * 16 + pc;
-          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
-          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
-          s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          fa[i] = __builtin_bit_cast(bf16x8, v);
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
+          fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int col = wc * WTN + j * 16 + pc;
-          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
-          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
-          s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          fb[j] = __builtin_bit_cast(bf16x8, v);
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
+          fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -379,82 +433,112 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       }
     return;
   } else {
-    // stage fp32 wave tile in LDS (row stride WTN+4 floats), then coalesced 16-B row stores.
-    constexpr int LD = WTN + 4;
-    float* sC = reinterpret_cast<float*>(smem) + wid * WTM * LD;
+    // lane holds 4 channels chan(j) .. chan(j)+3 per MFMA column tile j of pixel m = m0 + wr*WTM + 16i + fr
+    auto chan = [&](int j) {   // channel offset inside the BN tile of acc[j][*][0]
+      return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
+    };
+    if (p.nsplit > 1) {
+      // split-K forward (small-M inference shapes): raw fp32 partials, epilogue in the reduction
+      float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wr * WTM + i * 16 + fr;
+        if (m >= p.gm) continue;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          sC[(i * 16 + fq * 4 + e) * LD + j * 16 + fr] = acc[i][j][e];
-    __syncthreads();  // (also protects the smem reuse below for stats)
-    constexpr int CPR = WTN / 8;        // 8-wide chunks per row
-    constexpr int RPP = 64 / CPR;       // rows per pass
-    const int ch = lane % CPR, rp = lane / CPR;
-    const int col0 = n0 + wc * WTN + ch * 8;
-    const bool col_ok = col0 < p.gn;   // gn % 8 == 0 required by host
-    float bias[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias[e] = (p.bias && col_ok) ? p.bias[col0 + e] : 0.f;
-    float s1[8], s2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + chan(j);
+          if (n < p.gn) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[j][i];
+        }
+      }
+      return;
+    }
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
-    for (int r = rp; r < WTM; r += RPP) {
-      const int row = m0 + wr * WTM + r;
-      if (row >= p.gm || !col_ok) continue;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(sC + r * LD + ch * 8);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(sC + r * LD + ch * 8 + 4);
-      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      size_t orow = row;
+    constexpr int VW = PAIR ? 8 : 4;          // channels per store
+    constexpr int NV = TN * 4 / VW;           // stores per pixel row
+    float s1[TN][4], s2[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
+    float bias[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + chan(j);
+      if (p.bias && n < p.gn) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bias[j][e] = b[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bias[j][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + i * 16 + fr;
+      if (m >= p.gm) continue;
+      size_t orow = m;
       if constexpr (MODE == MODE_DGRAD) {
         if (p.sub) {
-          const int n = fdiv(row, p.fd_HW);
-          const int rem = row - n * p.dH * p.dW;
+          const int n = fdiv(m, p.fd_HW);
+          const int rem = m - n * p.dH * p.dW;
           const int hh = fdiv(rem, p.fd_W);
           const int ww = rem - hh * p.dW;
           orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
         }
       }
-      const size_t o = orow * p.gn + col0;
-      u16x8 rv;
-      if (p.resid) rv = *reinterpret_cast<const u16x8*>(p.resid + o);
-      u16x8 ov;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = v[e] * p.alpha + bias[e];
-        if (p.resid) x += bf2f(rv[e]);
-        if (p.relu) x = fmaxf(x, 0.f);
-        const unsigned short b = f2bf(x);
-        ov[e] = b;
-        const float xr = bf2f(b);
-        s1[e] += xr;
-        s2[e] += xr * xr;
+      for (int v = 0; v < NV; ++v) {
+        const int j0 = v * (VW / 4);
+        const int n = n0 + chan(j0);
+        if (n >= p.gn) continue;
+        const size_t o = orow * p.gn + n;
+        unsigned short rv[VW], ov[VW];
+        if (p.resid) {
+          if constexpr (VW == 8) *reinterpret_cast<u16x8*>(rv) = *reinterpret_cast<const u16x8*>(p.resid + o);
+          else *reinterpret_cast<u16x4*>(rv) = *reinterpret_cast<const u16x4*>(p.resid + o);
+        }
+#pragma unroll
+        for (int h = 0; h < VW / 4; ++h)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = j0 + h;
+            float x = acc[j][i][e] * p.alpha + bias[j][e];
+            if (p.resid) x += bf2f(rv[h * 4 + e]);
+            if (p.relu) x = fmaxf(x, 0.f);
+            const unsigned short b = f2bf(x);
+            ov[h * 4 + e] = b;
+            const float xr = bf2f(b);
+            s1[j][e] += xr;
+            s2[j][e] += xr * xr;
+          }
+        if constexpr (VW == 8) *reinterpret_cast<u16x8*>(out + o) = *reinterpret_cast<const u16x8*>(ov);
+        else *reinterpret_cast<u16x4*>(out + o) = *reinterpret_cast<const u16x4*>(ov);
       }
-      *reinterpret_cast<u16x8*>(out + o) = ov;
     }
     if (p.stats) {
-      // reduce over lanes sharing the same chunk (lane % CPR), then across WM waves via LDS.
+      // sum over the 16 pixels of the lane group, then across the WM waves of this column block
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int o = CPR; o < 64; o <<= 1) {
-          s1[e] += __shfl_xor(s1[e], o, 64);
-          s2[e] += __shfl_xor(s2[e], o, 64);
-        }
-      }
-      __syncthreads();
-      float* red = reinterpret_cast<float*>(smem);  // [2][BN]
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            s1[j][e] += __shfl_xor(s1[j][e], o, 64);
+            s2[j][e] += __shfl_xor(s2[j][e], o, 64);
+          }
+      float* red = reinterpret_cast<float*>(smem);  // [2][BN]; stage buffers are dead here
       for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
       __syncthreads();
-      if (rp == 0) {
+      if (fr == 0) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          atomicAdd(&red[wc * WTN + ch * 8 + e], s1[e]);
-          atomicAdd(&red[BN + wc * WTN + ch * 8 + e], s2[e]);
-        }
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = chan(j) + e;
+            atomicAdd(&red[c], s1[j][e]);
+            atomicAdd(&red[BN + c], s2[j][e]);
+          }
       }
       __syncthreads();
       float* st = p.stats + (size_t)tile_m * 2 * p.gn;
@@ -491,6 +575,29 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
   }
 }
 
+// split-K forward reduction + fused epilogue: out = act(sum_s ws[s] + bias (+ resid)) as bf16
+__global__ void splitk_epilogue_kernel(const float* __restrict__ ws, __bf16* __restrict__ out,
+                                       const float* __restrict__ bias, const __bf16* __restrict__ resid,
+                                       int64_t n, int gn, int nsplit, int relu) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 s = reinterpret_cast<const f32x4*>(ws)[i];
+    for (int k = 1; k < nsplit; ++k) s += reinterpret_cast<const f32x4*>(ws + (size_t)k * n)[i];
+    const int c = (int)((i * 4) % gn);
+    u16x4 rv, ov;
+    if (resid) rv = reinterpret_cast<const u16x4*>(resid)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = s[e] + (bias ? bias[c + e] : 0.f);
+      if (resid) x += bf2f(rv[e]);
+      if (relu) x = fmaxf(x, 0.f);
+      ov[e] = f2bf(x);
+    }
+    reinterpret_cast<u16x4*>(out)[i] = ov;
+  }
+}
+
 // weight transpose for DGRAD: wt[c][t][k] = w[k][r(t)][s(t)][c]  (bf16), taps t over a
 // (possibly strided) sub-grid r = r0 + rstep*(t / subS), s = s0 + rstep*(t % subS).
 __global__ void wt_transpose_kernel(const unsigned short* __restrict__ w, unsigned short* __restrict__ wt,
@@ -518,10 +625,16 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
   const int grid = p.tiles_m * p.tiles_n * p.nsplit;
-  constexpr size_t stage_bytes = 2 * (size_t)(BM + BN) * BK * 2;
-  constexpr size_t epi_bytes = 4 * (size_t)(BM / WM) * (BN / WN + 4) * 4;
-  const size_t smem = stage_bytes > epi_bytes ? stage_bytes : epi_bytes;
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN>), dim3(grid), dim3(NT), smem, st, p);
+  const size_t stage_bytes = (size_t)(BM + BN) * BK * 2;
+  const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
+  size_t smem = (nk > 1 ? 2 : 1) * stage_bytes;
+  smem = std::max(smem, (size_t)2 * BN * sizeof(float));
+  const int cin = MODE == MODE_FWD ? p.C : p.K;
+  const bool unif = MODE != MODE_WGRAD && cin % BK == 0 && p.ksplit % BK == 0;
+  if (unif)
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true>), dim3(grid), dim3(NT), smem, st, p);
+  else
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false>), dim3(grid), dim3(NT), smem, st, p);
   PCMP_LAUNCH_CHECK();
 }
 
@@ -538,6 +651,12 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
     if (p.gn <= 64) launch_cfg<MODE, 128, 64, 2, 2>(p, st);
     else launch_cfg<MODE, 128, 128, 2, 2>(p, st);
   }
+}
+
+static unsigned tensor_bytes(const at::Tensor& t) {
+  const int64_t b = t.numel() * t.element_size();
+  TORCH_CHECK(b < (1ll << 31), "igemm: operand larger than 2 GiB (buffer-resource range)");
+  return (unsigned)b;
 }
 
 static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int R, int S,
@@ -573,6 +692,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   TORCH_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)p.gm * K < (1ll << 31), "conv_fwd: tensor too large");
   auto y = at::empty({N, p.P, p.Q, K}, x.options());
   p.a = ptr<__bf16>(x); p.b = ptr<__bf16>(w); p.out = y.data_ptr();
+  p.a_bytes = tensor_bytes(x); p.b_bytes = tensor_bytes(w);
   if (bias.has_value() && bias->defined()) { PCMP_CHECK_F32(*bias); p.bias = ptr<float>(*bias); }
   if (resid.has_value() && resid->defined()) {
     PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
@@ -582,12 +702,36 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   p.relu = relu;
   p.ksplit = p.gk; p.nsplit = 1;
   const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
+  const int BNsel = p.gn <= 64 ? 64 : 128;
   at::Tensor stats;
   if (want_stats) {
     stats = at::empty({ceil_div(p.gm, BMsel), 2, K}, x.options().dtype(at::kFloat));
     p.stats = ptr<float>(stats);
   }
-  dispatch<MODE_FWD>(p, cur_stream());
+  auto st = cur_stream();
+  // Small-M shapes (batch-1 inference: 49..3136 pixels) leave most of the 256 CUs idle; split the
+  // reduction so the grid reaches ~256 workgroups, then reduce + epilogue in one pass.
+  const int tiles = ceil_div(p.gm, BMsel) * ceil_div(p.gn, BNsel);
+  const int ksteps = ceil_div(p.gk, BK);
+  int nsplit = 1;
+  if (!want_stats && tiles < 128 && ksteps >= 8)
+    nsplit = std::max(1, std::min({ceil_div(256, tiles), ksteps / 4, 32}));
+  if (nsplit > 1) {
+    const int steps_per = ceil_div(ksteps, nsplit);
+    nsplit = ceil_div(ksteps, steps_per);
+    p.ksplit = steps_per * BK;
+    p.nsplit = nsplit;
+    const int64_t n = (int64_t)p.gm * p.gn;
+    auto ws = at::empty({(int64_t)nsplit, n}, x.options().dtype(at::kFloat));
+    p.out = ws.data_ptr();
+    dispatch<MODE_FWD>(p, st);
+    const int blocks = (int)std::min<int64_t>(1024, (n / 4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<__bf16>(y),
+                       p.bias, p.resid, n, p.gn, nsplit, (int)relu);
+    PCMP_LAUNCH_CHECK();
+    return {y};
+  }
+  dispatch<MODE_FWD>(p, st);
   if (want_stats) return {y, stats};
   return {y};
 }
@@ -640,6 +784,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
         q.offx = (opw + pad - s0) / 2;
         q.gm = N * dH * dW; q.gn = C; q.gk = subR * subS * K;
         q.a = ptr<__bf16>(dy); q.b = ptr<__bf16>(wt); q.out = dx.data_ptr();
+        q.a_bytes = tensor_bytes(dy); q.b_bytes = tensor_bytes(wt);
         q.resid = ptr<__bf16>(dx);   // in-place accumulate
         q.ksplit = q.gk;
         dispatch<MODE_DGRAD>(q, st);
@@ -650,6 +795,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
   auto dx = at::empty({N, H, W, C}, dy.options());
   p.gm = N * H * W; p.gn = C; p.gk = R * S * K;
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(wt); p.out = dx.data_ptr();
+  p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(wt);
   if (has_res) p.resid = ptr<__bf16>(*resid);
   p.ksplit = p.gk;
   dispatch<MODE_DGRAD>(p, st);
@@ -668,6 +814,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   TORCH_CHECK(out.numel() == (int64_t)K * R * S * C, "conv_wgrad: out numel");
   p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(x);
+  p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(x);
   const int BM = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
   const int BN = p.gn <= 64 ? 64 : 128;
   const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);

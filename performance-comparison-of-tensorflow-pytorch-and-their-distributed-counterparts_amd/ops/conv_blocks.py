@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import torch
 
+from . import params as _params
 from .kernels import K
 from .params import compute_weight, emit_grad, sink_or_temp
 
@@ -36,11 +37,30 @@ def _conv_bn_train(x, L, dtype):
     return c, mean, invstd, scale, shift
 
 
-def _conv_bn_eval(x, L, dtype):
-    w = compute_weight(L.weight, dtype)
-    c = K.conv_fwd(x, w, L.stride, L.pad, None, None, False, False)[0]
-    scale, shift = K.bn_eval_coeff(L.gamma, L.beta, L.running_mean, L.running_var, L.eps)
-    return c, scale, shift
+def _folded(L, dtype):
+    """Inference-time BN folding: conv(x, W) * scale + shift == conv(x, W * scale) + shift.
+
+    The folded compute weight (from the fp32 master) and the fp32 bias are cached on the layer,
+    keyed on the global weight generation (bumped by optimizer steps and training-mode forwards
+    that move the running statistics) plus the tensors' own version counters (bumped by
+    ``load_state_dict`` / in-place edits), so eval forwards after the first are pure conv launches
+    (bias + residual + ReLU fused in the conv epilogue, no BN apply pass).
+    """
+    key = (_params.WEIGHT_GEN[0], L.weight._version, L.gamma._version, L.beta._version,
+           L.running_mean._version, L.running_var._version, dtype, L.weight.device)
+    f = getattr(L, "_fold", None)
+    if f is None or f[0] != key:
+        scale, shift = K.bn_eval_coeff(L.gamma.detach(), L.beta.detach(), L.running_mean, L.running_var, L.eps)
+        w = (L.weight.detach().float() * scale.view(-1, 1, 1, 1)).to(dtype).contiguous()
+        f = (key, w, shift.float().contiguous())
+        L._fold = f
+    return f[1], f[2]
+
+
+def _conv_bn_eval(x, L, dtype, relu, resid=None):
+    """Eval-mode conv + BN (folded) (+ residual) (+ ReLU): one conv launch."""
+    w, b = _folded(L, dtype)
+    return K.conv_fwd(x, w, L.stride, L.pad, b, resid, relu, False)[0]
 
 
 def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=None, L2=None, want_g=False):
@@ -76,17 +96,12 @@ class ResidualBlockFn(torch.autograd.Function):
         main, down = blk.main_layers(), blk.down_layer()
         if not blk.training:
             h = x
-            for i, L in enumerate(main):
-                c, sc, sh = _conv_bn_eval(h, L, dtype)
-                if i < len(main) - 1:
-                    h = K.bn_apply(c, sc, sh, None, None, None, True)
-                else:
-                    last = (c, sc, sh)
-            if down is not None:
-                cd, scd, shd = _conv_bn_eval(x, down, dtype)
-                return K.bn_apply(last[0], last[1], last[2], cd, scd, shd, True)
-            return K.bn_apply(last[0], last[1], last[2], x, None, None, True)
+            for L in main[:-1]:
+                h = _conv_bn_eval(h, L, dtype, True)
+            r = _conv_bn_eval(x, down, dtype, False) if down is not None else x
+            return _conv_bn_eval(h, main[-1], dtype, True, r)
 
+        _params.WEIGHT_GEN[0] += 1      # running statistics move in training mode
         acts, cs, stats = [x], [], []
         h = x
         for i, L in enumerate(main):
@@ -175,9 +190,8 @@ class StemFn(torch.autograd.Function):
         L = stem.conv
         dtype = x.dtype
         if not stem.training:
-            c, sc, sh = _conv_bn_eval(x, L, dtype)
-            a = K.bn_apply(c, sc, sh, None, None, None, True)
-            return K.maxpool_fwd(a, 3, 2, 1, False)[0]
+            return K.maxpool_fwd(_conv_bn_eval(x, L, dtype, True), 3, 2, 1, False)[0]
+        _params.WEIGHT_GEN[0] += 1
         c, mean, invstd, sc, sh = _conv_bn_train(x, L, dtype)
         a = K.bn_apply(c, sc, sh, None, None, None, True)
         y, idx = K.maxpool_fwd(a, 3, 2, 1, True)

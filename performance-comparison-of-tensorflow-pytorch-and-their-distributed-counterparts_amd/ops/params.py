@@ -18,6 +18,15 @@ from typing import Callable
 
 import torch
 
+# Global weight generation: bumped whenever parameters or BN running statistics change through a
+# path that does not touch the tensors' version counters (fused optimizer kernels, BN-statistics
+# updates inside training forwards).  Derived caches (inference BN folding) key on it.
+WEIGHT_GEN = [0]
+
+
+def bump_weight_gen():
+    WEIGHT_GEN[0] += 1
+
 
 def compute_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     sh = getattr(p, "_shadow", None)

@@ -18,6 +18,7 @@ import math
 import torch
 
 from .ops.kernels import K
+from .ops.params import bump_weight_gen
 from .utils.flat import FlatParams
 
 
@@ -79,6 +80,7 @@ class SGD(_FlatOptimizer):
         K.sgd_flat(self.flat.master, self.flat.grad, self.mom, self.flat.shadow, None, self.lr_t, self.grad_scale,
                    self.momentum, self.dampening, self.wd, self.nesterov, self.steps == 0)
         self.steps += 1
+        bump_weight_gen()
 
     def _state(self):
         return {"mom": self.mom}
@@ -99,6 +101,7 @@ class Adam(_FlatOptimizer):
         self.step_t.add_(1.0)
         K.adam_flat(self.flat.master, self.flat.grad, self.m1, self.m2, self.flat.shadow, None, self.lr_t,
                     self.grad_scale, self.step_t, self.beta1, self.beta2, self.eps, self.wd, self.decoupled)
+        bump_weight_gen()
         self.steps += 1
 
     def _state(self):

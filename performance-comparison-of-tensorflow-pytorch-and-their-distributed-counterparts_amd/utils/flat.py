@@ -70,6 +70,8 @@ class FlatParams:
             hook(p)
 
     def refresh_shadows(self):
+        from ..ops.params import bump_weight_gen
+        bump_weight_gen()
         if self.shadow is not None:
             from ..ops.kernels import K
             K.cast_to_bf16(self.master, self.shadow) if self.shadow.dtype == torch.bfloat16 \

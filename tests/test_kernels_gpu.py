@@ -38,6 +38,8 @@ CONV_SHAPES = [
     (2, 14, 14, 128, 128, 3, 2, 1),   # 3x3 stride 2
     (2, 14, 14, 256, 512, 1, 2, 0),   # 1x1 stride-2 downsample
     (3, 7, 7, 512, 512, 3, 1, 1),     # layer4 3x3 (M not a multiple of the tile)
+    (1, 7, 7, 512, 2048, 1, 1, 0),    # batch-1 inference: split-K forward
+    (1, 14, 14, 256, 256, 3, 1, 1),   # batch-1 inference 3x3: split-K forward
     (5, 1, 1, 2048, 16, 1, 1, 0),     # linear, tiny M, N
     (64, 1, 1, 512, 1000 + 8, 1, 1, 0),  # linear 1000(+pad) classes
 ]

@@ -133,3 +133,32 @@ def test_resnet_eval_mode_uses_running_stats():
     x = torch.randn(2, 3, 32, 32)
     with torch.no_grad():
         assert torch.allclose(m.forward_logits(x), t(x), atol=1e-4)
+
+
+def test_bn_folding_cache_invalidates():
+    """Eval forwards use BN folded into the conv weights; the cache must follow every weight /
+    running-stat change (training forward, fused optimizer step, load_state_dict)."""
+    from pcmp.engine.trainer import make_state
+    from pcmp.models.resnet import resnet18
+    from pcmp.models.torch_ref import TorchResNet
+    from pcmp.ops import cross_entropy
+    torch.manual_seed(0)
+    m = resnet18(10)
+    x = torch.randn(2, 3, 32, 32)
+
+    def check():
+        m.eval()
+        t = TorchResNet("resnet18", 10).load_from_pcmp(m).eval()
+        with torch.no_grad():
+            assert torch.allclose(m.forward_logits(x), t(x), atol=1e-4)
+        m.train()
+
+    check()
+    st = make_state(m, "sgd", lr=0.1, momentum=0.9)
+    for _ in range(2):
+        st.zero_grad()
+        st.backward_step(cross_entropy(m.forward_logits(torch.randn(4, 3, 32, 32)), torch.tensor([0, 1, 2, 3])))
+        check()
+    sd = {k: v.clone() * 1.01 if v.is_floating_point() else v for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    check()
