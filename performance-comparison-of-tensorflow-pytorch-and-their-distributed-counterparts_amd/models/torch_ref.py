@@ -84,6 +84,14 @@ class TorchResNet(nn.Module):
         self.layer1, self.layer2, self.layer3, self.layer4 = stages
         self.avgpool = nn.AdaptiveAvgPool2d(1)
         self.fc = head if head is not None else nn.Linear(cin, num_classes)
+        # torchvision ResNet initialisation (the reference's models.resnet50): kaiming-normal
+        # fan_out convs, BN gamma=1 / beta=0; Linear keeps the nn.Linear default.
+        for mod in self.modules():
+            if isinstance(mod, nn.Conv2d):
+                nn.init.kaiming_normal_(mod.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(mod, nn.BatchNorm2d):
+                nn.init.ones_(mod.weight)
+                nn.init.zeros_(mod.bias)
 
     def forward(self, x):
         x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
