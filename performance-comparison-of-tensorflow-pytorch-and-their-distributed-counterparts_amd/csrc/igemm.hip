@@ -62,6 +62,17 @@ struct IgemmParams {
   int tiles_m, tiles_n;
   float alpha;
   int accumulate;   // WGRAD with nsplit==1: out += result
+  // DGRAD fused BatchNorm-backward reduction (bn_x != null): the epilogue stores
+  // g = dgrad(+resid) * (bn_mask > 0) and writes per-tile partials [tiles_m][2][gn] of
+  // (sum g, sum g*xhat) to stats (and of (sum g, sum g*xhat2) to stats2 for a second BN sharing g).
+  const __bf16* bn_mask;
+  const __bf16* bn_x;
+  const float* bn_mean;
+  const float* bn_istd;
+  const __bf16* bn_x2;
+  const float* bn_mean2;
+  const float* bn_istd2;
+  float* stats2;
 };
 
 constexpr int BK = 64;
@@ -122,7 +133,8 @@ __device__ __forceinline__ int chan_perm(int rho) {
 // UNIF: the A source channel count (C for FWD, K for DGRAD) is a multiple of BK, so the 8 16-B
 // chunks of a K-step share one filter tap (r,s) and a block-uniform channel base c0: per K-step
 // the address update is one uniform scalar offset plus one add per row.
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF>
+// BNR (DGRAD only): 0 = plain epilogue, 1 = fused BN-backward reduction, 2 = dual (two BNs share g).
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int BNR>
 __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -455,11 +467,13 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
     constexpr int VW = PAIR ? 8 : 4;          // channels per store
     constexpr int NV = TN * 4 / VW;           // stores per pixel row
-    float s1[TN][4], s2[TN][4];
+    constexpr bool bnr = MODE == MODE_DGRAD && BNR > 0;
+    constexpr bool bnr2 = MODE == MODE_DGRAD && BNR > 1;
+    float s1[TN][4], s2[TN][4], s3[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
+      for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; s3[j][e] = 0.f; }
     float bias[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -493,10 +507,16 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
         const int n = n0 + chan(j0);
         if (n >= p.gn) continue;
         const size_t o = orow * p.gn + n;
-        unsigned short rv[VW], ov[VW];
-        if (p.resid) {
-          if constexpr (VW == 8) *reinterpret_cast<u16x8*>(rv) = *reinterpret_cast<const u16x8*>(p.resid + o);
-          else *reinterpret_cast<u16x4*>(rv) = *reinterpret_cast<const u16x4*>(p.resid + o);
+        unsigned short rv[VW], ov[VW], mk[VW], xv[VW], xv2[VW];
+        auto ldv = [&](unsigned short* d, const __bf16* src) {
+          if constexpr (VW == 8) *reinterpret_cast<u16x8*>(d) = *reinterpret_cast<const u16x8*>(src + o);
+          else *reinterpret_cast<u16x4*>(d) = *reinterpret_cast<const u16x4*>(src + o);
+        };
+        if (p.resid) ldv(rv, p.resid);
+        if constexpr (bnr) {
+          if (p.bn_mask) ldv(mk, p.bn_mask);
+          ldv(xv, p.bn_x);
+          if constexpr (bnr2) ldv(xv2, p.bn_x2);
         }
 #pragma unroll
         for (int h = 0; h < VW / 4; ++h)
@@ -506,11 +526,24 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
             float x = acc[j][i][e] * p.alpha + bias[j][e];
             if (p.resid) x += bf2f(rv[h * 4 + e]);
             if (p.relu) x = fmaxf(x, 0.f);
-            const unsigned short b = f2bf(x);
+            unsigned short b = f2bf(x);
+            if constexpr (bnr) {
+              // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
+              if (p.bn_mask) {
+                const unsigned short y = mk[h * 4 + e];
+                if ((y & 0x8000u) || !(y & 0x7fffu)) b = 0;
+              }
+              const float g = bf2f(b);
+              const int c = n + h * 4 + e;
+              s1[j][e] += g;
+              s2[j][e] += g * (bf2f(xv[h * 4 + e]) - p.bn_mean[c]) * p.bn_istd[c];
+              if constexpr (bnr2) s3[j][e] += g * (bf2f(xv2[h * 4 + e]) - p.bn_mean2[c]) * p.bn_istd2[c];
+            } else {
+              const float xr = bf2f(b);
+              s1[j][e] += xr;
+              s2[j][e] += xr * xr;
+            }
             ov[h * 4 + e] = b;
-            const float xr = bf2f(b);
-            s1[j][e] += xr;
-            s2[j][e] += xr * xr;
           }
         if constexpr (VW == 8) *reinterpret_cast<u16x8*>(out + o) = *reinterpret_cast<const u16x8*>(ov);
         else *reinterpret_cast<u16x4*>(out + o) = *reinterpret_cast<const u16x4*>(ov);
@@ -526,9 +559,10 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
           for (int o = 1; o < 16; o <<= 1) {
             s1[j][e] += __shfl_xor(s1[j][e], o, 64);
             s2[j][e] += __shfl_xor(s2[j][e], o, 64);
+            if constexpr (bnr2) s3[j][e] += __shfl_xor(s3[j][e], o, 64);
           }
-      float* red = reinterpret_cast<float*>(smem);  // [2][BN]; stage buffers are dead here
-      for (int i = tid; i < 2 * BN; i += NT) red[i] = 0.f;
+      float* red = reinterpret_cast<float*>(smem);  // [2 or 3][BN]; stage buffers are dead here
+      for (int i = tid; i < (bnr2 ? 3 : 2) * BN; i += NT) red[i] = 0.f;
       __syncthreads();
       if (fr == 0) {
 #pragma unroll
@@ -538,15 +572,21 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
             const int c = chan(j) + e;
             atomicAdd(&red[c], s1[j][e]);
             atomicAdd(&red[BN + c], s2[j][e]);
+            if constexpr (bnr2) atomicAdd(&red[2 * BN + c], s3[j][e]);
           }
       }
       __syncthreads();
       float* st = p.stats + (size_t)tile_m * 2 * p.gn;
+      float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
       for (int i = tid; i < BN; i += NT) {
         const int c = n0 + i;
         if (c < p.gn) {
           st[c] = red[i];
           st[p.gn + c] = red[BN + i];
+          if constexpr (bnr2) {
+            st2[c] = red[i];
+            st2[p.gn + c] = red[2 * BN + i];
+          }
         }
       }
     }
@@ -628,13 +668,28 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   const size_t stage_bytes = (size_t)(BM + BN) * BK * 2;
   const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
   size_t smem = (nk > 1 ? 2 : 1) * stage_bytes;
-  smem = std::max(smem, (size_t)2 * BN * sizeof(float));
+  smem = std::max(smem, (size_t)(MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2) * BN * sizeof(float));
   const int cin = MODE == MODE_FWD ? p.C : p.K;
   const bool unif = MODE != MODE_WGRAD && cin % BK == 0 && p.ksplit % BK == 0;
+  const int bnr = MODE == MODE_DGRAD && p.bn_x ? (p.bn_x2 ? 2 : 1) : 0;
+  if constexpr (MODE == MODE_DGRAD) {
+    if (bnr == 1) {
+      if (unif) hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true, 1>), dim3(grid), dim3(NT), smem, st, p);
+      else hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false, 1>), dim3(grid), dim3(NT), smem, st, p);
+      PCMP_LAUNCH_CHECK();
+      return;
+    }
+    if (bnr == 2) {
+      if (unif) hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true, 2>), dim3(grid), dim3(NT), smem, st, p);
+      else hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false, 2>), dim3(grid), dim3(NT), smem, st, p);
+      PCMP_LAUNCH_CHECK();
+      return;
+    }
+  }
   if (unif)
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true>), dim3(grid), dim3(NT), smem, st, p);
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true, 0>), dim3(grid), dim3(NT), smem, st, p);
   else
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false>), dim3(grid), dim3(NT), smem, st, p);
+    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false, 0>), dim3(grid), dim3(NT), smem, st, p);
   PCMP_LAUNCH_CHECK();
 }
 
@@ -670,7 +725,9 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.fd_HW = make_fastdiv(H * W);
   p.fd_W = make_fastdiv(W);
   p.dH = H; p.dW = W; p.offy = pad; p.offx = pad; p.sub = 0; p.oph = 0; p.opw = 0;
-  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr;
+  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.stats2 = nullptr;
+  p.bn_mask = nullptr; p.bn_x = nullptr; p.bn_mean = nullptr; p.bn_istd = nullptr;
+  p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
 }
 
@@ -751,8 +808,21 @@ static at::Tensor transpose_taps(const at::Tensor& w, int r0, int s0, int rstep,
 // Stride 2 runs as up to 4 sub-pixel (parity-class) GEMMs, each over only the taps that reach
 // that class of output pixels (no MFMA work on structural zeros); their epilogues accumulate in
 // place into the residual buffer, which is CONSUMED (its memory becomes dx).
-at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride,
-                      int64_t pad, const c10::optional<at::Tensor>& resid) {
+struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (see IgemmParams)
+  const __bf16* mask = nullptr;
+  const __bf16* x = nullptr;
+  const float* mean = nullptr;
+  const float* istd = nullptr;
+  const __bf16* x2 = nullptr;
+  const float* mean2 = nullptr;
+  const float* istd2 = nullptr;
+};
+
+static int bm_for(int gm) { return gm <= 32 ? 32 : (gm <= 64 ? 64 : 128); }
+
+static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
+                                          int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
+                                          const BnrArgs* bn) {
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(w);
   const int N = dy.size(0), K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
@@ -764,32 +834,65 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
     PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
     TORCH_CHECK(resid->numel() == (int64_t)N * H * W * C, "conv_dgrad: residual shape");
   }
+  auto set_bn = [&](IgemmParams& q) {
+    if (!bn) return;
+    q.bn_mask = bn->mask; q.bn_x = bn->x; q.bn_mean = bn->mean; q.bn_istd = bn->istd;
+    q.bn_x2 = bn->x2; q.bn_mean2 = bn->mean2; q.bn_istd2 = bn->istd2;
+  };
+  auto fopts = dy.options().dtype(at::kFloat);
+  const bool two = bn && bn->x2;
   auto st = cur_stream();
   if (stride == 2) {
     at::Tensor dx = has_res ? *resid : at::zeros({N, H, W, C}, dy.options());
+    struct Cls { int oph, opw, r0, s0, subR, subS, dH, dW; };
+    std::vector<Cls> cls;
     for (int oph = 0; oph < 2; ++oph)
       for (int opw = 0; opw < 2; ++opw) {
         const int r0 = (oph + pad) & 1, s0 = (opw + pad) & 1;
         const int subR = r0 < R ? (R - r0 + 1) / 2 : 0, subS = s0 < S ? (S - s0 + 1) / 2 : 0;
         const int dH = (H - oph + 1) / 2, dW = (W - opw + 1) / 2;
-        if (subR == 0 || subS == 0 || dH <= 0 || dW <= 0) continue;
-        at::Tensor wt = transpose_taps(w, r0, s0, 2, subR, subS, st);
-        IgemmParams q = p;
-        q.R = subR; q.S = subS;
-        q.sub = 1; q.oph = oph; q.opw = opw;
-        q.dH = dH; q.dW = dW;
-        q.fd_HW = make_fastdiv(dH * dW);
-        q.fd_W = make_fastdiv(dW);
-        q.offy = (oph + pad - r0) / 2;
-        q.offx = (opw + pad - s0) / 2;
-        q.gm = N * dH * dW; q.gn = C; q.gk = subR * subS * K;
-        q.a = ptr<__bf16>(dy); q.b = ptr<__bf16>(wt); q.out = dx.data_ptr();
-        q.a_bytes = tensor_bytes(dy); q.b_bytes = tensor_bytes(wt);
-        q.resid = ptr<__bf16>(dx);   // in-place accumulate
-        q.ksplit = q.gk;
-        dispatch<MODE_DGRAD>(q, st);
+        if (dH <= 0 || dW <= 0) continue;
+        if (subR == 0 || subS == 0) {
+          // no tap reaches this pixel class: its dx is resid (or 0) -- a fused BN reduction would miss it
+          TORCH_CHECK(!bn, "conv_dgrad_bnr: stride-2 filter leaves pixel classes uncovered");
+          continue;
+        }
+        cls.push_back({oph, opw, r0, s0, subR, subS, dH, dW});
       }
-    return dx;
+    at::Tensor part, part2;
+    if (bn) {
+      int T = 0;
+      for (auto& c : cls) T += ceil_div(N * c.dH * c.dW, bm_for(N * c.dH * c.dW));
+      part = at::empty({T, 2, C}, fopts);
+      if (two) part2 = at::empty({T, 2, C}, fopts);
+    }
+    int toff = 0;
+    for (auto& c : cls) {
+      at::Tensor wt = transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st);
+      IgemmParams q = p;
+      q.R = c.subR; q.S = c.subS;
+      q.sub = 1; q.oph = c.oph; q.opw = c.opw;
+      q.dH = c.dH; q.dW = c.dW;
+      q.fd_HW = make_fastdiv(c.dH * c.dW);
+      q.fd_W = make_fastdiv(c.dW);
+      q.offy = (c.oph + pad - c.r0) / 2;
+      q.offx = (c.opw + pad - c.s0) / 2;
+      q.gm = N * c.dH * c.dW; q.gn = C; q.gk = c.subR * c.subS * K;
+      q.a = ptr<__bf16>(dy); q.b = ptr<__bf16>(wt); q.out = dx.data_ptr();
+      q.a_bytes = tensor_bytes(dy); q.b_bytes = tensor_bytes(wt);
+      q.resid = ptr<__bf16>(dx);   // in-place accumulate
+      q.ksplit = q.gk;
+      if (bn) {
+        set_bn(q);
+        q.stats = ptr<float>(part) + (size_t)toff * 2 * C;
+        if (two) q.stats2 = ptr<float>(part2) + (size_t)toff * 2 * C;
+        toff += ceil_div(q.gm, bm_for(q.gm));
+      }
+      dispatch<MODE_DGRAD>(q, st);
+    }
+    if (!bn) return {dx};
+    if (two) return {dx, part, part2};
+    return {dx, part};
   }
   at::Tensor wt = transpose_taps(w, 0, 0, 1, R, S, st);
   auto dx = at::empty({N, H, W, C}, dy.options());
@@ -798,8 +901,54 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
   p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(wt);
   if (has_res) p.resid = ptr<__bf16>(*resid);
   p.ksplit = p.gk;
+  at::Tensor part, part2;
+  if (bn) {
+    const int T = ceil_div(p.gm, bm_for(p.gm));
+    part = at::empty({T, 2, C}, fopts);
+    set_bn(p);
+    p.stats = ptr<float>(part);
+    if (two) { part2 = at::empty({T, 2, C}, fopts); p.stats2 = ptr<float>(part2); }
+  }
   dispatch<MODE_DGRAD>(p, st);
-  return dx;
+  if (!bn) return {dx};
+  if (two) return {dx, part, part2};
+  return {dx, part};
+}
+
+// dy: [N,P,Q,K], w: [K,R,S,C] -> dx [N,H,W,C] (H, W given) = dgrad + resid (resid optional).
+// Stride 2 runs as up to 4 sub-pixel (parity-class) GEMMs, each over only the taps that reach
+// that class of output pixels (no MFMA work on structural zeros); their epilogues accumulate in
+// place into the residual buffer, which is CONSUMED (its memory becomes dx).
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride,
+                      int64_t pad, const c10::optional<at::Tensor>& resid) {
+  return dgrad_impl(dy, w, H, W, stride, pad, resid, nullptr)[0];
+}
+
+// conv_dgrad with the BatchNorm-backward reduction of the layer(s) whose output gradient this is
+// fused into the epilogue: returns [g, part(, part2)] with g = (dgrad + resid) * (ymask > 0) (bf16)
+// and part = per-tile [T][2][C] partial (sum g, sum g * (x - mean) * invstd) for bn_bwd_finalize.
+std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
+                                       int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
+                                       const c10::optional<at::Tensor>& ymask, const at::Tensor& x,
+                                       const at::Tensor& mean, const at::Tensor& invstd,
+                                       const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                                       const c10::optional<at::Tensor>& invstd2) {
+  const int64_t n = (int64_t)dy.size(0) * H * W * w.size(3);
+  auto chk = [&](const at::Tensor& t, const char* nm) {
+    PCMP_CHECK_BF16(t); PCMP_CHECK_CONTIG(t);
+    TORCH_CHECK(t.numel() == n, "conv_dgrad_bnr: ", nm, " shape");
+  };
+  BnrArgs a;
+  chk(x, "x");
+  PCMP_CHECK_F32(mean); PCMP_CHECK_F32(invstd);
+  a.x = ptr<__bf16>(x); a.mean = ptr<float>(mean); a.istd = ptr<float>(invstd);
+  if (ymask.has_value() && ymask->defined()) { chk(*ymask, "ymask"); a.mask = ptr<__bf16>(*ymask); }
+  if (x2.has_value() && x2->defined()) {
+    chk(*x2, "x2");
+    TORCH_CHECK(mean2.has_value() && invstd2.has_value(), "conv_dgrad_bnr: mean2/invstd2 required with x2");
+    a.x2 = ptr<__bf16>(*x2); a.mean2 = ptr<float>(*mean2); a.istd2 = ptr<float>(*invstd2);
+  }
+  return dgrad_impl(dy, w, H, W, stride, pad, resid, &a);
 }
 
 // dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
@@ -849,6 +998,9 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid) -> Tensor",
         &pcmp::conv_dgrad);
+  m.def("conv_dgrad_bnr(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? ymask, "
+        "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2) -> Tensor[]",
+        &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
         &pcmp::conv_wgrad);
 }

@@ -63,9 +63,14 @@ def _conv_bn_eval(x, L, dtype, relu, resid=None):
     return K.conv_fwd(x, w, L.stride, L.pad, b, resid, relu, False)[0]
 
 
-def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=None, L2=None, want_g=False):
-    """Backward of one BN (or two BNs sharing the incoming gradient) -> list of dx (+g)."""
-    parts = K.bn_bwd_reduce(dy, ymask, x, mean, invstd, x2, mean2, invstd2)
+def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=None, L2=None, want_g=False,
+                 parts=None):
+    """Backward of one BN (or two BNs sharing the incoming gradient) -> list of dx (+g).
+
+    ``parts`` = reduction partials already produced by a dgrad epilogue (``conv_dgrad_bnr``; then
+    ``dy`` is the masked gradient and ``ymask`` is None) -- skips the separate reduction pass."""
+    if parts is None:
+        parts = K.bn_bwd_reduce(dy, ymask, x, mean, invstd, x2, mean2, invstd2)
     count = x.numel() // x.shape[-1]
     gout, acc, fin = sink_or_temp(L.gamma)
     bout, bacc, bfin = sink_or_temp(L.beta)
@@ -80,6 +85,12 @@ def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=Non
         grads[L2.beta] = bfin2()
     outs = K.bn_bwd_apply(dy, ymask, x, coef, x2, coef2, want_g)
     return outs, grads
+
+
+def _bnr_ok(L):
+    """Fused dgrad+BN-reduce needs every input pixel produced by an epilogue (stride-2 sub-pixel
+    classes without taps would be skipped)."""
+    return L.stride == 1 or (L.stride == 2 and L.R >= 2 and L.S >= 2)
 
 
 def _wgrad(L, dy, x, grads):
@@ -162,9 +173,15 @@ class ResidualBlockFn(torch.autograd.Function):
             wcomp = compute_weight(L.weight, dh.dtype)
             if i > 0:
                 Hi, Wi = acts[i].shape[1], acts[i].shape[2]
-                da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None)
                 m_prev, is_prev = stats[i - 1]
-                outs, gr = _bn_backward(da, acts[i], cs[i - 1], m_prev, is_prev, main[i - 1])
+                if _bnr_ok(L):
+                    # dgrad epilogue applies the previous ReLU mask and emits that BN's reduction
+                    r = K.conv_dgrad_bnr(dh, wcomp, Hi, Wi, L.stride, L.pad, None, acts[i], cs[i - 1],
+                                         m_prev, is_prev, None, None, None)
+                    outs, gr = _bn_backward(r[0], None, cs[i - 1], m_prev, is_prev, main[i - 1], parts=r[1:])
+                else:
+                    da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None)
+                    outs, gr = _bn_backward(da, acts[i], cs[i - 1], m_prev, is_prev, main[i - 1])
                 grads.update(gr)
                 dh = outs[0]
             else:

@@ -16,7 +16,7 @@ from . import _lib, ref
 TRACE = [] if os.environ.get("PCMP_TRACE_OPS") else None
 
 OP_NAMES = (
-    "conv_fwd", "conv_dgrad", "conv_wgrad",
+    "conv_fwd", "conv_dgrad", "conv_dgrad_bnr", "conv_wgrad",
     "bn_partials", "bn_finalize", "bn_eval_coeff", "bn_apply", "bn_bwd_reduce", "bn_bwd_finalize",
     "bn_bwd_apply",
     "maxpool_fwd", "maxpool_bwd", "gap_fwd", "gap_bwd", "softmax_xent", "dropout", "relu_bwd", "colsum",

@@ -44,6 +44,11 @@ def conv_dgrad(dy, w, H, W, stride, pad, resid=None):
     return dx.to(dy.dtype).contiguous()
 
 
+def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None):
+    g = _masked(conv_dgrad(dy, w, H, W, stride, pad, resid), ymask).to(dy.dtype).contiguous()
+    return [g] + bn_bwd_reduce(g, None, x, mean, invstd, x2, mean2, invstd2)
+
+
 def conv_wgrad(dy, x, out, R, S, stride, pad, accumulate):
     K, C = dy.shape[-1], x.shape[-1]
     dw = torch.nn.grad.conv2d_weight(_nchw(x), (K, C, R, S), _nchw(dy), stride=stride, padding=pad)

@@ -76,6 +76,38 @@ def test_conv_dgrad(gpu, shape):
     close(_ops().conv_dgrad(dy, w, H, W, s, p, res.clone()), ref.conv_dgrad(dy, w, H, W, s, p, res))
 
 
+BNR_SHAPES = [
+    # N, H, W, C, K, R, stride, pad, dual, resid
+    (4, 14, 14, 64, 64, 3, 1, 1, False, False),     # bottleneck conv2 -> bn1
+    (4, 14, 14, 64, 256, 1, 1, 0, False, False),    # conv3 -> bn2
+    (4, 14, 14, 128, 128, 3, 2, 1, False, False),   # strided conv2 (sub-pixel classes) -> bn1
+    (3, 7, 7, 256, 64, 1, 1, 0, True, True),        # block input grad -> previous bn3 + downsample bn
+    (2, 9, 9, 64, 32, 3, 1, 1, False, True),        # M not a multiple of the tile, narrow K
+]
+
+
+@pytest.mark.parametrize("shape", BNR_SHAPES)
+def test_conv_dgrad_bn_reduce_fused(gpu, shape):
+    N, H, W, C, K, R, s, p, dual, has_res = shape
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    dy = rnd(N, P, Q, K, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * K)) ** 0.5)
+    ymask = rnd(N, H, W, C, dev=gpu).relu()
+    x = rnd(N, H, W, C, dev=gpu)
+    mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    x2 = rnd(N, H, W, C, dev=gpu) if dual else None
+    mean2, invstd2 = (torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5) if dual else (None, None)
+    res = rnd(N, H, W, C, dev=gpu) if has_res else None
+    out = _ops().conv_dgrad_bnr(dy, w, H, W, s, p, res.clone() if has_res else None, ymask, x, mean, invstd,
+                                x2, mean2, invstd2)
+    outr = ref.conv_dgrad_bnr(dy, w, H, W, s, p, res, ymask, x, mean, invstd, x2, mean2, invstd2)
+    assert len(out) == len(outr) == (3 if dual else 2)
+    close(out[0], outr[0])
+    assert (out[0][ymask <= 0] == 0).all()
+    for a, b in zip(out[1:], outr[1:]):
+        close(a.sum(0), b.sum(0), rtol=2e-2, atol=2e-1)
+
+
 @pytest.mark.parametrize("shape", CONV_SHAPES)
 def test_conv_wgrad(gpu, shape):
     N, H, W, C, K, R, s, p = shape
