@@ -18,6 +18,8 @@ stem conv7x7/2-bn-relu-maxpool3x3/2 (:455-458).
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import params as _params
@@ -98,6 +100,44 @@ def _wgrad(L, dy, x, grads):
     grads[L.weight] = g
 
 
+class _TailBN:
+    """The BatchNorm(s) feeding a residual block's output ``out = relu(bn3(c3) + shortcut)``,
+    published by the block's training forward so that the NEXT block's backward can fuse their
+    backward reduction into its final dgrad epilogue (``conv_dgrad_bnr`` with ``ymask = out``).
+    The next block hands back the masked gradient ``g`` and the partials; this block's backward
+    then skips its own reduction pass.  The masked gradient equals d(out) on the support of the
+    ReLU, which is all this block's backward consumes."""
+
+    __slots__ = ("out_ptr", "out_shape", "c", "mean", "invstd", "cd", "meand", "invstdd", "g_ptr", "parts",
+                 "__weakref__")
+
+    def __init__(self, out, c, mean, invstd, cd, meand, invstdd):
+        self.out_ptr, self.out_shape = out.data_ptr(), tuple(out.shape)
+        self.c, self.mean, self.invstd = c, mean, invstd
+        self.cd, self.meand, self.invstdd = cd, meand, invstdd
+        self.g_ptr = None
+        self.parts = None
+
+
+_LAST_TAIL = [lambda: None]   # weakref to the most recently published _TailBN
+
+
+def _link_prev_tail(x):
+    st = _LAST_TAIL[0]()
+    if st is not None and st.out_ptr == x.data_ptr() and st.out_shape == tuple(x.shape):
+        return st
+    return None
+
+
+def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
+    """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue."""
+    r = K.conv_dgrad_bnr(dh, w, H, W, L.stride, L.pad, resid, x, prev.c, prev.mean, prev.invstd,
+                         prev.cd, prev.meand, prev.invstdd)
+    prev.parts = r[1:]
+    prev.g_ptr = r[0].data_ptr()
+    return r[0]
+
+
 class ResidualBlockFn(torch.autograd.Function):
     """out = relu( BN_L(conv_L(...relu(BN_1(conv_1(x)))...)) + shortcut(x) )."""
 
@@ -131,6 +171,10 @@ class ResidualBlockFn(torch.autograd.Function):
             cd = meand = invstdd = None
             out = K.bn_apply(cs[-1], last[0], last[1], x, None, None, True)
         if any(ctx.needs_input_grad):
+            ctx.prev_tail = _link_prev_tail(x) if ctx.needs_input_grad[0] else None
+            tail = _TailBN(out, cs[-1], stats[-1][0], stats[-1][1], cd, meand, invstdd)
+            _LAST_TAIL[0] = weakref.ref(tail)
+            ctx.tail = tail
             ctx.save_for_backward(x, out)
             ctx.main = main
             ctx.down = down
@@ -156,10 +200,19 @@ class ResidualBlockFn(torch.autograd.Function):
         grads = {}
         Ll = main[-1]
         mean, invstd = stats[-1]
+        tail = ctx.tail
+        fused = tail.parts is not None and tail.g_ptr == dout.data_ptr()
+        parts = tail.parts if fused else None
+        mask = None if fused else out          # a fused dout is already masked by out > 0
+        tail.parts = None
         if down is not None:
-            outs, gr = _bn_backward(dout, out, cs[-1], mean, invstd, Ll, cd, meand, invstdd, down)
+            outs, gr = _bn_backward(dout, mask, cs[-1], mean, invstd, Ll, cd, meand, invstdd, down, parts=parts)
             dh, dcd = outs[0], outs[1]
             gid = None
+        elif fused:
+            outs, gr = _bn_backward(dout, None, cs[-1], mean, invstd, Ll, parts=parts)
+            dh, gid = outs[0], dout
+            dcd = None
         else:
             outs, gr = _bn_backward(dout, out, cs[-1], mean, invstd, Ll, want_g=True)
             dh, gid = outs[0], outs[1]
@@ -185,16 +238,25 @@ class ResidualBlockFn(torch.autograd.Function):
                 grads.update(gr)
                 dh = outs[0]
             else:
+                prev = ctx.prev_tail if (need_dx and _bnr_ok(L)) else None
                 if down is not None:
                     _wgrad(down, dcd, acts[0], grads)
                     if need_dx:
-                        t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None)
                         wd = compute_weight(down.weight, dh.dtype)
-                        dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t)
+                        if prev is not None:
+                            t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None)
+                            dx = _dgrad_into_prev(dh, wcomp, H, W, L, t, x, prev)
+                        else:
+                            t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None)
+                            dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t)
                 elif need_dx:
-                    dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid)
+                    if prev is not None:
+                        dx = _dgrad_into_prev(dh, wcomp, H, W, L, gid, x, prev)
+                    else:
+                        dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid)
         # free saved activations early
         ctx.acts = ctx.cs = ctx.dstate = None
+        ctx.prev_tail = ctx.tail = None
         pgrads = tuple(grads.get(p) for p in ctx.params)
         return (dx, None) + pgrads
 

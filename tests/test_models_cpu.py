@@ -162,3 +162,27 @@ def test_bn_folding_cache_invalidates():
     sd = {k: v.clone() * 1.01 if v.is_floating_point() else v for k, v in m.state_dict().items()}
     m.load_state_dict(sd)
     check()
+
+
+def test_block_boundary_bn_fusion_matches_unfused(monkeypatch):
+    """The next block's dgrad epilogue computing this block's BN-backward reduction (and handing
+    back the ReLU-masked gradient) must give the same gradients as the separate reduction pass."""
+    from pcmp.models.resnet import resnet18, resnet50
+    from pcmp.ops import conv_blocks, cross_entropy
+    for ctor in (resnet18, resnet50):
+        torch.manual_seed(0)
+        m = ctor(10)
+        x = torch.randn(2, 3, 64, 64)
+        y = torch.tensor([1, 2])
+
+        def grads():
+            for p in m.parameters():
+                p.grad = None
+            cross_entropy(m.forward_logits(x), y).backward()
+            return [p.grad.clone() for p in m.parameters()]
+        g_fused = grads()
+        monkeypatch.setattr(conv_blocks, "_link_prev_tail", lambda x: None)
+        g_plain = grads()
+        monkeypatch.undo()
+        for a, b in zip(g_fused, g_plain):
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
