@@ -28,12 +28,15 @@ constexpr int kWave = 64;
 __device__ __forceinline__ float bf2f(unsigned short u) {
   return __uint_as_float(((unsigned)u) << 16);
 }
-// round-to-nearest-even f32 -> bf16 (NaN stays NaN: quiet bit forced)
+// round-to-nearest-even f32 -> bf16: the gfx950 hardware conversion (v_cvt_pk_bf16_f32, NaN-safe)
 __device__ __forceinline__ unsigned short f2bf(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
+}
+// two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32): low half = a, high half = b
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned f2bf2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
 
 __device__ __forceinline__ float warp_sum(float v) {

@@ -133,8 +133,24 @@ __device__ __forceinline__ int chan_perm(int rho) {
 // UNIF: the A source channel count (C for FWD, K for DGRAD) is a multiple of BK, so the 8 16-B
 // chunks of a K-step share one filter tap (r,s) and a block-uniform channel base c0: per K-step
 // the address update is one uniform scalar offset plus one add per row.
-// BNR (DGRAD only): 0 = plain epilogue, 1 = fused BN-backward reduction, 2 = dual (two BNs share g).
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int BNR>
+// Epilogue variants (FWD/DGRAD): plain store, + BatchNorm partial statistics of the stored output
+// (FWD training), + fused BatchNorm-backward reduction (DGRAD; BNR2: two BNs share the gradient).
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNR = 2, EPI_BNR2 = 3 };
+
+// sum over the 16 lanes of a DPP row (lanes 16r..16r+15); every lane of the row gets the total
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dppf<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dppf<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dppf<0x141>(v);   // row_half_mirror
+  v += dppf<0x140>(v);   // row_mirror
+  return v;
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI>
 __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -467,13 +483,18 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
     __bf16* out = reinterpret_cast<__bf16*>(p.out);
     constexpr int VW = PAIR ? 8 : 4;          // channels per store
     constexpr int NV = TN * 4 / VW;           // stores per pixel row
-    constexpr bool bnr = MODE == MODE_DGRAD && BNR > 0;
-    constexpr bool bnr2 = MODE == MODE_DGRAD && BNR > 1;
-    float s1[TN][4], s2[TN][4], s3[TN][4];
+    constexpr int NP = VW / 2;                // packed bf16 pairs per store
+    constexpr bool stats = EPI == EPI_STATS;
+    constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
+    constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
+    constexpr int NS = bnr2 ? 3 : 2;          // per-channel sums kept
+    float sm[NS][TN][4];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int k = 0; k < NS; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; s3[j][e] = 0.f; }
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
     float bias[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -507,10 +528,10 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
         const int n = n0 + chan(j0);
         if (n >= p.gn) continue;
         const size_t o = orow * p.gn + n;
-        unsigned short rv[VW], ov[VW], mk[VW], xv[VW], xv2[VW];
-        auto ldv = [&](unsigned short* d, const __bf16* src) {
-          if constexpr (VW == 8) *reinterpret_cast<u16x8*>(d) = *reinterpret_cast<const u16x8*>(src + o);
-          else *reinterpret_cast<u16x4*>(d) = *reinterpret_cast<const u16x4*>(src + o);
+        unsigned rv[NP], ov[NP], mk[NP], xv[NP], xv2[NP];
+        auto ldv = [&](unsigned* d, const __bf16* src) {
+          if constexpr (VW == 8) *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(src + o);
+          else *reinterpret_cast<uint2*>(d) = *reinterpret_cast<const uint2*>(src + o);
         };
         if (p.resid) ldv(rv, p.resid);
         if constexpr (bnr) {
@@ -519,73 +540,80 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
           if constexpr (bnr2) ldv(xv2, p.bn_x2);
         }
 #pragma unroll
-        for (int h = 0; h < VW / 4; ++h)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int j = j0 + h;
-            float x = acc[j][i][e] * p.alpha + bias[j][e];
-            if (p.resid) x += bf2f(rv[h * 4 + e]);
-            if (p.relu) x = fmaxf(x, 0.f);
-            unsigned short b = f2bf(x);
-            if constexpr (bnr) {
-              // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
-              if (p.bn_mask) {
-                const unsigned short y = mk[h * 4 + e];
-                if ((y & 0x8000u) || !(y & 0x7fffu)) b = 0;
-              }
-              const float g = bf2f(b);
-              const int c = n + h * 4 + e;
-              s1[j][e] += g;
-              s2[j][e] += g * (bf2f(xv[h * 4 + e]) - p.bn_mean[c]) * p.bn_istd[c];
-              if constexpr (bnr2) s3[j][e] += g * (bf2f(xv2[h * 4 + e]) - p.bn_mean2[c]) * p.bn_istd2[c];
-            } else {
-              const float xr = bf2f(b);
-              s1[j][e] += xr;
-              s2[j][e] += xr * xr;
-            }
-            ov[h * 4 + e] = b;
+        for (int q = 0; q < NP; ++q) {
+          const int j = j0 + (q >> 1), e0 = (q & 1) * 2;
+          float x0 = acc[j][i][e0] + bias[j][e0];
+          float x1 = acc[j][i][e0 + 1] + bias[j][e0 + 1];
+          if (p.resid) {
+            x0 += __uint_as_float(rv[q] << 16);
+            x1 += __uint_as_float(rv[q] & 0xffff0000u);
           }
-        if constexpr (VW == 8) *reinterpret_cast<u16x8*>(out + o) = *reinterpret_cast<const u16x8*>(ov);
-        else *reinterpret_cast<u16x4*>(out + o) = *reinterpret_cast<const u16x4*>(ov);
+          if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+          unsigned u = f2bf2(x0, x1);
+          if constexpr (bnr) {
+            // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
+            if (p.bn_mask) {
+              const unsigned y = mk[q];
+              const unsigned keep = (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
+                                    (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
+              u &= keep;
+            }
+          }
+          ov[q] = u;
+          if constexpr (stats || bnr) {
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            if constexpr (stats) {
+              sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+              sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
+            } else {
+              const int c = n + (q >> 1) * 4 + e0;
+              sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+              sm[1][j][e0] += r0 * ((__uint_as_float(xv[q] << 16) - p.bn_mean[c]) * p.bn_istd[c]);
+              sm[1][j][e0 + 1] += r1 * ((__uint_as_float(xv[q] & 0xffff0000u) - p.bn_mean[c + 1]) * p.bn_istd[c + 1]);
+              if constexpr (bnr2) {
+                sm[2][j][e0] += r0 * ((__uint_as_float(xv2[q] << 16) - p.bn_mean2[c]) * p.bn_istd2[c]);
+                sm[2][j][e0 + 1] +=
+                    r1 * ((__uint_as_float(xv2[q] & 0xffff0000u) - p.bn_mean2[c + 1]) * p.bn_istd2[c + 1]);
+              }
+            }
+          }
+        }
+        if constexpr (VW == 8) *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(ov);
+        else *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<const uint2*>(ov);
       }
     }
-    if (p.stats) {
-      // sum over the 16 pixels of the lane group, then across the WM waves of this column block
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            s1[j][e] += __shfl_xor(s1[j][e], o, 64);
-            s2[j][e] += __shfl_xor(s2[j][e], o, 64);
-            if constexpr (bnr2) s3[j][e] += __shfl_xor(s3[j][e], o, 64);
-          }
-      float* red = reinterpret_cast<float*>(smem);  // [2 or 3][BN]; stage buffers are dead here
-      for (int i = tid; i < (bnr2 ? 3 : 2) * BN; i += NT) red[i] = 0.f;
+    if constexpr (stats || bnr) {
+      // sum over the 16 pixels of the lane's DPP row, then across the WM waves sharing the columns
+      float* red = reinterpret_cast<float*>(smem);  // [WM][NS][BN]; stage buffers are dead here
       __syncthreads();
-      if (fr == 0) {
+      // (DPP reads neighbouring lanes: every lane of the wave must execute the reduction)
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int c = chan(j) + e;
-            atomicAdd(&red[c], s1[j][e]);
-            atomicAdd(&red[BN + c], s2[j][e]);
-            if constexpr (bnr2) atomicAdd(&red[2 * BN + c], s3[j][e]);
+            const float t = row_sum16(sm[k][j][e]);
+            if (fr == 0) red[(wr * NS + k) * BN + chan(j) + e] = t;
           }
-      }
       __syncthreads();
       float* st = p.stats + (size_t)tile_m * 2 * p.gn;
       float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
       for (int i = tid; i < BN; i += NT) {
         const int c = n0 + i;
         if (c < p.gn) {
-          st[c] = red[i];
-          st[p.gn + c] = red[BN + i];
+          float t[NS];
+#pragma unroll
+          for (int k = 0; k < NS; ++k) {
+            t[k] = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) t[k] += red[(w * NS + k) * BN + i];
+          }
+          st[c] = t[0];
+          st[p.gn + c] = t[1];
           if constexpr (bnr2) {
-            st2[c] = red[i];
-            st2[p.gn + c] = red[2 * BN + i];
+            st2[c] = t[0];
+            st2[p.gn + c] = t[2];
           }
         }
       }
@@ -668,28 +696,32 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   const size_t stage_bytes = (size_t)(BM + BN) * BK * 2;
   const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
   size_t smem = (nk > 1 ? 2 : 1) * stage_bytes;
-  smem = std::max(smem, (size_t)(MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2) * BN * sizeof(float));
+  smem = std::max(smem, (size_t)WM * (MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2) * BN * sizeof(float));
   const int cin = MODE == MODE_FWD ? p.C : p.K;
   const bool unif = MODE != MODE_WGRAD && cin % BK == 0 && p.ksplit % BK == 0;
-  const int bnr = MODE == MODE_DGRAD && p.bn_x ? (p.bn_x2 ? 2 : 1) : 0;
-  if constexpr (MODE == MODE_DGRAD) {
-    if (bnr == 1) {
-      if (unif) hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true, 1>), dim3(grid), dim3(NT), smem, st, p);
-      else hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false, 1>), dim3(grid), dim3(NT), smem, st, p);
-      PCMP_LAUNCH_CHECK();
-      return;
+  int epi = EPI_PLAIN;
+  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
+  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
+#define PCMP_IGEMM_LAUNCH(U, E) \
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, U, E>), dim3(grid), dim3(NT), smem, st, p)
+  if constexpr (MODE == MODE_FWD) {
+    if (epi == EPI_STATS) {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_STATS); else PCMP_IGEMM_LAUNCH(false, EPI_STATS);
+    } else {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
-    if (bnr == 2) {
-      if (unif) hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true, 2>), dim3(grid), dim3(NT), smem, st, p);
-      else hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false, 2>), dim3(grid), dim3(NT), smem, st, p);
-      PCMP_LAUNCH_CHECK();
-      return;
+  } else if constexpr (MODE == MODE_DGRAD) {
+    if (epi == EPI_BNR) {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR); else PCMP_IGEMM_LAUNCH(false, EPI_BNR);
+    } else if (epi == EPI_BNR2) {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH(false, EPI_BNR2);
+    } else {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
+  } else {
+    PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
   }
-  if (unif)
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, true, 0>), dim3(grid), dim3(NT), smem, st, p);
-  else
-    hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, false, 0>), dim3(grid), dim3(NT), smem, st, p);
+#undef PCMP_IGEMM_LAUNCH
   PCMP_LAUNCH_CHECK();
 }
 
