@@ -73,6 +73,10 @@ struct IgemmParams {
   const float* bn_mean2;
   const float* bn_istd2;
   float* stats2;
+  // mask recomputed from bn_x instead of read: relu(bn_x * bn_msc + bn_msh) > 0 (the forward BN
+  // apply of an intermediate layer); used when bn_mask is null
+  const float* bn_msc;
+  const float* bn_msh;
 };
 
 constexpr int BK = 64;
@@ -136,19 +140,6 @@ __device__ __forceinline__ int chan_perm(int rho) {
 // Epilogue variants (FWD/DGRAD): plain store, + BatchNorm partial statistics of the stored output
 // (FWD training), + fused BatchNorm-backward reduction (DGRAD; BNR2: two BNs share the gradient).
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNR = 2, EPI_BNR2 = 3 };
-
-// sum over the 16 lanes of a DPP row (lanes 16r..16r+15); every lane of the row gets the total
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row_sum16(float v) {
-  v += dppf<0xB1>(v);    // quad_perm [1,0,3,2]
-  v += dppf<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dppf<0x141>(v);   // row_half_mirror
-  v += dppf<0x140>(v);   // row_mirror
-  return v;
-}
 
 template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI>
 __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
@@ -495,26 +486,17 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
-    float bias[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + chan(j);
-      if (p.bias && n < p.gn) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(p.bias + n);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bias[j][e] = b[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bias[j][e] = 0.f;
-      }
-    }
+    const bool has_res = p.resid != nullptr;
+    const bool has_mk = bnr && p.bn_mask != nullptr;
+    const bool mfx = bnr && !has_mk && p.bn_msc != nullptr;   // ReLU mask recomputed from x
+    // output row offsets of the TM pixel-row groups
+    size_t orows[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wr * WTM + i * 16 + fr;
-      if (m >= p.gm) continue;
-      size_t orow = m;
+      size_t orow = m < p.gm ? m : 0;
       if constexpr (MODE == MODE_DGRAD) {
-        if (p.sub) {
+        if (p.sub && m < p.gm) {
           const int n = fdiv(m, p.fd_HW);
           const int rem = m - n * p.dH * p.dW;
           const int hh = fdiv(rem, p.fd_W);
@@ -522,80 +504,154 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
           orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
         }
       }
+      orows[i] = orow;
+    }
+    // Stores walk (i outer, v inner: the two 64-B halves of a pixel's 128-B channel run are stored
+    // back to back); the resid / mask / x operand loads of step t+1 are issued before the math of
+    // step t (one-deep software pipeline).
+    unsigned rvA[2][NP], mkA[2][NP], xvA[2][NP], xv2A[2][NP];
+    auto issue = [&](int t, int b) {
+      const int i = t / NV, v = t % NV;
+      const int m = m0 + wr * WTM + i * 16 + fr;
+      const int n = n0 + chan(v * (VW / 4));
+      const bool ok = m < p.gm && n < p.gn;
+      const size_t o = orows[i] * p.gn + (ok ? n : 0);
+      auto ldv = [&](unsigned* d, const __bf16* src) {
+        if constexpr (VW == 8) {
+          const uint4 t4 = ok ? *reinterpret_cast<const uint4*>(src + o) : uint4{0, 0, 0, 0};
+          d[0] = t4.x; d[1] = t4.y; d[2] = t4.z; d[3] = t4.w;
+        } else {
+          const uint2 t2 = ok ? *reinterpret_cast<const uint2*>(src + o) : uint2{0, 0};
+          d[0] = t2.x; d[1] = t2.y;
+        }
+      };
+      if (has_res) ldv(rvA[b], p.resid);
+      if constexpr (bnr) {
+        if (has_mk) ldv(mkA[b], p.bn_mask);
+        ldv(xvA[b], p.bn_x);
+        if constexpr (bnr2) ldv(xv2A[b], p.bn_x2);
+      }
+    };
+    if (has_res || bnr) issue(0, 0);
+    // per-channel coefficient tables of the tile's BN columns, staged once in LDS (stage buffers
+    // are dead; the column-sum scratch that reuses this space is written after a barrier)
+    float* ctab = reinterpret_cast<float*>(smem);
+    const bool has_bias = MODE == MODE_FWD && p.bias != nullptr;
+    if (bnr || has_bias) {
+      for (int idx = tid; idx < BN; idx += NT) {
+        const int c = min(n0 + idx, p.gn - 1);
+        if (has_bias) ctab[idx] = p.bias[c];
+        if constexpr (bnr) {
+          const float is = p.bn_istd[c];
+          ctab[0 * BN + idx] = is;
+          ctab[1 * BN + idx] = -p.bn_mean[c] * is;
+          ctab[2 * BN + idx] = mfx ? p.bn_msc[c] : 0.f;
+          ctab[3 * BN + idx] = mfx ? p.bn_msh[c] : 0.f;
+          if constexpr (bnr2) {
+            const float is2 = p.bn_istd2[c];
+            ctab[4 * BN + idx] = is2;
+            ctab[5 * BN + idx] = -p.bn_mean2[c] * is2;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    auto ldt = [&](float* d, int tab, int j0) {
+#pragma unroll
+      for (int e4 = 0; e4 < VW; e4 += 4) {
+        const f32x4 t4 = *reinterpret_cast<const f32x4*>(ctab + tab * BN + chan(j0) + e4);
+        d[e4] = t4[0]; d[e4 + 1] = t4[1]; d[e4 + 2] = t4[2]; d[e4 + 3] = t4[3];
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + i * 16 + fr;
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
+        const int t = i * NV + v, b = t & 1;
+        if ((has_res || bnr) && t + 1 < NV * TM) issue(t + 1, (t + 1) & 1);
         const int j0 = v * (VW / 4);
         const int n = n0 + chan(j0);
-        if (n >= p.gn) continue;
-        const size_t o = orow * p.gn + n;
-        unsigned rv[NP], ov[NP], mk[NP], xv[NP], xv2[NP];
-        auto ldv = [&](unsigned* d, const __bf16* src) {
-          if constexpr (VW == 8) *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(src + o);
-          else *reinterpret_cast<uint2*>(d) = *reinterpret_cast<const uint2*>(src + o);
-        };
-        if (p.resid) ldv(rv, p.resid);
-        if constexpr (bnr) {
-          if (p.bn_mask) ldv(mk, p.bn_mask);
-          ldv(xv, p.bn_x);
-          if constexpr (bnr2) ldv(xv2, p.bn_x2);
+        if (m >= p.gm || n >= p.gn) continue;
+        const size_t o = orows[i] * p.gn + n;
+        float bias[VW], ka[VW], kb[VW], ka2[VW], kb2[VW], msc[VW], msh[VW];
+        if (has_bias) ldt(bias, 0, j0);
+        else {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) bias[e] = 0.f;
         }
+        if constexpr (bnr) {
+          ldt(ka, 0, j0); ldt(kb, 1, j0);
+          if (mfx) { ldt(msc, 2, j0); ldt(msh, 3, j0); }
+          if constexpr (bnr2) { ldt(ka2, 4, j0); ldt(kb2, 5, j0); }
+        }
+        unsigned ov[NP];
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
-          const int j = j0 + (q >> 1), e0 = (q & 1) * 2;
-          float x0 = acc[j][i][e0] + bias[j][e0];
-          float x1 = acc[j][i][e0 + 1] + bias[j][e0 + 1];
-          if (p.resid) {
-            x0 += __uint_as_float(rv[q] << 16);
-            x1 += __uint_as_float(rv[q] & 0xffff0000u);
+          const int j = j0 + (q >> 1), e0 = (q & 1) * 2, ce = 2 * q;   // ce: channel within the store
+          float x0 = acc[j][i][e0] + bias[ce];
+          float x1 = acc[j][i][e0 + 1] + bias[ce + 1];
+          if (has_res) {
+            x0 += __uint_as_float(rvA[b][q] << 16);
+            x1 += __uint_as_float(rvA[b][q] & 0xffff0000u);
           }
           if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
           unsigned u = f2bf2(x0, x1);
           if constexpr (bnr) {
+            const float xa = __uint_as_float(xvA[b][q] << 16), xb = __uint_as_float(xvA[b][q] & 0xffff0000u);
             // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
-            if (p.bn_mask) {
-              const unsigned y = mk[q];
+            if (has_mk) {
+              const unsigned y = mkA[b][q];
               const unsigned keep = (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
                                     (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
               u &= keep;
+            } else if (mfx) {
+              const float z0 = fmaf(xa, msc[ce], msh[ce]);
+              const float z1 = fmaf(xb, msc[ce + 1], msh[ce + 1]);
+              u &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
             }
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+            sm[1][j][e0] += r0 * fmaf(xa, ka[ce], kb[ce]);
+            sm[1][j][e0 + 1] += r1 * fmaf(xb, ka[ce + 1], kb[ce + 1]);
+            if constexpr (bnr2) {
+              sm[2][j][e0] += r0 * fmaf(__uint_as_float(xv2A[b][q] << 16), ka2[ce], kb2[ce]);
+              sm[2][j][e0 + 1] += r1 * fmaf(__uint_as_float(xv2A[b][q] & 0xffff0000u), ka2[ce + 1], kb2[ce + 1]);
+            }
+          } else if constexpr (stats) {
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+            sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
           }
           ov[q] = u;
-          if constexpr (stats || bnr) {
-            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
-            if constexpr (stats) {
-              sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
-              sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
-            } else {
-              const int c = n + (q >> 1) * 4 + e0;
-              sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
-              sm[1][j][e0] += r0 * ((__uint_as_float(xv[q] << 16) - p.bn_mean[c]) * p.bn_istd[c]);
-              sm[1][j][e0 + 1] += r1 * ((__uint_as_float(xv[q] & 0xffff0000u) - p.bn_mean[c + 1]) * p.bn_istd[c + 1]);
-              if constexpr (bnr2) {
-                sm[2][j][e0] += r0 * ((__uint_as_float(xv2[q] << 16) - p.bn_mean2[c]) * p.bn_istd2[c]);
-                sm[2][j][e0 + 1] +=
-                    r1 * ((__uint_as_float(xv2[q] & 0xffff0000u) - p.bn_mean2[c + 1]) * p.bn_istd2[c + 1]);
-              }
-            }
-          }
         }
         if constexpr (VW == 8) *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(ov);
         else *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<const uint2*>(ov);
       }
     }
     if constexpr (stats || bnr) {
-      // sum over the 16 pixels of the lane's DPP row, then across the WM waves sharing the columns
-      float* red = reinterpret_cast<float*>(smem);  // [WM][NS][BN]; stage buffers are dead here
-      __syncthreads();
-      // (DPP reads neighbouring lanes: every lane of the wave must execute the reduction)
+      // Column sums over the tile's pixels: each wave transposes its lanes' partial sums through
+      // LDS ([16 pixel rows][NS][WTN], padded rows) and every lane then sums 16 values for its
+      // (k, channel) pairs -- ~3 LDS ops per value instead of a 4-step cross-lane reduction.
+      constexpr int RS = NS * WTN + 4;
+      float* tb = reinterpret_cast<float*>(smem) + wid * 16 * RS;
+      float* red = reinterpret_cast<float*>(smem) + 4 * 16 * RS;   // [WM][NS][BN]
+      __syncthreads();   // stage buffers are dead from here on
 #pragma unroll
       for (int k = 0; k < NS; ++k)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(tb + fr * RS + k * WTN + chan(j) - wc * WTN) =
+              f32x4{sm[k][j][0], sm[k][j][1], sm[k][j][2], sm[k][j][3]};
+      __syncthreads();
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float t = row_sum16(sm[k][j][e]);
-            if (fr == 0) red[(wr * NS + k) * BN + chan(j) + e] = t;
-          }
+      for (int idx = lane; idx < NS * WTN; idx += 64) {
+        const int k = idx / WTN, ch = idx - k * WTN;
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += tb[r * RS + k * WTN + ch];
+        red[(wr * NS + k) * BN + wc * WTN + ch] = t;
+      }
       __syncthreads();
       float* st = p.stats + (size_t)tile_m * 2 * p.gn;
       float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
@@ -696,7 +752,11 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   const size_t stage_bytes = (size_t)(BM + BN) * BK * 2;
   const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
   size_t smem = (nk > 1 ? 2 : 1) * stage_bytes;
-  smem = std::max(smem, (size_t)WM * (MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2) * BN * sizeof(float));
+  const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
+  if (epi_red) {  // epilogue column-sum scratch: 4 waves x [16][NS*WTN+4] + [WM][NS][BN] floats
+    const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
+    smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
+  }
   const int cin = MODE == MODE_FWD ? p.C : p.K;
   const bool unif = MODE != MODE_WGRAD && cin % BK == 0 && p.ksplit % BK == 0;
   int epi = EPI_PLAIN;
@@ -759,7 +819,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.dH = H; p.dW = W; p.offy = pad; p.offx = pad; p.sub = 0; p.oph = 0; p.opw = 0;
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.stats2 = nullptr;
   p.bn_mask = nullptr; p.bn_x = nullptr; p.bn_mean = nullptr; p.bn_istd = nullptr;
-  p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr;
+  p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr; p.bn_msc = nullptr; p.bn_msh = nullptr;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
 }
 
@@ -848,6 +908,8 @@ struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (s
   const __bf16* x2 = nullptr;
   const float* mean2 = nullptr;
   const float* istd2 = nullptr;
+  const float* msc = nullptr;
+  const float* msh = nullptr;
 };
 
 static int bm_for(int gm) { return gm <= 32 ? 32 : (gm <= 64 ? 64 : 128); }
@@ -870,6 +932,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     if (!bn) return;
     q.bn_mask = bn->mask; q.bn_x = bn->x; q.bn_mean = bn->mean; q.bn_istd = bn->istd;
     q.bn_x2 = bn->x2; q.bn_mean2 = bn->mean2; q.bn_istd2 = bn->istd2;
+    q.bn_msc = bn->msc; q.bn_msh = bn->msh;
   };
   auto fopts = dy.options().dtype(at::kFloat);
   const bool two = bn && bn->x2;
@@ -964,7 +1027,9 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& ymask, const at::Tensor& x,
                                        const at::Tensor& mean, const at::Tensor& invstd,
                                        const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
-                                       const c10::optional<at::Tensor>& invstd2) {
+                                       const c10::optional<at::Tensor>& invstd2,
+                                       const c10::optional<at::Tensor>& mscale,
+                                       const c10::optional<at::Tensor>& mshift) {
   const int64_t n = (int64_t)dy.size(0) * H * W * w.size(3);
   auto chk = [&](const at::Tensor& t, const char* nm) {
     PCMP_CHECK_BF16(t); PCMP_CHECK_CONTIG(t);
@@ -979,6 +1044,11 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
     chk(*x2, "x2");
     TORCH_CHECK(mean2.has_value() && invstd2.has_value(), "conv_dgrad_bnr: mean2/invstd2 required with x2");
     a.x2 = ptr<__bf16>(*x2); a.mean2 = ptr<float>(*mean2); a.istd2 = ptr<float>(*invstd2);
+  }
+  if (!a.mask && mscale.has_value() && mscale->defined()) {
+    TORCH_CHECK(mshift.has_value() && mshift->defined(), "conv_dgrad_bnr: mshift required with mscale");
+    PCMP_CHECK_F32(*mscale); PCMP_CHECK_F32(*mshift);
+    a.msc = ptr<float>(*mscale); a.msh = ptr<float>(*mshift);
   }
   return dgrad_impl(dy, w, H, W, stride, pad, resid, &a);
 }
@@ -1031,7 +1101,8 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("conv_dgrad(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid) -> Tensor",
         &pcmp::conv_dgrad);
   m.def("conv_dgrad_bnr(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? ymask, "
-        "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2) -> Tensor[]",
+        "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2, Tensor? mscale, "
+        "Tensor? mshift) -> Tensor[]",
         &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
         &pcmp::conv_wgrad);

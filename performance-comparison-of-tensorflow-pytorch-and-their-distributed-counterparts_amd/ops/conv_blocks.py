@@ -132,7 +132,7 @@ def _link_prev_tail(x):
 def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
     """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue."""
     r = K.conv_dgrad_bnr(dh, w, H, W, L.stride, L.pad, resid, x, prev.c, prev.mean, prev.invstd,
-                         prev.cd, prev.meand, prev.invstdd)
+                         prev.cd, prev.meand, prev.invstdd, None, None)
     prev.parts = r[1:]
     prev.g_ptr = r[0].data_ptr()
     return r[0]
@@ -153,12 +153,13 @@ class ResidualBlockFn(torch.autograd.Function):
             return _conv_bn_eval(h, main[-1], dtype, True, r)
 
         _params.WEIGHT_GEN[0] += 1      # running statistics move in training mode
-        acts, cs, stats = [x], [], []
+        acts, cs, stats, coefs = [x], [], [], []
         h = x
         for i, L in enumerate(main):
             c, mean, invstd, sc, sh = _conv_bn_train(h, L, dtype)
             cs.append(c)
             stats.append((mean, invstd))
+            coefs.append((sc, sh))
             if i < len(main) - 1:
                 h = K.bn_apply(c, sc, sh, None, None, None, True)
                 acts.append(h)
@@ -181,6 +182,7 @@ class ResidualBlockFn(torch.autograd.Function):
             ctx.acts = acts[1:]          # intermediates only; x and out go through save_for_backward
             ctx.cs = cs
             ctx.stats = stats
+            ctx.coefs = coefs
             ctx.dstate = (cd, meand, invstdd)
             ctx.params = params
             ctx.saved_ok = True
@@ -229,8 +231,10 @@ class ResidualBlockFn(torch.autograd.Function):
                 m_prev, is_prev = stats[i - 1]
                 if _bnr_ok(L):
                     # dgrad epilogue applies the previous ReLU mask and emits that BN's reduction
-                    r = K.conv_dgrad_bnr(dh, wcomp, Hi, Wi, L.stride, L.pad, None, acts[i], cs[i - 1],
-                                         m_prev, is_prev, None, None, None)
+                    # the ReLU mask of acts[i] = relu(cs[i-1] * scale + shift) is recomputed from cs[i-1]
+                    sc_prev, sh_prev = ctx.coefs[i - 1]
+                    r = K.conv_dgrad_bnr(dh, wcomp, Hi, Wi, L.stride, L.pad, None, None, cs[i - 1],
+                                         m_prev, is_prev, None, None, None, sc_prev, sh_prev)
                     outs, gr = _bn_backward(r[0], None, cs[i - 1], m_prev, is_prev, main[i - 1], parts=r[1:])
                 else:
                     da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None)
@@ -255,7 +259,7 @@ class ResidualBlockFn(torch.autograd.Function):
                     else:
                         dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid)
         # free saved activations early
-        ctx.acts = ctx.cs = ctx.dstate = None
+        ctx.acts = ctx.cs = ctx.dstate = ctx.coefs = None
         ctx.prev_tail = ctx.tail = None
         pgrads = tuple(grads.get(p) for p in ctx.params)
         return (dx, None) + pgrads

@@ -44,7 +44,10 @@ def conv_dgrad(dy, w, H, W, stride, pad, resid=None):
     return dx.to(dy.dtype).contiguous()
 
 
-def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None):
+def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None,
+                   mscale=None, mshift=None):
+    if ymask is None and mscale is not None:      # mask recomputed from x: relu(x * scale + shift) > 0
+        ymask = (x.float() * mscale + mshift).reshape(x.shape)
     g = _masked(conv_dgrad(dy, w, H, W, stride, pad, resid), ymask).to(dy.dtype).contiguous()
     return [g] + bn_bwd_reduce(g, None, x, mean, invstd, x2, mean2, invstd2)
 

@@ -99,13 +99,22 @@ def test_conv_dgrad_bn_reduce_fused(gpu, shape):
     mean2, invstd2 = (torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5) if dual else (None, None)
     res = rnd(N, H, W, C, dev=gpu) if has_res else None
     out = _ops().conv_dgrad_bnr(dy, w, H, W, s, p, res.clone() if has_res else None, ymask, x, mean, invstd,
-                                x2, mean2, invstd2)
+                                x2, mean2, invstd2, None, None)
     outr = ref.conv_dgrad_bnr(dy, w, H, W, s, p, res, ymask, x, mean, invstd, x2, mean2, invstd2)
     assert len(out) == len(outr) == (3 if dual else 2)
     close(out[0], outr[0])
     assert (out[0][ymask <= 0] == 0).all()
     for a, b in zip(out[1:], outr[1:]):
         close(a.sum(0), b.sum(0), rtol=2e-2, atol=2e-1)
+    if not dual:
+        # intermediate-layer form: ReLU mask recomputed from x (relu(x * scale + shift) > 0)
+        sc, sh = torch.randn(C, device=gpu), torch.randn(C, device=gpu) * 0.5
+        out = _ops().conv_dgrad_bnr(dy, w, H, W, s, p, res.clone() if has_res else None, None, x, mean, invstd,
+                                    None, None, None, sc, sh)
+        outr = ref.conv_dgrad_bnr(dy, w, H, W, s, p, res, None, x, mean, invstd, None, None, None, sc, sh)
+        close(out[0], outr[0])
+        assert ((out[0] == 0) | ((x.float() * sc + sh) > 0)).all()
+        close(out[1].sum(0), outr[1].sum(0), rtol=2e-2, atol=2e-1)
 
 
 @pytest.mark.parametrize("shape", CONV_SHAPES)

@@ -61,7 +61,13 @@ def main():
         for mode in a.modes.split(","):
             if mode == "dgrad" and name.startswith("stem"):
                 continue
-            if mode == "fwd":
+            if mode == "dgrad_bnr":
+                if name.startswith("stem"):
+                    continue
+                xm = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+                mu, isd = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+                fn = lambda: ops.conv_dgrad_bnr(dy, w, H, W, s, p, None, None, xm, mu, isd, None, None, None, isd, mu)
+            elif mode == "fwd":
                 fn = lambda: ops.conv_fwd(x, w, s, p, None, None, False, True)
             elif mode == "dgrad":
                 fn = lambda: ops.conv_dgrad(dy, w, H, W, s, p, None)
@@ -75,7 +81,7 @@ def main():
                 dyc = dy.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
                 if mode == "fwd":
                     tf = lambda: torch.nn.functional.conv2d(xc, wc, None, s, p)
-                elif mode == "dgrad":
+                elif mode.startswith("dgrad"):
                     tf = lambda: torch.nn.grad.conv2d_input(xc.shape, wc, dyc, s, p)
                 else:
                     tf = lambda: torch.nn.grad.conv2d_weight(xc, wc.shape, dyc, s, p)
