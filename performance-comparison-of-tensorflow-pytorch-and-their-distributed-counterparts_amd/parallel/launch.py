@@ -49,9 +49,13 @@ def init(local_rank_arg: int | None = None, backend: str | None = None, timeout_
     rank, world, local = env_ranks(local_rank_arg)
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
+    # Rehearsal overrides (multi-rank logic on a one-GPU box): PCMP_SHARED_DEVICE=1 binds every
+    # rank to cuda:0, PCMP_DIST_BACKEND=gloo selects gloo (RCCL needs one GPU per rank).
+    dev_index = 0 if os.environ.get("PCMP_SHARED_DEVICE") == "1" else local
+    backend = backend or os.environ.get("PCMP_DIST_BACKEND") or None
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
     be = None
