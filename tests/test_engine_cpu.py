@@ -126,3 +126,16 @@ def test_synthetic_datasets_shapes():
     ids, mask, lab = t.get_batch(list(range(50)))
     assert ids.shape == (50, 128) and (ids[:, 0] == 101).all() and torch.equal(mask, (ids > 0).long())
     assert len(BatchLoader(ds, 32)) == 4
+
+
+def test_label_tables_and_decode():
+    from pcmp.data.labels import decode_topk, imagenette_labels, parse_label_table
+    txt = "{0: 'tench, Tinca tinca',\n 1: 'goldfish, Carassius auratus',\n 2: \"great white shark\"}"
+    assert parse_label_table(txt) == ["tench, Tinca tinca", "goldfish, Carassius auratus", "great white shark"]
+    assert parse_label_table("a\nb\n\nc\n") == ["a", "b", "c"]
+    labels = imagenette_labels()
+    assert len(labels) == 10
+    logits = torch.tensor([[0.0, 5.0, 1.0]])
+    top = decode_topk(logits, ["x", "y", "z"], k=2)
+    assert [t[0] for t in top[0]] == [1, 2] and top[0][0][1] == "y"
+    assert abs(sum(torch.softmax(logits, -1)[0].tolist()) - 1) < 1e-6
