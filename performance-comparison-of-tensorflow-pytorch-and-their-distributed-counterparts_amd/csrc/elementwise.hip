@@ -225,14 +225,17 @@ __global__ void relu_bwd_kernel(const __bf16* __restrict__ dy, const __bf16* __r
 // ---------------------------------------------------------------- column sums (bias grad) -------
 // x [M][C] bf16 -> out[C] f32 (+= if accumulate). grid.x over 64-vector column slabs,
 // grid.y over row chunks -> partial f32 atomics (few rows chunks; deterministic when grid.y==1)
-__global__ void colsum_kernel(const __bf16* __restrict__ x, float* __restrict__ out, int M, int C,
-                              int rows_per_block) {
+// Column sums of a bf16 [M][C] matrix (bias gradients): stage 1 writes per-chunk partial sums
+// part[chunk][C] (grid = column blocks x row chunks, sized to fill the GPU), stage 2 reduces the
+// chunks deterministically (launch_col_reduce).
+__global__ void colsum_partial_kernel(const __bf16* __restrict__ x, float* __restrict__ part, int M, int C,
+                                      int rows_per_chunk) {
   const int CV = C / 8;
   const int cv = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
-  __shared__ float sh[4][64][8];
+  __shared__ float sh[4][64][9];
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(M, r0 + rows_per_chunk);
   if (cv < CV) {
     for (int r = r0 + g; r < r1; r += 4) {
       float v[8];
@@ -245,13 +248,48 @@ __global__ void colsum_kernel(const __bf16* __restrict__ x, float* __restrict__ 
   for (int e = 0; e < 8; ++e) sh[g][threadIdx.x & 63][e] = acc[e];
   __syncthreads();
   if (g == 0 && cv < CV) {
+    float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = acc[e] + sh[1][threadIdx.x][e] + sh[2][threadIdx.x][e] + sh[3][threadIdx.x][e];
-      if (gridDim.y == 1) out[cv * 8 + e] = v;
-      else atomicAdd(out + cv * 8 + e, v);
-    }
+    for (int e = 0; e < 8; ++e) v[e] = acc[e] + sh[1][threadIdx.x][e] + sh[2][threadIdx.x][e] + sh[3][threadIdx.x][e];
+    f32x4* o = reinterpret_cast<f32x4*>(part + (size_t)blockIdx.y * C + cv * 8);
+    o[0] = f32x4{v[0], v[1], v[2], v[3]};
+    o[1] = f32x4{v[4], v[5], v[6], v[7]};
   }
+}
+
+// out[l] (+)= sum_t part[t][l]: block = 64 column quads x 4 row groups, float4 loads
+__global__ void col_reduce_kernel(const float* __restrict__ part, int T, int L, float* __restrict__ out,
+                                  int accumulate) {
+  const int L4 = L / 4;
+  const int q = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  __shared__ f32x4 sh[4][64];
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (q < L4) {
+    const f32x4* p4 = reinterpret_cast<const f32x4*>(part);
+    int t = g;
+    for (; t + 12 < T; t += 16) {
+      const f32x4 a = p4[(size_t)t * L4 + q], b = p4[(size_t)(t + 4) * L4 + q];
+      const f32x4 c = p4[(size_t)(t + 8) * L4 + q], d = p4[(size_t)(t + 12) * L4 + q];
+      s += (a + b) + (c + d);
+    }
+    for (; t < T; t += 4) s += p4[(size_t)t * L4 + q];
+  }
+  sh[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && q < L4) {
+    s = (sh[0][threadIdx.x] + sh[1][threadIdx.x]) + (sh[2][threadIdx.x] + sh[3][threadIdx.x]);
+    f32x4* o = reinterpret_cast<f32x4*>(out);
+    if (accumulate) s += o[q];
+    o[q] = s;
+  }
+}
+
+void launch_col_reduce(const float* part, int T, int L, float* out, bool accumulate, hipStream_t st) {
+  TORCH_CHECK(L % 4 == 0, "col_reduce: L % 4");
+  hipLaunchKernelGGL(col_reduce_kernel, dim3(ceil_div(L / 4, 64)), dim3(256), 0, st, part, T, L, out,
+                     (int)accumulate);
+  PCMP_LAUNCH_CHECK();
 }
 
 // ---------------------------------------------------------------- input conversion -------------
@@ -388,25 +426,19 @@ at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y) {
 }
 
 void colsum(const at::Tensor& x, at::Tensor out, bool accumulate) {
-  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out);
+  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
   const int C = x.size(-1);
   const int M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && out.numel() == C, "colsum: shapes");
-  int chunks = std::max(1, std::min(64, M / 2048));
-  if (accumulate && chunks == 1) {
-    // keep deterministic single pass; accumulate via temp
-    auto tmp = at::empty_like(out);
-    hipLaunchKernelGGL(colsum_kernel, dim3(ceil_div(C / 8, 64), 1), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
-                       ptr<float>(tmp), M, C, M);
-    PCMP_LAUNCH_CHECK();
-    out.add_(tmp);
-    return;
-  }
-  if (chunks > 1 && !accumulate) out.zero_();
-  const int rpb = ceil_div(M, chunks);
-  hipLaunchKernelGGL(colsum_kernel, dim3(ceil_div(C / 8, 64), chunks), dim3(256), 0, cur_stream(),
-                     ptr<__bf16>(x), ptr<float>(out), M, C, rpb);
+  const int colblocks = ceil_div(C / 8, 64);
+  const int chunks = std::max(1, std::min({ceil_div(512, colblocks), ceil_div(M, 16), 256}));
+  const int rpc = ceil_div(M, chunks);
+  const int T = ceil_div(M, rpc);
+  auto part = at::empty({T, C}, out.options());
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(colblocks, T), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                     ptr<float>(part), M, C, rpc);
   PCMP_LAUNCH_CHECK();
+  launch_col_reduce(ptr<float>(part), T, C, ptr<float>(out), accumulate, cur_stream());
 }
 
 at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad, double scale, const c10::optional<at::Tensor>& mean,

@@ -156,14 +156,6 @@ __global__ void layernorm_bwd_kernel(const __bf16* __restrict__ dy, const __bf16
 }
 
 // column reduction of partials [T][L] -> out[L] (fp32 result, fp64 accumulation); accumulate opt.
-__global__ void colreduce_kernel(const float* __restrict__ part, int T, int L, float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= L) return;
-  double s = 0;
-  for (int t = 0; t < T; ++t) s += part[(size_t)t * L + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
-}
-
 // ------------------------------------------------------------------------------- activations
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float dgelu_erf(float x) {
@@ -575,9 +567,7 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& xs, const at::T
                      ptr<__bf16>(dx), ptr<float>(part), M, D, rpb);
   PCMP_LAUNCH_CHECK();
   auto red = at::empty({2 * D}, mean.options());
-  hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(2 * D, 256)), dim3(256), 0, cur_stream(), ptr<float>(part), T,
-                     2 * D, ptr<float>(red), 0);
-  PCMP_LAUNCH_CHECK();
+  launch_col_reduce(ptr<float>(part), T, 2 * D, ptr<float>(red), false, cur_stream());
   if (dg.has_value() && dg->defined()) {
     if (accumulate) dg->add_(red.narrow(0, 0, D)); else dg->copy_(red.narrow(0, 0, D));
   }

@@ -249,3 +249,14 @@ def test_input_conversion(gpu):
     close(_ops().nchw_to_nhwc(x, 8, 1.0, None, None), ref.nchw_to_nhwc(x, 8, 1.0), 0, 1e-2)
     xu = (torch.rand(2, 3, 9, 11, device=gpu) * 255).to(torch.uint8)
     close(_ops().nchw_to_nhwc(xu, 8, 1 / 255, None, None), ref.nchw_to_nhwc(xu, 8, 1 / 255), 0, 1e-2)
+
+
+@pytest.mark.parametrize("M,C", [(4096, 768), (4096, 3072), (37, 24), (256, 1000 + 8), (1, 64)])
+def test_colsum_bias_grad(gpu, M, C):
+    x = rnd(M, C, dev=gpu)
+    ref_sum = x.float().sum(0)
+    out = torch.empty(C, device=gpu)
+    _ops().colsum(x, out, False)
+    close(out, ref_sum, rtol=1e-4, atol=1e-3)
+    _ops().colsum(x, out, True)
+    close(out, 2 * ref_sum, rtol=1e-4, atol=2e-3)
