@@ -46,3 +46,21 @@ def test_format_time_and_accuracy():
 def test_latency_stats():
     s = R.latency_stats([0.001] * 98 + [0.01, 0.02])
     assert abs(s["p50_ms"] - 1.0) < 1e-9 and s["n"] == 100 and s["p99_ms"] > 9.0
+
+
+def test_device_report_cpu_and_seeding():
+    import random
+
+    import numpy as np
+    import torch
+
+    from pcmp.parallel.launch import device_report
+    from pcmp.utils.misc import seed_everything
+    out = []
+    dev = device_report(0, printer=lambda *a: out.append(" ".join(str(x) for x in a)))
+    if not torch.cuda.is_available():
+        assert out == ["No GPU. switching to CPU"] and dev.type == "cpu"
+    seed_everything(42)
+    a = (random.random(), float(np.random.rand()), float(torch.rand(1)))
+    seed_everything(42)
+    assert a == (random.random(), float(np.random.rand()), float(torch.rand(1)))
