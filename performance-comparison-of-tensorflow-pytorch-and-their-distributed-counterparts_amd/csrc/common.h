@@ -84,6 +84,11 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 #define PCMP_CHECK_BF16(x) TORCH_CHECK((x).scalar_type() == at::kBFloat16, #x " must be bf16")
 #define PCMP_CHECK_F32(x) TORCH_CHECK((x).scalar_type() == at::kFloat, #x " must be fp32")
 #define PCMP_LAUNCH_CHECK() C10_HIP_KERNEL_LAUNCH_CHECK()
+#define PCMP_HIP_CHECK(expr)                                                                  \
+  do {                                                                                        \
+    const hipError_t e_ = (expr);                                                             \
+    TORCH_CHECK(e_ == hipSuccess, #expr " failed: ", hipGetErrorString(e_));                  \
+  } while (0)
 
 template <typename T>
 inline T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }

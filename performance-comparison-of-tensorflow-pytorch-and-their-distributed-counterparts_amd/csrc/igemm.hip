@@ -77,6 +77,7 @@ struct IgemmParams {
   // apply of an intermediate layer); used when bn_mask is null
   const float* bn_msc;
   const float* bn_msh;
+  int stats_cap;   // BM-row tiles the stats / stats2 buffers hold (host-side bounds check)
 };
 
 constexpr int BK = 64;
@@ -140,6 +141,243 @@ __device__ __forceinline__ int chan_perm(int rho) {
 // Epilogue variants (FWD/DGRAD): plain store, + BatchNorm partial statistics of the stored output
 // (FWD training), + fused BatchNorm-backward reduction (DGRAD; BNR2: two BNs share the gradient).
 enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNR = 2, EPI_BNR2 = 3 };
+
+// FWD/DGRAD epilogue shared by the 4-wave and 8-wave kernels.  acc[j][i] holds the D^T fragment of
+// MFMA column tile j (4 output channels, PAIR-permuted) x row tile i (16 pixels).
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int NTHR>
+__device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&acc)[BN / WN / 16][BM / WM / 16],
+                                                  char* smem, int tid, int m0, int n0, int tile_m, int split) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr bool PAIR = (TN % 2 == 0);
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  {
+    // lane holds 4 channels chan(j) .. chan(j)+3 per MFMA column tile j of pixel m = m0 + wr*WTM + 16i + fr
+    auto chan = [&](int j) {   // channel offset inside the BN tile of acc[j][*][0]
+      return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
+    };
+    if (p.nsplit > 1) {
+      // split-K forward (small-M inference shapes): raw fp32 partials, epilogue in the reduction
+      float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wr * WTM + i * 16 + fr;
+        if (m >= p.gm) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + chan(j);
+          if (n < p.gn) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[j][i];
+        }
+      }
+      return;
+    }
+    __bf16* out = reinterpret_cast<__bf16*>(p.out);
+    constexpr int VW = PAIR ? 8 : 4;          // channels per store
+    constexpr int NV = TN * 4 / VW;           // stores per pixel row
+    constexpr int NP = VW / 2;                // packed bf16 pairs per store
+    constexpr bool stats = EPI == EPI_STATS;
+    constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
+    constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
+    constexpr int NS = bnr2 ? 3 : 2;          // per-channel sums kept
+    float sm[NS][TN][4];
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
+    const bool has_res = p.resid != nullptr;
+    const bool has_mk = bnr && p.bn_mask != nullptr;
+    const bool mfx = bnr && !has_mk && p.bn_msc != nullptr;   // ReLU mask recomputed from x
+    // output row offsets of the TM pixel-row groups
+    size_t orows[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + i * 16 + fr;
+      size_t orow = m < p.gm ? m : 0;
+      if constexpr (MODE == MODE_DGRAD) {
+        if (p.sub && m < p.gm) {
+          const int n = fdiv(m, p.fd_HW);
+          const int rem = m - n * p.dH * p.dW;
+          const int hh = fdiv(rem, p.fd_W);
+          const int ww = rem - hh * p.dW;
+          orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
+        }
+      }
+      orows[i] = orow;
+    }
+    // Stores walk (i outer, v inner: the two 64-B halves of a pixel's 128-B channel run are stored
+    // back to back); the resid / mask / x operand loads of step t+1 are issued before the math of
+    // step t (one-deep software pipeline).
+    unsigned rvA[2][NP], mkA[2][NP], xvA[2][NP], xv2A[2][NP];
+    auto issue = [&](int t, int b) {
+      const int i = t / NV, v = t % NV;
+      const int m = m0 + wr * WTM + i * 16 + fr;
+      const int n = n0 + chan(v * (VW / 4));
+      const bool ok = m < p.gm && n < p.gn;
+      const size_t o = orows[i] * p.gn + (ok ? n : 0);
+      auto ldv = [&](unsigned* d, const __bf16* src) {
+        if constexpr (VW == 8) {
+          const uint4 t4 = ok ? *reinterpret_cast<const uint4*>(src + o) : uint4{0, 0, 0, 0};
+          d[0] = t4.x; d[1] = t4.y; d[2] = t4.z; d[3] = t4.w;
+        } else {
+          const uint2 t2 = ok ? *reinterpret_cast<const uint2*>(src + o) : uint2{0, 0};
+          d[0] = t2.x; d[1] = t2.y;
+        }
+      };
+      if (has_res) ldv(rvA[b], p.resid);
+      if constexpr (bnr) {
+        if (has_mk) ldv(mkA[b], p.bn_mask);
+        ldv(xvA[b], p.bn_x);
+        if constexpr (bnr2) ldv(xv2A[b], p.bn_x2);
+      }
+    };
+    if (has_res || bnr) issue(0, 0);
+    // per-channel coefficient tables of the tile's BN columns, staged once in LDS (stage buffers
+    // are dead; the column-sum scratch that reuses this space is written after a barrier)
+    float* ctab = reinterpret_cast<float*>(smem);
+    const bool has_bias = MODE == MODE_FWD && p.bias != nullptr;
+    if (bnr || has_bias) {
+      for (int idx = tid; idx < BN; idx += NTHR) {
+        const int c = min(n0 + idx, p.gn - 1);
+        if (has_bias) ctab[idx] = p.bias[c];
+        if constexpr (bnr) {
+          const float is = p.bn_istd[c];
+          ctab[0 * BN + idx] = is;
+          ctab[1 * BN + idx] = -p.bn_mean[c] * is;
+          ctab[2 * BN + idx] = mfx ? p.bn_msc[c] : 0.f;
+          ctab[3 * BN + idx] = mfx ? p.bn_msh[c] : 0.f;
+          if constexpr (bnr2) {
+            const float is2 = p.bn_istd2[c];
+            ctab[4 * BN + idx] = is2;
+            ctab[5 * BN + idx] = -p.bn_mean2[c] * is2;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    auto ldt = [&](float* d, int tab, int j0) {
+#pragma unroll
+      for (int e4 = 0; e4 < VW; e4 += 4) {
+        const f32x4 t4 = *reinterpret_cast<const f32x4*>(ctab + tab * BN + chan(j0) + e4);
+        d[e4] = t4[0]; d[e4 + 1] = t4[1]; d[e4 + 2] = t4[2]; d[e4 + 3] = t4[3];
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + i * 16 + fr;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int t = i * NV + v, b = t & 1;
+        if ((has_res || bnr) && t + 1 < NV * TM) issue(t + 1, (t + 1) & 1);
+        const int j0 = v * (VW / 4);
+        const int n = n0 + chan(j0);
+        if (m >= p.gm || n >= p.gn) continue;
+        const size_t o = orows[i] * p.gn + n;
+        float bias[VW], ka[VW], kb[VW], ka2[VW], kb2[VW], msc[VW], msh[VW];
+        if (has_bias) ldt(bias, 0, j0);
+        else {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) bias[e] = 0.f;
+        }
+        if constexpr (bnr) {
+          ldt(ka, 0, j0); ldt(kb, 1, j0);
+          if (mfx) { ldt(msc, 2, j0); ldt(msh, 3, j0); }
+          if constexpr (bnr2) { ldt(ka2, 4, j0); ldt(kb2, 5, j0); }
+        }
+        unsigned ov[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          const int j = j0 + (q >> 1), e0 = (q & 1) * 2, ce = 2 * q;   // ce: channel within the store
+          float x0 = acc[j][i][e0] + bias[ce];
+          float x1 = acc[j][i][e0 + 1] + bias[ce + 1];
+          if (has_res) {
+            x0 += __uint_as_float(rvA[b][q] << 16);
+            x1 += __uint_as_float(rvA[b][q] & 0xffff0000u);
+          }
+          if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+          unsigned u = f2bf2(x0, x1);
+          if constexpr (bnr) {
+            const float xa = __uint_as_float(xvA[b][q] << 16), xb = __uint_as_float(xvA[b][q] & 0xffff0000u);
+            // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
+            if (has_mk) {
+              const unsigned y = mkA[b][q];
+              const unsigned keep = (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
+                                    (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
+              u &= keep;
+            } else if (mfx) {
+              const float z0 = fmaf(xa, msc[ce], msh[ce]);
+              const float z1 = fmaf(xb, msc[ce + 1], msh[ce + 1]);
+              u &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
+            }
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+            sm[1][j][e0] += r0 * fmaf(xa, ka[ce], kb[ce]);
+            sm[1][j][e0 + 1] += r1 * fmaf(xb, ka[ce + 1], kb[ce + 1]);
+            if constexpr (bnr2) {
+              sm[2][j][e0] += r0 * fmaf(__uint_as_float(xv2A[b][q] << 16), ka2[ce], kb2[ce]);
+              sm[2][j][e0 + 1] += r1 * fmaf(__uint_as_float(xv2A[b][q] & 0xffff0000u), ka2[ce + 1], kb2[ce + 1]);
+            }
+          } else if constexpr (stats) {
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+            sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
+          }
+          ov[q] = u;
+        }
+        if constexpr (VW == 8) *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(ov);
+        else *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<const uint2*>(ov);
+      }
+    }
+    if constexpr (stats || bnr) {
+      // Column sums over the tile's pixels: each wave transposes its lanes' partial sums through
+      // LDS ([16 pixel rows][NS][WTN], padded rows) and every lane then sums 16 values for its
+      // (k, channel) pairs -- ~3 LDS ops per value instead of a 4-step cross-lane reduction.
+      constexpr int RS = NS * WTN + 4;
+      float* tb = reinterpret_cast<float*>(smem) + wid * 16 * RS;
+      float* red = reinterpret_cast<float*>(smem) + (NTHR / 64) * 16 * RS;   // [WM][NS][BN]
+      __syncthreads();   // stage buffers are dead from here on
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(tb + fr * RS + k * WTN + chan(j) - wc * WTN) =
+              f32x4{sm[k][j][0], sm[k][j][1], sm[k][j][2], sm[k][j][3]};
+      __syncthreads();
+#pragma unroll
+      for (int idx = lane; idx < NS * WTN; idx += 64) {
+        const int k = idx / WTN, ch = idx - k * WTN;
+        float t = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += tb[r * RS + k * WTN + ch];
+        red[(wr * NS + k) * BN + wc * WTN + ch] = t;
+      }
+      __syncthreads();
+      float* st = p.stats + (size_t)tile_m * 2 * p.gn;
+      float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
+      for (int i = tid; i < BN; i += NTHR) {
+        const int c = n0 + i;
+        if (c < p.gn) {
+          float t[NS];
+#pragma unroll
+          for (int k = 0; k < NS; ++k) {
+            t[k] = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) t[k] += red[(w * NS + k) * BN + i];
+          }
+          st[c] = t[0];
+          st[p.gn + c] = t[1];
+          if constexpr (bnr2) {
+            st2[c] = t[0];
+            st2[p.gn + c] = t[2];
+          }
+        }
+      }
+    }
+  }
+}
 
 template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI>
 __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
@@ -452,229 +690,221 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       }
     return;
   } else {
-    // lane holds 4 channels chan(j) .. chan(j)+3 per MFMA column tile j of pixel m = m0 + wr*WTM + 16i + fr
-    auto chan = [&](int j) {   // channel offset inside the BN tile of acc[j][*][0]
-      return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
-    };
-    if (p.nsplit > 1) {
-      // split-K forward (small-M inference shapes): raw fp32 partials, epilogue in the reduction
-      float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wr * WTM + i * 16 + fr;
-        if (m >= p.gm) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + chan(j);
-          if (n < p.gn) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[j][i];
-        }
-      }
-      return;
-    }
-    __bf16* out = reinterpret_cast<__bf16*>(p.out);
-    constexpr int VW = PAIR ? 8 : 4;          // channels per store
-    constexpr int NV = TN * 4 / VW;           // stores per pixel row
-    constexpr int NP = VW / 2;                // packed bf16 pairs per store
-    constexpr bool stats = EPI == EPI_STATS;
-    constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
-    constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
-    constexpr int NS = bnr2 ? 3 : 2;          // per-channel sums kept
-    float sm[NS][TN][4];
-#pragma unroll
-    for (int k = 0; k < NS; ++k)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
-    const bool has_res = p.resid != nullptr;
-    const bool has_mk = bnr && p.bn_mask != nullptr;
-    const bool mfx = bnr && !has_mk && p.bn_msc != nullptr;   // ReLU mask recomputed from x
-    // output row offsets of the TM pixel-row groups
-    size_t orows[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wr * WTM + i * 16 + fr;
-      size_t orow = m < p.gm ? m : 0;
-      if constexpr (MODE == MODE_DGRAD) {
-        if (p.sub && m < p.gm) {
-          const int n = fdiv(m, p.fd_HW);
-          const int rem = m - n * p.dH * p.dW;
-          const int hh = fdiv(rem, p.fd_W);
-          const int ww = rem - hh * p.dW;
-          orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
-        }
-      }
-      orows[i] = orow;
-    }
-    // Stores walk (i outer, v inner: the two 64-B halves of a pixel's 128-B channel run are stored
-    // back to back); the resid / mask / x operand loads of step t+1 are issued before the math of
-    // step t (one-deep software pipeline).
-    unsigned rvA[2][NP], mkA[2][NP], xvA[2][NP], xv2A[2][NP];
-    auto issue = [&](int t, int b) {
-      const int i = t / NV, v = t % NV;
-      const int m = m0 + wr * WTM + i * 16 + fr;
-      const int n = n0 + chan(v * (VW / 4));
-      const bool ok = m < p.gm && n < p.gn;
-      const size_t o = orows[i] * p.gn + (ok ? n : 0);
-      auto ldv = [&](unsigned* d, const __bf16* src) {
-        if constexpr (VW == 8) {
-          const uint4 t4 = ok ? *reinterpret_cast<const uint4*>(src + o) : uint4{0, 0, 0, 0};
-          d[0] = t4.x; d[1] = t4.y; d[2] = t4.z; d[3] = t4.w;
-        } else {
-          const uint2 t2 = ok ? *reinterpret_cast<const uint2*>(src + o) : uint2{0, 0};
-          d[0] = t2.x; d[1] = t2.y;
-        }
-      };
-      if (has_res) ldv(rvA[b], p.resid);
-      if constexpr (bnr) {
-        if (has_mk) ldv(mkA[b], p.bn_mask);
-        ldv(xvA[b], p.bn_x);
-        if constexpr (bnr2) ldv(xv2A[b], p.bn_x2);
-      }
-    };
-    if (has_res || bnr) issue(0, 0);
-    // per-channel coefficient tables of the tile's BN columns, staged once in LDS (stage buffers
-    // are dead; the column-sum scratch that reuses this space is written after a barrier)
-    float* ctab = reinterpret_cast<float*>(smem);
-    const bool has_bias = MODE == MODE_FWD && p.bias != nullptr;
-    if (bnr || has_bias) {
-      for (int idx = tid; idx < BN; idx += NT) {
-        const int c = min(n0 + idx, p.gn - 1);
-        if (has_bias) ctab[idx] = p.bias[c];
-        if constexpr (bnr) {
-          const float is = p.bn_istd[c];
-          ctab[0 * BN + idx] = is;
-          ctab[1 * BN + idx] = -p.bn_mean[c] * is;
-          ctab[2 * BN + idx] = mfx ? p.bn_msc[c] : 0.f;
-          ctab[3 * BN + idx] = mfx ? p.bn_msh[c] : 0.f;
-          if constexpr (bnr2) {
-            const float is2 = p.bn_istd2[c];
-            ctab[4 * BN + idx] = is2;
-            ctab[5 * BN + idx] = -p.bn_mean2[c] * is2;
-          }
-        }
-      }
-      __syncthreads();
-    }
-    auto ldt = [&](float* d, int tab, int j0) {
-#pragma unroll
-      for (int e4 = 0; e4 < VW; e4 += 4) {
-        const f32x4 t4 = *reinterpret_cast<const f32x4*>(ctab + tab * BN + chan(j0) + e4);
-        d[e4] = t4[0]; d[e4 + 1] = t4[1]; d[e4 + 2] = t4[2]; d[e4 + 3] = t4[3];
-      }
-    };
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wr * WTM + i * 16 + fr;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int t = i * NV + v, b = t & 1;
-        if ((has_res || bnr) && t + 1 < NV * TM) issue(t + 1, (t + 1) & 1);
-        const int j0 = v * (VW / 4);
-        const int n = n0 + chan(j0);
-        if (m >= p.gm || n >= p.gn) continue;
-        const size_t o = orows[i] * p.gn + n;
-        float bias[VW], ka[VW], kb[VW], ka2[VW], kb2[VW], msc[VW], msh[VW];
-        if (has_bias) ldt(bias, 0, j0);
-        else {
-#pragma unroll
-          for (int e = 0; e < VW; ++e) bias[e] = 0.f;
-        }
-        if constexpr (bnr) {
-          ldt(ka, 0, j0); ldt(kb, 1, j0);
-          if (mfx) { ldt(msc, 2, j0); ldt(msh, 3, j0); }
-          if constexpr (bnr2) { ldt(ka2, 4, j0); ldt(kb2, 5, j0); }
-        }
-        unsigned ov[NP];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {
-          const int j = j0 + (q >> 1), e0 = (q & 1) * 2, ce = 2 * q;   // ce: channel within the store
-          float x0 = acc[j][i][e0] + bias[ce];
-          float x1 = acc[j][i][e0 + 1] + bias[ce + 1];
-          if (has_res) {
-            x0 += __uint_as_float(rvA[b][q] << 16);
-            x1 += __uint_as_float(rvA[b][q] & 0xffff0000u);
-          }
-          if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
-          unsigned u = f2bf2(x0, x1);
-          if constexpr (bnr) {
-            const float xa = __uint_as_float(xvA[b][q] << 16), xb = __uint_as_float(xvA[b][q] & 0xffff0000u);
-            // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
-            if (has_mk) {
-              const unsigned y = mkA[b][q];
-              const unsigned keep = (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
-                                    (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
-              u &= keep;
-            } else if (mfx) {
-              const float z0 = fmaf(xa, msc[ce], msh[ce]);
-              const float z1 = fmaf(xb, msc[ce + 1], msh[ce + 1]);
-              u &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
-            }
-            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
-            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
-            sm[1][j][e0] += r0 * fmaf(xa, ka[ce], kb[ce]);
-            sm[1][j][e0 + 1] += r1 * fmaf(xb, ka[ce + 1], kb[ce + 1]);
-            if constexpr (bnr2) {
-              sm[2][j][e0] += r0 * fmaf(__uint_as_float(xv2A[b][q] << 16), ka2[ce], kb2[ce]);
-              sm[2][j][e0 + 1] += r1 * fmaf(__uint_as_float(xv2A[b][q] & 0xffff0000u), ka2[ce + 1], kb2[ce + 1]);
-            }
-          } else if constexpr (stats) {
-            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
-            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
-            sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
-          }
-          ov[q] = u;
-        }
-        if constexpr (VW == 8) *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(ov);
-        else *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<const uint2*>(ov);
-      }
-    }
-    if constexpr (stats || bnr) {
-      // Column sums over the tile's pixels: each wave transposes its lanes' partial sums through
-      // LDS ([16 pixel rows][NS][WTN], padded rows) and every lane then sums 16 values for its
-      // (k, channel) pairs -- ~3 LDS ops per value instead of a 4-step cross-lane reduction.
-      constexpr int RS = NS * WTN + 4;
-      float* tb = reinterpret_cast<float*>(smem) + wid * 16 * RS;
-      float* red = reinterpret_cast<float*>(smem) + 4 * 16 * RS;   // [WM][NS][BN]
-      __syncthreads();   // stage buffers are dead from here on
-#pragma unroll
-      for (int k = 0; k < NS; ++k)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          *reinterpret_cast<f32x4*>(tb + fr * RS + k * WTN + chan(j) - wc * WTN) =
-              f32x4{sm[k][j][0], sm[k][j][1], sm[k][j][2], sm[k][j][3]};
-      __syncthreads();
-#pragma unroll
-      for (int idx = lane; idx < NS * WTN; idx += 64) {
-        const int k = idx / WTN, ch = idx - k * WTN;
-        float t = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += tb[r * RS + k * WTN + ch];
-        red[(wr * NS + k) * BN + wc * WTN + ch] = t;
-      }
-      __syncthreads();
-      float* st = p.stats + (size_t)tile_m * 2 * p.gn;
-      float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
-      for (int i = tid; i < BN; i += NT) {
-        const int c = n0 + i;
-        if (c < p.gn) {
-          float t[NS];
-#pragma unroll
-          for (int k = 0; k < NS; ++k) {
-            t[k] = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) t[k] += red[(w * NS + k) * BN + i];
-          }
-          st[c] = t[0];
-          st[p.gn + c] = t[1];
-          if constexpr (bnr2) {
-            st2[c] = t[0];
-            st2[p.gn + c] = t[2];
-          }
-        }
-      }
-    }
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT>(p, acc, smem, tid, m0, n0, tile_m, split);
   }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// 8-wave LDS-DMA kernel for the large FWD/DGRAD GEMMs (BM = 256 pixels x BN = 256|128 channels,
+// 512 threads, ~1 block per CU).  Operand tiles are staged global -> LDS by buffer_load ... lds
+// (LDS-DMA: no VGPR round trip, hardware zero-fill for padding / tails through the buffer range
+// check); the XOR swizzle of the row-read image is applied to the per-lane SOURCE chunk and undone
+// on the ds_read (cdna_hip_programming.md §5.4 rule 21).  Each K-tile (BK = 64) is computed in
+// four phases, one output quadrant per phase (16/8 MFMAs per wave); during phase p of tile t the
+// p-th half-tile of tile t+1 is DMA'd into the other LDS buffer, and counted s_waitcnt vmcnt(N)
+// waits retire exactly the half-tile the next phase reads, so operand loads stay in flight across
+// the barriers instead of draining every K-step.  Half-tile issue order (A0, B0, B1, A1) follows
+// the quadrant order (0,0) (0,1) (1,1) (1,0) of the consumer.
+constexpr int NT8 = 512;
+constexpr int BM8 = 256;
+template <int BN> struct G8Cfg;
+template <> struct G8Cfg<256> { static constexpr int WM = 2, WN = 4; };
+template <> struct G8Cfg<128> { static constexpr int WM = 4, WN = 2; };   // (not dispatched: see use_igemm8)
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int MODE, int BN, int EPI, bool PRIO>
+__global__ void __launch_bounds__(NT8, 1) igemm8_kernel(const IgemmParams p) {
+  constexpr int BM = BM8;
+  constexpr int WM = G8Cfg<BN>::WM, WN = G8Cfg<BN>::WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;   // 128x64 (BN 256) or 64x64 (BN 128)
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int TMH = TM / 2, TNH = TN / 2;     // fragments per quadrant
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NA = 2;                         // LDS-DMA instructions per thread per A half-tile
+  constexpr int NB = BN / 128;                  // ... per B half-tile (BN/2 rows)
+  constexpr int AH = WTM / 2;                   // rows of one wave-row segment of an A half
+  static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
+  static_assert(TM % 2 == 0 && TN % 2 == 0, "quadrants");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lin % p.tiles_n;
+  const int tile_m = lin / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk = (p.gk + BK - 1) / BK;
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+
+  // ---- loader slots: each DMA instruction writes 8 consecutive LDS rows (1 KB); lane -> (row
+  // base + lane/8, chunk position lane%8) and loads global chunk (lane%8) ^ (row & 7)
+  const int gch = (lane & 7) ^ (lane >> 3);
+  int a_off[2][NA], a_y[2][NA], a_x[2][NA], a_lds[2][NA];
+  int b_off[2][NB], b_lds[2][NB];
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int h0 = wid * (8 * NA) + i * 8;                 // first half-row of this instruction
+      const int row0 = (h0 / AH) * WTM + mh * AH + h0 % AH;  // logical (= LDS) row of lane 0
+      a_lds[mh][i] = row0 * (BK * 2);
+      const int m = m0 + row0 + (lane >> 3);
+      const bool v = m < p.gm;
+      const int mm = v ? m : 0;
+      if constexpr (MODE == MODE_FWD) {
+        const int n = fdiv(mm, p.fd_PQ);
+        const int rem = mm - n * p.P * p.Q;
+        const int pp = fdiv(rem, p.fd_Q);
+        const int qq = rem - pp * p.Q;
+        const int yv = pp * p.stride - p.pad;
+        a_y[mh][i] = v ? yv : -(1 << 28);
+        a_x[mh][i] = qq * p.stride - p.pad;
+        a_off[mh][i] = ((n * p.H + yv) * p.W + a_x[mh][i]) * p.C + gch * 8;
+      } else {
+        const int n = fdiv(mm, p.fd_HW);
+        const int rem = mm - n * p.dH * p.dW;
+        const int hh = fdiv(rem, p.fd_W);
+        const int ww = rem - hh * p.dW;
+        const int yv = hh + p.offy;
+        a_y[mh][i] = v ? yv : -(1 << 28);
+        a_x[mh][i] = ww + p.offx;
+        a_off[mh][i] = ((n * p.P + yv) * p.Q + a_x[mh][i]) * p.K + gch * 8;
+      }
+    }
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int h0 = wid * (8 * NB) + i * 8;
+      const int rho0 = (h0 / 32) * WTN + nh * 32 + h0 % 32;
+      b_lds[nh][i] = A_BYTES + rho0 * (BK * 2);
+      const int n = n0 + chan_perm<true>(rho0 + (lane >> 3));
+      b_off[nh][i] = n < p.gn ? n * p.gk + gch * 8 : -1;
+    }
+
+  // uniform tap / channel state of the next K-tile to load (C or K is a multiple of BK)
+  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
+  int kr = 0, ks = 0, kc = 0, k0 = 0;
+  auto issue_a = [&](int mh, int buf) {
+    int tap;
+    if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
+    else tap = -(kr * p.Q + ks) * p.K + kc;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      bool ok;
+      if constexpr (MODE == MODE_FWD)
+        ok = (unsigned)(a_y[mh][i] + kr) < (unsigned)p.H && (unsigned)(a_x[mh][i] + ks) < (unsigned)p.W;
+      else
+        ok = (unsigned)(a_y[mh][i] - kr) < (unsigned)p.P && (unsigned)(a_x[mh][i] - ks) < (unsigned)p.Q;
+      const unsigned voff = ok ? (unsigned)(a_off[mh][i] + tap) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(smem + buf * STAGE + a_lds[mh][i]),
+                                               16, voff, 0, 0, 0);
+    }
+  };
+  auto issue_b = [&](int nh, int buf) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const unsigned voff = b_off[nh][i] >= 0 ? (unsigned)(b_off[nh][i] + k0) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(smem + buf * STAGE + b_lds[nh][i]),
+                                               16, voff, 0, 0, 0);
+    }
+  };
+  auto advance = [&]() {
+    k0 += BK;
+    kc += BK;
+    if (kc >= CIN) {
+      kc = 0;
+      if (++ks == p.S) { ks = 0; ++kr; }
+    }
+  };
+
+  bf16x8 fa[TMH][2], fb[2][TNH][2];
+  auto read_a = [&](int mh, int buf) {
+    const char* sA = smem + buf * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < TMH; ++i) {
+        const int row = wr * WTM + mh * AH + i * 16 + (lane & 15);
+        fa[i][kk] = *reinterpret_cast<const bf16x8*>(sA + rr_off(row, kk * 4 + (lane >> 4)));
+      }
+  };
+  auto read_b = [&](int nh, int buf) {
+    const char* sB = smem + buf * STAGE + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < TNH; ++j) {
+        const int row = wc * WTN + nh * 32 + j * 16 + (lane & 15);
+        fb[nh][j][kk] = *reinterpret_cast<const bf16x8*>(sB + rr_off(row, kk * 4 + (lane >> 4)));
+      }
+  };
+  auto mma = [&](int mh, int nh) {
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < TNH; ++j)
+#pragma unroll
+        for (int i = 0; i < TMH; ++i)
+          acc[nh * TNH + j][mh * TMH + i] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][j][kk], fa[i][kk], acc[nh * TNH + j][mh * TMH + i], 0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- prologue: tile 0 complete in buffer 0
+  issue_a(0, 0); issue_b(0, 0); issue_b(1, 0); issue_a(1, 0);
+  advance();
+  wait_vm<0>();
+  lds_barrier();
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1, nb = buf ^ 1;
+    const bool nxt = t + 1 < nk;
+    // phase 0: quadrant (0,0); DMA A0 of t+1
+    read_a(0, buf); read_b(0, buf);
+    if (nxt) issue_a(0, nb);
+    mma(0, 0);
+    if (nxt) wait_vm<2 * NA>(); else wait_vm<NA>();     // retire B1(t)
+    lds_barrier();
+    // phase 1: quadrant (0,1); DMA B0 of t+1
+    read_b(1, buf);
+    if (nxt) issue_b(0, nb);
+    mma(0, 1);
+    if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A1(t)
+    lds_barrier();
+    // phase 2: quadrant (1,1); DMA B1 of t+1 (nothing to retire: phase 3 re-reads B0(t))
+    read_a(1, buf);
+    if (nxt) issue_b(1, nb);
+    mma(1, 1);
+    // phase 3: quadrant (1,0); DMA A1 of t+1
+    read_b(0, buf);
+    if (nxt) { issue_a(1, nb); advance(); }
+    mma(1, 0);
+    if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A0(t+1), B0(t+1)
+    lds_barrier();
+  }
+  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT8>(p, acc, smem, tid, m0, n0, tile_m, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -748,6 +978,7 @@ template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
+  TORCH_CHECK(MODE == MODE_WGRAD || !p.stats || p.tiles_m <= p.stats_cap, "igemm: partial-stats buffer too small");
   const int grid = p.tiles_m * p.tiles_n * p.nsplit;
   const size_t stage_bytes = (size_t)(BM + BN) * BK * 2;
   const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
@@ -785,8 +1016,78 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
+static int igemm8_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("PCMP_IGEMM8");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int MODE, int BN>
+static void launch8(IgemmParams& p, hipStream_t st) {
+  constexpr int WM = G8Cfg<BN>::WM, WN = G8Cfg<BN>::WN;
+  p.tiles_m = ceil_div(p.gm, BM8);
+  p.tiles_n = ceil_div(p.gn, BN);
+  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm8: partial-stats buffer too small");
+  const int grid = p.tiles_m * p.tiles_n;
+  size_t smem = (size_t)2 * (BM8 + BN) * BK * 2;
+  const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
+  if (epi_red) {
+    const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
+    smem = std::max(smem, (size_t)((NT8 / 64) * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
+  }
+  int epi = EPI_PLAIN;
+  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
+  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
+#define PCMP_IGEMM8_LAUNCH_P(E, PR)                                                                    \
+  do {                                                                                                \
+    static bool attr_set = false;                                                                     \
+    if (!attr_set) {                                                                                  \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm8_kernel<MODE, BN, E, PR>), \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
+      attr_set = true;                                                                                \
+    }                                                                                                 \
+    hipLaunchKernelGGL((igemm8_kernel<MODE, BN, E, PR>), dim3(grid), dim3(NT8), smem, st, p);         \
+  } while (0)
+#define PCMP_IGEMM8_LAUNCH(E) PCMP_IGEMM8_LAUNCH_P(E, false)
+  if constexpr (MODE == MODE_FWD) {
+    if (epi == EPI_STATS) PCMP_IGEMM8_LAUNCH(EPI_STATS); else PCMP_IGEMM8_LAUNCH(EPI_PLAIN);
+  } else {
+    TORCH_CHECK(epi != EPI_BNR2, "igemm8: dual BN-reduce epilogue not instantiated");
+    if (epi == EPI_BNR) PCMP_IGEMM8_LAUNCH(EPI_BNR);
+    else PCMP_IGEMM8_LAUNCH(EPI_PLAIN);
+  }
+#undef PCMP_IGEMM8_LAUNCH
+#undef PCMP_IGEMM8_LAUNCH_P
+  PCMP_LAUNCH_CHECK();
+}
+
+// 8-wave LDS-DMA kernel eligibility: FWD/DGRAD with the block-uniform tap walk (source channels a
+// multiple of BK), no split-K, enough K-tiles for the phase pipeline, and a grid that still covers
+// every CU with BM = 256 tiles.  PCMP_IGEMM8=0 disables it (A/B runs).
+static int use_igemm8(int mode, const IgemmParams& p) {
+  if (!igemm8_mode() || mode == MODE_WGRAD || p.nsplit != 1) return 0;
+  const int cin = mode == MODE_FWD ? p.C : p.K;
+  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < 4 || p.gn < 256) return 0;
+  // (measured: the BN=128 variant does not beat the 4-wave 128x128 kernel; the dual BN-reduce
+  //  epilogue of a 128x64 wave tile spills)
+  if (mode == MODE_DGRAD && p.bn_x2) return 0;
+  if (ceil_div(p.gm, BM8) * ceil_div(p.gn, 256) < 240) return 0;
+  return 256;
+}
+
+// BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
+static int igemm_bm(int mode, const IgemmParams& p) {
+  if (use_igemm8(mode, p)) return BM8;
+  return p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
+}
+
 template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
+  if constexpr (MODE != MODE_WGRAD) {
+    if (use_igemm8(MODE, p) == 256) { launch8<MODE, 256>(p, st); return; }
+  }
   // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)
   if (p.gm <= 32) {
     if (p.gn <= 64) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
@@ -820,6 +1121,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.stats2 = nullptr;
   p.bn_mask = nullptr; p.bn_x = nullptr; p.bn_mean = nullptr; p.bn_istd = nullptr;
   p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr; p.bn_msc = nullptr; p.bn_msh = nullptr;
+  p.stats_cap = 0;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
 }
 
@@ -854,7 +1156,8 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   const int BNsel = p.gn <= 64 ? 64 : 128;
   at::Tensor stats;
   if (want_stats) {
-    stats = at::empty({ceil_div(p.gm, BMsel), 2, K}, x.options().dtype(at::kFloat));
+    p.stats_cap = ceil_div(p.gm, igemm_bm(MODE_FWD, p));
+    stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
     p.stats = ptr<float>(stats);
   }
   auto st = cur_stream();
@@ -912,8 +1215,6 @@ struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (s
   const float* msh = nullptr;
 };
 
-static int bm_for(int gm) { return gm <= 32 ? 32 : (gm <= 64 ? 64 : 128); }
-
 static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
                                           int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
                                           const BnrArgs* bn) {
@@ -954,16 +1255,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
         }
         cls.push_back({oph, opw, r0, s0, subR, subS, dH, dW});
       }
-    at::Tensor part, part2;
-    if (bn) {
-      int T = 0;
-      for (auto& c : cls) T += ceil_div(N * c.dH * c.dW, bm_for(N * c.dH * c.dW));
-      part = at::empty({T, 2, C}, fopts);
-      if (two) part2 = at::empty({T, 2, C}, fopts);
-    }
-    int toff = 0;
-    for (auto& c : cls) {
-      at::Tensor wt = transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st);
+    auto class_params = [&](const Cls& c, const at::Tensor& wt) {
       IgemmParams q = p;
       q.R = c.subR; q.S = c.subS;
       q.sub = 1; q.oph = c.oph; q.opw = c.opw;
@@ -973,15 +1265,33 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
       q.offy = (c.oph + pad - c.r0) / 2;
       q.offx = (c.opw + pad - c.s0) / 2;
       q.gm = N * c.dH * c.dW; q.gn = C; q.gk = c.subR * c.subS * K;
-      q.a = ptr<__bf16>(dy); q.b = ptr<__bf16>(wt); q.out = dx.data_ptr();
-      q.a_bytes = tensor_bytes(dy); q.b_bytes = tensor_bytes(wt);
+      q.a = ptr<__bf16>(dy); q.out = dx.data_ptr();
+      q.a_bytes = tensor_bytes(dy);
+      if (wt.defined()) { q.b = ptr<__bf16>(wt); q.b_bytes = tensor_bytes(wt); }
       q.resid = ptr<__bf16>(dx);   // in-place accumulate
       q.ksplit = q.gk;
+      set_bn(q);                   // (the kernel choice, hence the partial-row count, depends on it)
+      return q;
+    };
+    at::Tensor part, part2;
+    if (bn) {
+      int T = 0;
+      for (auto& c : cls) {
+        const IgemmParams q = class_params(c, at::Tensor());
+        T += ceil_div(q.gm, igemm_bm(MODE_DGRAD, q));
+      }
+      part = at::empty({T, 2, C}, fopts);
+      if (two) part2 = at::empty({T, 2, C}, fopts);
+    }
+    int toff = 0;
+    for (auto& c : cls) {
+      at::Tensor wt = transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st);
+      IgemmParams q = class_params(c, wt);
       if (bn) {
-        set_bn(q);
         q.stats = ptr<float>(part) + (size_t)toff * 2 * C;
         if (two) q.stats2 = ptr<float>(part2) + (size_t)toff * 2 * C;
-        toff += ceil_div(q.gm, bm_for(q.gm));
+        q.stats_cap = (int)part.size(0) - toff;
+        toff += ceil_div(q.gm, igemm_bm(MODE_DGRAD, q));
       }
       dispatch<MODE_DGRAD>(q, st);
     }
@@ -998,9 +1308,10 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   p.ksplit = p.gk;
   at::Tensor part, part2;
   if (bn) {
-    const int T = ceil_div(p.gm, bm_for(p.gm));
+    set_bn(p);   // before igemm_bm: the kernel choice depends on the epilogue variant
+    const int T = ceil_div(p.gm, igemm_bm(MODE_DGRAD, p));
     part = at::empty({T, 2, C}, fopts);
-    set_bn(p);
+    p.stats_cap = T;
     p.stats = ptr<float>(part);
     if (two) { part2 = at::empty({T, 2, C}, fopts); p.stats2 = ptr<float>(part2); }
   }

@@ -260,3 +260,48 @@ def test_colsum_bias_grad(gpu, M, C):
     close(out, ref_sum, rtol=1e-4, atol=1e-3)
     _ops().colsum(x, out, True)
     close(out, 2 * ref_sum, rtol=1e-4, atol=2e-3)
+
+
+# Shapes large enough for the 8-wave LDS-DMA kernel (BM=256 tiles >= 240, >= 4 K-tiles)
+BIG_SHAPES = [
+    # N, H, W, C, K, R, stride, pad
+    (20, 56, 56, 64, 256, 3, 1, 1),     # FWD BN=256 (gn=256)
+    (20, 56, 56, 128, 128, 3, 1, 1),    # FWD/DGRAD BN=128
+    (20, 112, 112, 64, 128, 3, 2, 1),   # strided FWD; sub-pixel DGRAD classes
+    (20, 56, 56, 256, 64, 1, 1, 0),     # DGRAD gn=256 over K=64 x 1x1 -> 1 K-tile (old kernel) / FWD gk=256
+    (20, 56, 56, 256, 64, 3, 1, 1),     # DGRAD gn=256, 9 K-tiles -> 8-wave kernel incl. BN-reduce epilogue
+    (5, 56, 56, 256, 512, 3, 1, 1),     # M tail (15680 = 61.25 tiles), N = 2 x 256
+]
+
+
+@pytest.mark.parametrize("shape", BIG_SHAPES)
+def test_conv_large_shapes_8wave(gpu, shape):
+    N, H, W, C, K, R, s, p = shape
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    x = rnd(N, H, W, C, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+    y, st = _ops().conv_fwd(x, w, s, p, None, None, False, True)
+    yr, str_ = ref.conv_fwd(x, w, s, p, None, None, False, True)
+    close(y, yr)
+    close(st.sum(0), str_.sum(0), rtol=2e-2, atol=5e-1)
+    bias = torch.randn(K, device=gpu)
+    res = rnd(*yr.shape, dev=gpu)
+    close(_ops().conv_fwd(x, w, s, p, bias, res, True, False)[0], ref.conv_fwd(x, w, s, p, bias, res, True, False)[0])
+    dy = rnd(N, P, Q, K, dev=gpu)
+    wd = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * K)) ** 0.5)
+    dres = rnd(N, H, W, C, dev=gpu)
+    close(_ops().conv_dgrad(dy, wd, H, W, s, p, dres.clone()), ref.conv_dgrad(dy, wd, H, W, s, p, dres))
+    # fused BN-backward reduction (intermediate form: mask from x, and tail form: mask tensor)
+    xb = rnd(N, H, W, C, dev=gpu)
+    mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    sc, sh = torch.randn(C, device=gpu), torch.randn(C, device=gpu) * 0.5
+    out = _ops().conv_dgrad_bnr(dy, wd, H, W, s, p, None, None, xb, mean, invstd, None, None, None, sc, sh)
+    outr = ref.conv_dgrad_bnr(dy, wd, H, W, s, p, None, None, xb, mean, invstd, None, None, None, sc, sh)
+    close(out[0], outr[0])
+    close(out[1].sum(0), outr[1].sum(0), rtol=2e-2, atol=1.0)
+    ymask = rnd(N, H, W, C, dev=gpu).relu()
+    out = _ops().conv_dgrad_bnr(dy, wd, H, W, s, p, dres.clone(), ymask, xb, mean, invstd, x, mean, invstd, None, None)
+    outr = ref.conv_dgrad_bnr(dy, wd, H, W, s, p, dres, ymask, xb, mean, invstd, x, mean, invstd)
+    close(out[0], outr[0])
+    for a, b in zip(out[1:], outr[1:]):
+        close(a.sum(0), b.sum(0), rtol=2e-2, atol=1.0)
