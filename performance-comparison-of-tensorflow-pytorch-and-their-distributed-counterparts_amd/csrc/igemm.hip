@@ -972,6 +972,40 @@ __global__ void wt_transpose_kernel(const unsigned short* __restrict__ w, unsign
   }
 }
 
+// Batched weight transpose of a whole model's conv weights in ONE launch (after each optimizer
+// step, instead of one wt_transpose launch per DGRAD): desc[i] = {src_off, dst_off, K, RS, C,
+// first_block} (elements of the flat bf16 shadow / transposed-shadow buffers); block b handles one
+// 64x64 (k, c) tile of one tap of tensor i = the last i with first_block <= b.
+__global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src, unsigned short* __restrict__ dst,
+                                          const int64_t* __restrict__ desc, int n) {
+  __shared__ unsigned short tile[64][65];
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;   // binary search on first_block (block-uniform)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid * 6 + 5] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* d = desc + lo * 6;
+  const unsigned short* w = src + d[0];
+  unsigned short* wt = dst + d[1];
+  const int K = (int)d[2], T = (int)d[3], C = (int)d[4];
+  const int nc = (C + 63) / 64, nk = (K + 63) / 64;
+  int local = b - (int)d[5];
+  const int t = local / (nc * nk);
+  local -= t * nc * nk;
+  const int k0 = (local / nc) * 64, c0 = (local % nc) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + tx;
+    tile[r][tx] = (k < K && c < C) ? w[((size_t)k * T + t) * C + c] : 0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + tx;
+    if (c < C && k < K) wt[((size_t)c * T + t) * K + k] = tile[tx][r];
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 template <int MODE, int BM, int BN, int WM, int WN>
@@ -1024,6 +1058,15 @@ static int igemm8_mode() {
   return v;
 }
 
+// minimum 256x256 tile count for the 8-wave kernel (PCMP_IGEMM8_MINTILES overrides, A/B runs)
+static int igemm8_min_tiles() {
+  static const int v = [] {
+    const char* e = std::getenv("PCMP_IGEMM8_MINTILES");
+    return e ? std::atoi(e) : 160;
+  }();
+  return v;
+}
+
 template <int MODE, int BN>
 static void launch8(IgemmParams& p, hipStream_t st) {
   constexpr int WM = G8Cfg<BN>::WM, WN = G8Cfg<BN>::WN;
@@ -1065,7 +1108,9 @@ static void launch8(IgemmParams& p, hipStream_t st) {
 
 // 8-wave LDS-DMA kernel eligibility: FWD/DGRAD with the block-uniform tap walk (source channels a
 // multiple of BK), no split-K, enough K-tiles for the phase pipeline, and a grid that still covers
-// every CU with BM = 256 tiles.  PCMP_IGEMM8=0 disables it (A/B runs).
+// most CUs with BM = 256 tiles: >= 160 tiles (ResNet-50 layer3 at B=256 has 196 and runs 20-28 %
+// faster than on the 4-wave kernel's 784 tiles; layer4's 98 tiles run 25-35 % slower, measured
+// profiles/r1_igemm8_mintiles_ab.txt).  PCMP_IGEMM8=0 disables it (A/B runs).
 static int use_igemm8(int mode, const IgemmParams& p) {
   if (!igemm8_mode() || mode == MODE_WGRAD || p.nsplit != 1) return 0;
   const int cin = mode == MODE_FWD ? p.C : p.K;
@@ -1073,7 +1118,7 @@ static int use_igemm8(int mode, const IgemmParams& p) {
   // (measured: the BN=128 variant does not beat the 4-wave 128x128 kernel; the dual BN-reduce
   //  epilogue of a 128x64 wave tile spills)
   if (mode == MODE_DGRAD && p.bn_x2) return 0;
-  if (ceil_div(p.gm, BM8) * ceil_div(p.gn, 256) < 240) return 0;
+  if (ceil_div(p.gm, BM8) * ceil_div(p.gn, 256) < igemm8_min_tiles()) return 0;
   return 256;
 }
 
@@ -1217,7 +1262,7 @@ struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (s
 
 static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
                                           int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
-                                          const BnrArgs* bn) {
+                                          const BnrArgs* bn, const c10::optional<at::Tensor>& wt_given) {
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(w);
   const int N = dy.size(0), K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
@@ -1238,6 +1283,15 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   auto fopts = dy.options().dtype(at::kFloat);
   const bool two = bn && bn->x2;
   auto st = cur_stream();
+  // a pre-transposed weight [C][R][S][K] (batched refresh, pcmp.utils.flat) replaces the per-call
+  // transpose wherever the GEMM uses every tap: stride 1, and 1x1 stride 2 (one parity class)
+  at::Tensor wt_full;
+  if (wt_given.has_value() && wt_given->defined()) {
+    PCMP_CHECK_BF16(*wt_given); PCMP_CHECK_CONTIG(*wt_given);
+    TORCH_CHECK(wt_given->numel() == w.numel() && wt_given->size(0) == C && wt_given->size(-1) == K,
+                "conv_dgrad: transposed weight must be [C,R,S,K]");
+    wt_full = *wt_given;
+  }
   if (stride == 2) {
     at::Tensor dx = has_res ? *resid : at::zeros({N, H, W, C}, dy.options());
     struct Cls { int oph, opw, r0, s0, subR, subS, dH, dW; };
@@ -1285,7 +1339,8 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     }
     int toff = 0;
     for (auto& c : cls) {
-      at::Tensor wt = transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st);
+      const bool whole = c.subR == R && c.subS == S && wt_full.defined();
+      at::Tensor wt = whole ? wt_full : transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st);
       IgemmParams q = class_params(c, wt);
       if (bn) {
         q.stats = ptr<float>(part) + (size_t)toff * 2 * C;
@@ -1299,7 +1354,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     if (two) return {dx, part, part2};
     return {dx, part};
   }
-  at::Tensor wt = transpose_taps(w, 0, 0, 1, R, S, st);
+  at::Tensor wt = wt_full.defined() ? wt_full : transpose_taps(w, 0, 0, 1, R, S, st);
   auto dx = at::empty({N, H, W, C}, dy.options());
   p.gm = N * H * W; p.gn = C; p.gk = R * S * K;
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(wt); p.out = dx.data_ptr();
@@ -1326,8 +1381,8 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
 // that class of output pixels (no MFMA work on structural zeros); their epilogues accumulate in
 // place into the residual buffer, which is CONSUMED (its memory becomes dx).
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride,
-                      int64_t pad, const c10::optional<at::Tensor>& resid) {
-  return dgrad_impl(dy, w, H, W, stride, pad, resid, nullptr)[0];
+                      int64_t pad, const c10::optional<at::Tensor>& resid, const c10::optional<at::Tensor>& wt) {
+  return dgrad_impl(dy, w, H, W, stride, pad, resid, nullptr, wt)[0];
 }
 
 // conv_dgrad with the BatchNorm-backward reduction of the layer(s) whose output gradient this is
@@ -1340,7 +1395,8 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
                                        const c10::optional<at::Tensor>& invstd2,
                                        const c10::optional<at::Tensor>& mscale,
-                                       const c10::optional<at::Tensor>& mshift) {
+                                       const c10::optional<at::Tensor>& mshift,
+                                       const c10::optional<at::Tensor>& wt) {
   const int64_t n = (int64_t)dy.size(0) * H * W * w.size(3);
   auto chk = [&](const at::Tensor& t, const char* nm) {
     PCMP_CHECK_BF16(t); PCMP_CHECK_CONTIG(t);
@@ -1361,7 +1417,7 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
     PCMP_CHECK_F32(*mscale); PCMP_CHECK_F32(*mshift);
     a.msc = ptr<float>(*mscale); a.msh = ptr<float>(*mshift);
   }
-  return dgrad_impl(dy, w, H, W, stride, pad, resid, &a);
+  return dgrad_impl(dy, w, H, W, stride, pad, resid, &a, wt);
 }
 
 // dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
@@ -1404,16 +1460,29 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   PCMP_LAUNCH_CHECK();
 }
 
+// src/dst: flat bf16 buffers; desc: int64 [n][6] on device (see wt_transpose_multi_kernel)
+void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor& desc, int64_t blocks) {
+  PCMP_CHECK_CUDA(src); PCMP_CHECK_BF16(src); PCMP_CHECK_BF16(dst); PCMP_CHECK_CONTIG(src); PCMP_CHECK_CONTIG(dst);
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.dim() == 2 &&
+              desc.size(1) == 6, "wt_transpose_multi: desc must be int64 [n,6] on the device");
+  const int n = desc.size(0);
+  if (n == 0 || blocks <= 0) return;
+  hipLaunchKernelGGL(wt_transpose_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, cur_stream(),
+                     ptr<unsigned short>(src), ptr<unsigned short>(dst), desc.data_ptr<int64_t>(), n);
+  PCMP_LAUNCH_CHECK();
+}
+
 }  // namespace pcmp
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("wt_transpose_multi(Tensor src, Tensor(a!) dst, Tensor desc, int blocks) -> ()", &pcmp::wt_transpose_multi);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu, bool want_stats) -> Tensor[]",
         &pcmp::conv_fwd);
-  m.def("conv_dgrad(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid) -> Tensor",
+  m.def("conv_dgrad(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? wt=None) -> Tensor",
         &pcmp::conv_dgrad);
   m.def("conv_dgrad_bnr(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? ymask, "
         "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2, Tensor? mscale, "
-        "Tensor? mshift) -> Tensor[]",
+        "Tensor? mshift, Tensor? wt=None) -> Tensor[]",
         &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
         &pcmp::conv_wgrad);

@@ -24,7 +24,7 @@ import torch
 
 from . import params as _params
 from .kernels import K
-from .params import compute_weight, emit_grad, sink_or_temp
+from .params import compute_weight, compute_weight_t, emit_grad, sink_or_temp
 
 
 def _conv_bn_train(x, L, dtype):
@@ -132,7 +132,7 @@ def _link_prev_tail(x):
 def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
     """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue."""
     r = K.conv_dgrad_bnr(dh, w, H, W, L.stride, L.pad, resid, x, prev.c, prev.mean, prev.invstd,
-                         prev.cd, prev.meand, prev.invstdd, None, None)
+                         prev.cd, prev.meand, prev.invstdd, None, None, compute_weight_t(L.weight, dh.dtype))
     prev.parts = r[1:]
     prev.g_ptr = r[0].data_ptr()
     return r[0]
@@ -226,6 +226,7 @@ class ResidualBlockFn(torch.autograd.Function):
             L = main[i]
             _wgrad(L, dh, acts[i], grads)
             wcomp = compute_weight(L.weight, dh.dtype)
+            wt = compute_weight_t(L.weight, dh.dtype)
             if i > 0:
                 Hi, Wi = acts[i].shape[1], acts[i].shape[2]
                 m_prev, is_prev = stats[i - 1]
@@ -234,10 +235,10 @@ class ResidualBlockFn(torch.autograd.Function):
                     # the ReLU mask of acts[i] = relu(cs[i-1] * scale + shift) is recomputed from cs[i-1]
                     sc_prev, sh_prev = ctx.coefs[i - 1]
                     r = K.conv_dgrad_bnr(dh, wcomp, Hi, Wi, L.stride, L.pad, None, None, cs[i - 1],
-                                         m_prev, is_prev, None, None, None, sc_prev, sh_prev)
+                                         m_prev, is_prev, None, None, None, sc_prev, sh_prev, wt)
                     outs, gr = _bn_backward(r[0], None, cs[i - 1], m_prev, is_prev, main[i - 1], parts=r[1:])
                 else:
-                    da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None)
+                    da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None, wt)
                     outs, gr = _bn_backward(da, acts[i], cs[i - 1], m_prev, is_prev, main[i - 1])
                 grads.update(gr)
                 dh = outs[0]
@@ -247,17 +248,18 @@ class ResidualBlockFn(torch.autograd.Function):
                     _wgrad(down, dcd, acts[0], grads)
                     if need_dx:
                         wd = compute_weight(down.weight, dh.dtype)
+                        wdt = compute_weight_t(down.weight, dh.dtype)
                         if prev is not None:
-                            t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None)
+                            t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt)
                             dx = _dgrad_into_prev(dh, wcomp, H, W, L, t, x, prev)
                         else:
-                            t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None)
-                            dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t)
+                            t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None, wt)
+                            dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t, wdt)
                 elif need_dx:
                     if prev is not None:
                         dx = _dgrad_into_prev(dh, wcomp, H, W, L, gid, x, prev)
                     else:
-                        dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid)
+                        dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid, wt)
         # free saved activations early
         ctx.acts = ctx.cs = ctx.dstate = ctx.coefs = None
         ctx.prev_tail = ctx.tail = None
@@ -300,7 +302,8 @@ class StemFn(torch.autograd.Function):
         _wgrad(L, dc, x, grads)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = K.conv_dgrad(dc, compute_weight(L.weight, dc.dtype), x.shape[1], x.shape[2], L.stride, L.pad, None)
+            dx = K.conv_dgrad(dc, compute_weight(L.weight, dc.dtype), x.shape[1], x.shape[2], L.stride, L.pad, None,
+                              compute_weight_t(L.weight, dc.dtype))
         ctx.state = None
         return (dx, None) + tuple(grads.get(p) for p in ctx.params)
 
@@ -331,7 +334,7 @@ class ConvBiasActFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = K.conv_dgrad(dy, compute_weight(weight, dy.dtype), x.shape[1], x.shape[2], conv.stride, conv.pad,
-                              None)
+                              None, compute_weight_t(weight, dy.dtype))
         return dx, None, gw, gb
 
 

@@ -21,7 +21,7 @@ OP_NAMES = (
     "bn_bwd_apply",
     "maxpool_fwd", "maxpool_bwd", "gap_fwd", "gap_bwd", "softmax_xent", "dropout", "relu_bwd", "colsum",
     "nchw_to_nhwc",
-    "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16",
+    "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16", "wt_transpose_multi",
     "embedding_fwd", "embedding_bwd", "lstm_cell_fwd", "lstm_cell_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
     "masked_mean_fwd", "masked_mean_bwd",
     "layernorm_fwd", "layernorm_bwd", "gelu_fwd", "gelu_bwd", "bias_act_fwd",

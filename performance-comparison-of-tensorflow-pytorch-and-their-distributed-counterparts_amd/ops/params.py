@@ -41,6 +41,15 @@ def compute_weight(p: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return cache[1]
 
 
+def compute_weight_t(p: torch.Tensor, dtype: torch.dtype):
+    """Transposed [C,R,S,K] compute weight for DGRAD from the flat arena, or None (the kernel
+    then transposes per call)."""
+    owner = getattr(p, "_flat_owner", None)
+    if owner is None or dtype != torch.bfloat16:
+        return None
+    return owner.transposed(p)
+
+
 def emit_grad(p: torch.Tensor | None, compute: Callable[[torch.Tensor, bool], None]):
     """Produce the gradient of ``p``.  ``compute(out, accumulate)`` fills an fp32 tensor.
 

@@ -35,7 +35,9 @@ def conv_fwd(x, w, stride, pad, bias=None, resid=None, relu=False, want_stats=Fa
     return [y]
 
 
-def conv_dgrad(dy, w, H, W, stride, pad, resid=None):
+def conv_dgrad(dy, w, H, W, stride, pad, resid=None, wt=None):
+    if wt is not None:   # the pre-transposed weight must agree with w (checked, then unused)
+        assert wt.shape == (w.shape[3], w.shape[1], w.shape[2], w.shape[0]), "conv_dgrad: wt must be [C,R,S,K]"
     N, K, R, S, C = dy.shape[0], w.shape[0], w.shape[1], w.shape[2], w.shape[3]
     dx = torch.nn.grad.conv2d_input((N, C, H, W), _nchw(w), _nchw(dy), stride=stride, padding=pad)
     dx = _nhwc(dx)
@@ -45,10 +47,10 @@ def conv_dgrad(dy, w, H, W, stride, pad, resid=None):
 
 
 def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None,
-                   mscale=None, mshift=None):
+                   mscale=None, mshift=None, wt=None):
     if ymask is None and mscale is not None:      # mask recomputed from x: relu(x * scale + shift) > 0
         ymask = (x.float() * mscale + mshift).reshape(x.shape)
-    g = _masked(conv_dgrad(dy, w, H, W, stride, pad, resid), ymask).to(dy.dtype).contiguous()
+    g = _masked(conv_dgrad(dy, w, H, W, stride, pad, resid, wt), ymask).to(dy.dtype).contiguous()
     return [g] + bn_bwd_reduce(g, None, x, mean, invstd, x2, mean2, invstd2)
 
 
@@ -314,6 +316,14 @@ def grad_clip_coef(g, pre_scale, max_norm, post_scale):
 
 def cast_to_bf16(x, y):
     y.copy_(x.to(y.dtype))
+
+
+def wt_transpose_multi(src, dst, desc, blocks):
+    """dst[C][R*S][K] = src[K][R*S][C] for every tensor described by desc rows
+    (src_off, dst_off, K, RS, C, first_block) -- the batched DGRAD weight transpose."""
+    for so, do, K, T, C, _ in desc.tolist():
+        n = K * T * C
+        dst[do:do + n].copy_(src[so:so + n].view(K, T, C).permute(2, 1, 0).reshape(-1))
 
 
 # ------------------------------------------------------------------------------ text / LSTM

@@ -51,7 +51,47 @@ class FlatParams:
                 p._shadow = self.shadow[o:o + n].view_as(p)
             p._grad_fresh = True
             self._hooks.append(p.register_post_accumulate_grad_hook(self._fold_torch_grad))
+        self._init_transposed()
         self.refresh_shadows()
+
+    # ----------------------------------------------------------------------------------------
+    def _init_transposed(self):
+        """DGRAD consumes every conv weight as [C][R][S][K].  Instead of one transpose launch per
+        DGRAD call, all 4-D weights get a transposed bf16 copy in one more flat buffer, refreshed by
+        ONE batched launch (``wt_transpose_multi``) the first time backward asks for it after the
+        weights changed (keyed on the global weight generation)."""
+        self.shadow_t, self._t_desc, self._t_blocks, self._t_gen = None, None, 0, None
+        if self.shadow is None or self.shadow.dtype != torch.bfloat16:
+            return
+        rows, off, blocks = [], 0, 0
+        for p, o in zip(self.params, self.offsets):
+            if p.dim() != 4:
+                continue
+            K, R, S, C = p.shape
+            rows.append([o, off, K, R * S, C, blocks])
+            p._t_slice = (off, (C, R, S, K))
+            blocks += R * S * ((K + 63) // 64) * ((C + 63) // 64)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        if not rows:
+            return
+        self.shadow_t = torch.empty(off, dtype=torch.bfloat16, device=self.device)
+        self._t_desc = torch.tensor(rows, dtype=torch.int64, device=self.device)
+        self._t_blocks = blocks
+        for p in self.params:
+            sl = getattr(p, "_t_slice", None)
+            if sl is not None:
+                o, shp = sl
+                p._shadow_t = self.shadow_t[o:o + p.numel()].view(shp)
+                p._flat_owner = self
+
+    def transposed(self, p):
+        """[C,R,S,K] bf16 compute weight of a conv weight ``p`` (batched refresh when stale)."""
+        from ..ops.params import WEIGHT_GEN
+        if self._t_gen != WEIGHT_GEN[0]:
+            from ..ops.kernels import K
+            K.wt_transpose_multi(self.shadow, self.shadow_t, self._t_desc, self._t_blocks)
+            self._t_gen = WEIGHT_GEN[0]
+        return p._shadow_t
 
     # ----------------------------------------------------------------------------------------
     @staticmethod

@@ -271,6 +271,10 @@ BIG_SHAPES = [
     (20, 56, 56, 256, 64, 1, 1, 0),     # DGRAD gn=256 over K=64 x 1x1 -> 1 K-tile (old kernel) / FWD gk=256
     (20, 56, 56, 256, 64, 3, 1, 1),     # DGRAD gn=256, 9 K-tiles -> 8-wave kernel incl. BN-reduce epilogue
     (5, 56, 56, 256, 512, 3, 1, 1),     # M tail (15680 = 61.25 tiles), N = 2 x 256
+    # ResNet-50 layer3 at B=256: 196 BM=256 tiles (the 8-wave kernel's lower grid bound)
+    (256, 14, 14, 256, 256, 3, 1, 1),
+    (256, 14, 14, 1024, 256, 1, 1, 0),
+    (256, 28, 28, 256, 256, 3, 2, 1),   # layer3.0 conv2: stride-2 DGRAD parity classes of 196 tiles
 ]
 
 
@@ -305,3 +309,32 @@ def test_conv_large_shapes_8wave(gpu, shape):
     close(out[0], outr[0])
     for a, b in zip(out[1:], outr[1:]):
         close(a.sum(0), b.sum(0), rtol=2e-2, atol=1.0)
+
+
+def test_batched_weight_transpose_and_dgrad_with_pretransposed(gpu):
+    """FlatParams' transposed conv-weight arena (one wt_transpose_multi launch) equals the per-call
+    transpose, and DGRAD with the pre-transposed weight equals DGRAD without it."""
+    from pcmp.ops.params import bump_weight_gen, compute_weight, compute_weight_t
+    from pcmp.utils.flat import FlatParams
+    shapes = [(64, 3, 3, 64), (256, 1, 1, 64), (72, 7, 7, 8), (512, 1, 1, 256), (128, 3, 3, 128)]
+    ps = [torch.nn.Parameter(torch.randn(*s, device=gpu) * 0.05) for s in shapes]
+    lin = torch.nn.Parameter(torch.randn(40, 24, device=gpu))     # 2-D: no transposed copy
+    flat = FlatParams(ps + [lin])
+    assert getattr(lin, "_flat_owner", None) is None
+    for p in ps:
+        wt = compute_weight_t(p, torch.bfloat16)
+        assert torch.equal(wt, compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0).contiguous())
+    # stale after a weight change -> refreshed on the next request
+    flat.master.mul_(-1.0)
+    flat.refresh_shadows()
+    p = ps[0]
+    assert torch.equal(compute_weight_t(p, torch.bfloat16), compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0).contiguous())
+    bump_weight_gen()
+    for (K_, R, S, C), p, (s, pad) in zip(shapes, ps, [(1, 1), (1, 0), (2, 3), (2, 0), (2, 1)]):
+        N, H, W = 2, 14, 14
+        P, Q = (H + 2 * pad - R) // s + 1, (W + 2 * pad - S) // s + 1
+        dy = rnd(N, P, Q, K_, dev=gpu)
+        w = compute_weight(p, torch.bfloat16)
+        a = _ops().conv_dgrad(dy, w, H, W, s, pad, None)
+        b = _ops().conv_dgrad(dy, w, H, W, s, pad, None, compute_weight_t(p, torch.bfloat16))
+        assert torch.equal(a, b)

@@ -86,3 +86,18 @@ def test_maxpool_reference_idx_roundtrip():
     dy = torch.randn_like(y)
     yt.backward(dy.permute(0, 3, 1, 2))
     assert torch.allclose(ref.maxpool_bwd(dy, idx, 9, 9, 3, 2, 1), xt.grad.permute(0, 2, 3, 1), atol=1e-6)
+
+
+def test_batched_weight_transpose_reference():
+    from pcmp.ops.params import compute_weight, compute_weight_t
+    from pcmp.utils.flat import FlatParams
+    ps = [torch.nn.Parameter(torch.randn(*s)) for s in [(16, 3, 3, 8), (32, 1, 1, 16), (8, 7, 7, 8)]]
+    FlatParams(ps)
+    for p in ps:
+        wt = compute_weight_t(p, torch.bfloat16)
+        assert wt.shape == (p.shape[3], p.shape[1], p.shape[2], p.shape[0])
+        assert torch.equal(wt, compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0))
+    dy = torch.randn(2, 5, 5, 16).to(torch.bfloat16)
+    w = compute_weight(ps[0], torch.bfloat16)
+    assert torch.equal(K.conv_dgrad(dy, w, 5, 5, 1, 1, None, compute_weight_t(ps[0], torch.bfloat16)),
+                       K.conv_dgrad(dy, w, 5, 5, 1, 1, None))

@@ -24,6 +24,9 @@ SHAPES = [  # name, N, H, W, C, K, R, stride, pad
     ("l3_3x3_256", 256, 14, 14, 256, 256, 3, 1, 1),
     ("l3_1x1_1024to256", 256, 14, 14, 1024, 256, 1, 1, 0),
     ("l4_3x3_512", 256, 7, 7, 512, 512, 3, 1, 1),
+    ("l3_1x1_256to1024", 256, 14, 14, 256, 1024, 1, 1, 0),
+    ("l4_1x1_2048to512", 256, 7, 7, 2048, 512, 1, 1, 0),
+    ("l4_1x1_512to2048", 256, 7, 7, 512, 2048, 1, 1, 0),
     ("stem_7x7", 256, 224, 224, 8, 64, 7, 2, 3),
     # GEMM-like probes for the 8-wave BM=256 kernel (BN=256 variant)
     ("x_3x3_256_28", 256, 28, 28, 256, 256, 3, 1, 1),
