@@ -1122,6 +1122,29 @@ static int use_igemm8(int mode, const IgemmParams& p) {
   return 256;
 }
 
+// WGRAD tiles with 64x64 wave tiles where one GEMM side is narrow: RSC <= 64 (gn) -> 256x64 with
+// the 4 waves along M; cout <= 64 (gm) -> 64x256 with the waves along N, only for the Cin=8 stem
+// (measured profiles/r1_wgrad_wide_ab.txt: stem -7 %, 1x1 64->256 -5 %, but the layer1 3x3 and
+// 1x1 256->64 WGRADs ran 5-16 % slower on 64x256).  PCMP_WG64=0 disables them (A/B runs).
+static int wgrad_wide(const IgemmParams& p) {
+  static const int v = [] {
+    const char* e = std::getenv("PCMP_WG64");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (!v) return 0;
+  if (p.gm > 32 && p.gm <= 64 && p.gn >= 256 && p.C == 8) return 1;   // 64 x 256 (stem)
+  if (p.gn > 32 && p.gn <= 64 && p.gm >= 256) return 2;   // 256 x 64
+  return 0;
+}
+
+static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
+  const int w = wgrad_wide(p);
+  if (w == 1) { BM = 64; BN = 256; return; }
+  if (w == 2) { BM = 256; BN = 64; return; }
+  BM = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
+  BN = p.gn <= 64 ? 64 : 128;
+}
+
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
 static int igemm_bm(int mode, const IgemmParams& p) {
   if (use_igemm8(mode, p)) return BM8;
@@ -1132,6 +1155,11 @@ template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE != MODE_WGRAD) {
     if (use_igemm8(MODE, p) == 256) { launch8<MODE, 256>(p, st); return; }
+  }
+  if constexpr (MODE == MODE_WGRAD) {
+    const int w = wgrad_wide(p);
+    if (w == 1) { launch_cfg<MODE, 64, 256, 1, 4>(p, st); return; }
+    if (w == 2) { launch_cfg<MODE, 256, 64, 4, 1>(p, st); return; }
   }
   // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)
   if (p.gm <= 32) {
@@ -1293,9 +1321,9 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     wt_full = *wt_given;
   }
   if (stride == 2) {
-    at::Tensor dx = has_res ? *resid : at::zeros({N, H, W, C}, dy.options());
     struct Cls { int oph, opw, r0, s0, subR, subS, dH, dW; };
     std::vector<Cls> cls;
+    bool uncovered = false;   // a parity class no tap reaches (1x1/2): its dx is resid or zero
     for (int oph = 0; oph < 2; ++oph)
       for (int opw = 0; opw < 2; ++opw) {
         const int r0 = (oph + pad) & 1, s0 = (opw + pad) & 1;
@@ -1305,10 +1333,16 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
         if (subR == 0 || subS == 0) {
           // no tap reaches this pixel class: its dx is resid (or 0) -- a fused BN reduction would miss it
           TORCH_CHECK(!bn, "conv_dgrad_bnr: stride-2 filter leaves pixel classes uncovered");
+          uncovered = true;
           continue;
         }
         cls.push_back({oph, opw, r0, s0, subR, subS, dH, dW});
       }
+    // the classes partition dx: without a residual and with every class covered, each pixel is
+    // written exactly once -> no zero fill and no read-back of the accumulation buffer
+    const bool accum = has_res || uncovered;
+    at::Tensor dx = has_res ? *resid : (uncovered ? at::zeros({N, H, W, C}, dy.options())
+                                                  : at::empty({N, H, W, C}, dy.options()));
     auto class_params = [&](const Cls& c, const at::Tensor& wt) {
       IgemmParams q = p;
       q.R = c.subR; q.S = c.subS;
@@ -1322,7 +1356,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
       q.a = ptr<__bf16>(dy); q.out = dx.data_ptr();
       q.a_bytes = tensor_bytes(dy);
       if (wt.defined()) { q.b = ptr<__bf16>(wt); q.b_bytes = tensor_bytes(wt); }
-      q.resid = ptr<__bf16>(dx);   // in-place accumulate
+      q.resid = accum ? ptr<__bf16>(dx) : nullptr;   // in-place accumulate
       q.ksplit = q.gk;
       set_bn(q);                   // (the kernel choice, hence the partial-row count, depends on it)
       return q;
@@ -1433,8 +1467,8 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(x);
   p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(x);
-  const int BM = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
-  const int BN = p.gn <= 64 ? 64 : 128;
+  int BM, BN;
+  wgrad_tile(p, BM, BN);
   const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
   const int ksteps = ceil_div(p.gk, BK);
   int nsplit = std::max(1, std::min(std::min(ceil_div(1024, tiles), ksteps / 8), 256));

@@ -275,6 +275,10 @@ BIG_SHAPES = [
     (256, 14, 14, 256, 256, 3, 1, 1),
     (256, 14, 14, 1024, 256, 1, 1, 0),
     (256, 28, 28, 256, 256, 3, 2, 1),   # layer3.0 conv2: stride-2 DGRAD parity classes of 196 tiles
+    # narrow outputs over >= 131072 pixels: BM=256 x BN=64 tiles (4 waves along M)
+    (48, 56, 56, 64, 64, 3, 1, 1),
+    (48, 56, 56, 256, 64, 1, 1, 0),
+    (12, 224, 224, 8, 64, 7, 2, 3),     # stem (FWD 7x7/2; DGRAD over 64 -> 8 channels stays 4-wave)
 ]
 
 
