@@ -86,9 +86,21 @@ __global__ void partials_reduce_kernel(const float* __restrict__ part, int T, in
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
   const int r0 = blockIdx.y * rpb, r1 = min(T, r0 + rpb);
-  double s = 0;
-  if (col < L)
-    for (int r = r0 + g; r < r1; r += 4) s += part[(size_t)r * L + col];
+  // 8 independent loads in flight per thread (a dependent add chain would expose one global-load
+  // latency per row: this launch-boundary reduction is latency-bound, not bandwidth-bound)
+  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < L) {
+    int r = r0 + g;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + 4 * u) * L + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s8[u] += v[u];
+    }
+    for (; r < r1; r += 4) s8[0] += part[(size_t)r * L + col];
+  }
+  const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
   sh[g][threadIdx.x & 63] = s;
   __syncthreads();
   if (g == 0 && col < L) red[(size_t)blockIdx.y * L + col] = s + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
@@ -107,7 +119,18 @@ __global__ void bn_finalize_kernel(const PT* __restrict__ part, int T, int C, do
   const int g = threadIdx.x >> 6;
   double s1 = 0, s2 = 0;
   if (c < C) {
-    for (int t = g; t < T; t += 4) {
+    int t = g;
+    for (; t + 12 < T; t += 16) {   // 4 rows x 2 sums of independent loads in flight
+      PT a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = part[(size_t)(t + 4 * u) * 2 * C + c];
+        b[u] = part[(size_t)(t + 4 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { s1 += a[u]; s2 += b[u]; }
+    }
+    for (; t < T; t += 4) {
       s1 += part[(size_t)t * 2 * C + c];
       s2 += part[(size_t)t * 2 * C + C + c];
     }
@@ -256,7 +279,18 @@ __global__ void bn_bwd_finalize_kernel(const PT* __restrict__ part, int T, int C
   const int g = threadIdx.x >> 6;
   double sg = 0, sgx = 0;
   if (c < C) {
-    for (int t = g; t < T; t += 4) {
+    int t = g;
+    for (; t + 12 < T; t += 16) {   // 4 rows x 2 sums of independent loads in flight
+      PT a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = part[(size_t)(t + 4 * u) * 2 * C + c];
+        b[u] = part[(size_t)(t + 4 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { sg += a[u]; sgx += b[u]; }
+    }
+    for (; t < T; t += 4) {
       sg += part[(size_t)t * 2 * C + c];
       sgx += part[(size_t)t * 2 * C + C + c];
     }

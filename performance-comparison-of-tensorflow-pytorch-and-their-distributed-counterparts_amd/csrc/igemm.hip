@@ -21,6 +21,12 @@
 // statistics of the stored (bf16-rounded) output.
 #include "common.h"
 
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
 namespace pcmp {
 
 // ----------------------------------------------------------------------------------------------
@@ -1454,6 +1460,92 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
   return dgrad_impl(dy, w, H, W, stride, pad, resid, &a, wt);
 }
 
+// split-K WGRAD: partial dW per split into a workspace, then one deterministic reduction pass
+static void wgrad_run(IgemmParams p, int nsplit, float* out, bool accumulate, const at::TensorOptions& fopts,
+                      hipStream_t st) {
+  const int ksteps = ceil_div(p.gk, BK);
+  const int steps_per = ceil_div(ksteps, nsplit);
+  nsplit = ceil_div(ksteps, steps_per);
+  p.ksplit = steps_per * BK;
+  p.nsplit = nsplit;
+  if (nsplit == 1) {
+    p.out = out;
+    p.accumulate = accumulate;
+    dispatch<MODE_WGRAD>(p, st);
+    return;
+  }
+  const int64_t n = (int64_t)p.gm * p.gn;
+  TORCH_CHECK(n % 4 == 0, "conv_wgrad: numel % 4");
+  auto ws = at::empty({(int64_t)nsplit, n}, fopts);
+  p.out = ws.data_ptr();
+  dispatch<MODE_WGRAD>(p, st);
+  const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out, n, nsplit,
+                     (int)accumulate);
+  PCMP_LAUNCH_CHECK();
+}
+
+// WGRAD split-K autotuning (cudnn.benchmark-style): the best split count of a shape depends on tile
+// quantisation against 256 CUs and on the workspace traffic of the reduction, and measured
+// non-monotonically (profiles/r1_wgrad_splitk_ab.txt), so the first call of each shape times a few
+// grid targets on a scratch output and caches the fastest.  Never while a graph is being captured.
+// PCMP_AUTOTUNE=0 (or an explicit PCMP_WGRAD_WGS) keeps the static 1024-workgroup target, which
+// also keeps runs bitwise reproducible (a tuned split count changes the summation order).
+static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions& fopts, hipStream_t st) {
+  const int ksteps = ceil_div(p.gk, BK);
+  auto nsplit_for = [&](int target) { return std::max(1, std::min(std::min(ceil_div(target, tiles), ksteps / 8), 256)); };
+  static const int fixed_target = [] {
+    const char* e = std::getenv("PCMP_WGRAD_WGS");
+    return e ? std::max(64, std::atoi(e)) : 0;
+  }();
+  static const bool tune = [] {
+    const char* e = std::getenv("PCMP_AUTOTUNE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (fixed_target) return nsplit_for(fixed_target);
+  const int dflt = nsplit_for(1024);
+  if (!tune) return dflt;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
+  static std::mutex mu;
+  static std::unordered_map<std::string, int> cache;
+  char key[160];
+  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  std::vector<int> cands;
+  for (int t : {256, 512, 768, 1024, 1536, 2048}) {
+    const int ns = nsplit_for(t);
+    if (std::find(cands.begin(), cands.end(), ns) == cands.end()) cands.push_back(ns);
+  }
+  int best = dflt;
+  if (cands.size() > 1) {
+    auto scratch = at::empty({(int64_t)p.gm * p.gn}, fopts);
+    hipEvent_t e0, e1;
+    PCMP_HIP_CHECK(hipEventCreate(&e0));
+    PCMP_HIP_CHECK(hipEventCreate(&e1));
+    float best_ms = 1e30f;
+    for (int ns : cands) {
+      wgrad_run(p, ns, ptr<float>(scratch), false, fopts, st);   // warm (workspace allocation, caches)
+      PCMP_HIP_CHECK(hipEventRecord(e0, st));
+      for (int r = 0; r < 3; ++r) wgrad_run(p, ns, ptr<float>(scratch), false, fopts, st);
+      PCMP_HIP_CHECK(hipEventRecord(e1, st));
+      PCMP_HIP_CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      PCMP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best_ms) { best_ms = ms; best = ns; }
+    }
+    PCMP_HIP_CHECK(hipEventDestroy(e0));
+    PCMP_HIP_CHECK(hipEventDestroy(e1));
+  }
+  std::lock_guard<std::mutex> g(mu);
+  cache.emplace(key, best);
+  return best;
+}
+
 // dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
                 int64_t stride, int64_t pad, bool accumulate) {
@@ -1470,28 +1562,9 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   int BM, BN;
   wgrad_tile(p, BM, BN);
   const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
-  const int ksteps = ceil_div(p.gk, BK);
-  int nsplit = std::max(1, std::min(std::min(ceil_div(1024, tiles), ksteps / 8), 256));
-  const int steps_per = ceil_div(ksteps, nsplit);
-  nsplit = ceil_div(ksteps, steps_per);
-  p.ksplit = steps_per * BK;
-  p.nsplit = nsplit;
   auto st = cur_stream();
-  if (nsplit == 1) {
-    p.out = out.data_ptr();
-    p.accumulate = accumulate;
-    dispatch<MODE_WGRAD>(p, st);
-    return;
-  }
-  auto ws = at::empty({(int64_t)nsplit, (int64_t)p.gm * p.gn}, out.options());
-  p.out = ws.data_ptr();
-  dispatch<MODE_WGRAD>(p, st);
-  const int64_t n = (int64_t)p.gm * p.gn;
-  TORCH_CHECK(n % 4 == 0, "conv_wgrad: numel % 4");
-  const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<float>(out),
-                     n, nsplit, (int)accumulate);
-  PCMP_LAUNCH_CHECK();
+  const int nsplit = wgrad_nsplit(p, tiles, out.options(), st);
+  wgrad_run(p, nsplit, ptr<float>(out), accumulate, out.options(), st);
 }
 
 // src/dst: flat bf16 buffers; desc: int64 [n][6] on device (see wt_transpose_multi_kernel)
