@@ -173,7 +173,8 @@ __global__ void bn_eval_coeff_kernel(int C, const float* __restrict__ gamma, con
 __global__ void bn_apply_kernel(const __bf16* __restrict__ x, const float* __restrict__ sc,
                                 const float* __restrict__ shf, const __bf16* __restrict__ x2,
                                 const float* __restrict__ sc2, const float* __restrict__ shf2,
-                                __bf16* __restrict__ y, int64_t nvec, int CV, int relu) {
+                                __bf16* __restrict__ y, int64_t nvec, int CV, int relu,
+                                uint8_t* __restrict__ mbits) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int cv = (int)(i % CV);
@@ -200,7 +201,16 @@ __global__ void bn_apply_kernel(const __bf16* __restrict__ x, const float* __res
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
-    store8(y + i * 8, v);
+    u16x8 u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+    *reinterpret_cast<u16x8*>(y + i * 8) = u;
+    if (mbits) {   // bit e = stored y[e] > 0 (sign clear, nonzero): the backward ReLU mask
+      unsigned bits = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bits |= ((u[e] & 0x8000u) == 0 && (u[e] & 0x7fffu) != 0) ? (1u << e) : 0u;
+      mbits[i] = (uint8_t)bits;
+    }
   }
 }
 
@@ -435,7 +445,7 @@ static int ew_blocks(int64_t nvec) { return (int)std::min<int64_t>(4096, (nvec +
 
 at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
                     const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
-                    const c10::optional<at::Tensor>& shift2, bool relu) {
+                    const c10::optional<at::Tensor>& shift2, bool relu, const c10::optional<at::Tensor>& mbits) {
   check_act(x, "bn_apply");
   const int C = x.size(-1);
   auto y = at::empty_like(x);
@@ -446,9 +456,15 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
     TORCH_CHECK(x2->numel() == x.numel(), "bn_apply: x2 shape");
     x2p = ptr<__bf16>(*x2);
   }
+  uint8_t* mb = nullptr;
+  if (mbits.has_value() && mbits->defined()) {
+    TORCH_CHECK(mbits->scalar_type() == at::kByte && mbits->is_contiguous() && mbits->numel() == nvec,
+                "bn_apply: mbits must be contiguous uint8 with one byte per 8 elements");
+    mb = mbits->data_ptr<uint8_t>();
+  }
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
                      ptr<float>(scale), ptr<float>(shift), x2p, optr<float>(scale2), optr<float>(shift2),
-                     ptr<__bf16>(y), nvec, C / 8, (int)relu);
+                     ptr<__bf16>(y), nvec, C / 8, (int)relu, mb);
   PCMP_LAUNCH_CHECK();
   return y;
 }
@@ -531,7 +547,8 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::bn_finalize);
   m.def("bn_eval_coeff(Tensor? gamma, Tensor? beta, Tensor running_mean, Tensor running_var, float eps) -> Tensor[]",
         &pcmp::bn_eval_coeff);
-  m.def("bn_apply(Tensor x, Tensor scale, Tensor shift, Tensor? x2, Tensor? scale2, Tensor? shift2, bool relu) -> Tensor",
+  m.def("bn_apply(Tensor x, Tensor scale, Tensor shift, Tensor? x2, Tensor? scale2, Tensor? shift2, bool relu, "
+        "Tensor(a!)? mbits=None) -> Tensor",
         &pcmp::bn_apply);
   m.def("bn_bwd_reduce(Tensor dy, Tensor? ymask, Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, "
         "Tensor? invstd2) -> Tensor[]",

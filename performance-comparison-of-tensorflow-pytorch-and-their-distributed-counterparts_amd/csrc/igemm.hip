@@ -83,6 +83,9 @@ struct IgemmParams {
   // apply of an intermediate layer); used when bn_mask is null
   const float* bn_msc;
   const float* bn_msh;
+  // mask as bits (1 byte per 8 channels, written by the forward bn_apply of a block output): used
+  // instead of bn_mask -- 1/16 of the bytes of the bf16 tensor
+  const uint8_t* bn_mbits;
   int stats_cap;   // BM-row tiles the stats / stats2 buffers hold (host-side bounds check)
 };
 
@@ -195,8 +198,9 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
 #pragma unroll
         for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
     const bool has_res = p.resid != nullptr;
-    const bool has_mk = bnr && p.bn_mask != nullptr;
-    const bool mfx = bnr && !has_mk && p.bn_msc != nullptr;   // ReLU mask recomputed from x
+    const bool has_mb = bnr && p.bn_mbits != nullptr;
+    const bool has_mk = bnr && !has_mb && p.bn_mask != nullptr;
+    const bool mfx = bnr && !has_mb && !has_mk && p.bn_msc != nullptr;   // ReLU mask recomputed from x
     // output row offsets of the TM pixel-row groups
     size_t orows[TM];
 #pragma unroll
@@ -217,7 +221,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     // Stores walk (i outer, v inner: the two 64-B halves of a pixel's 128-B channel run are stored
     // back to back); the resid / mask / x operand loads of step t+1 are issued before the math of
     // step t (one-deep software pipeline).
-    unsigned rvA[2][NP], mkA[2][NP], xvA[2][NP], xv2A[2][NP];
+    unsigned rvA[2][NP], mkA[2][NP], xvA[2][NP], xv2A[2][NP], mbA[2];
     auto issue = [&](int t, int b) {
       const int i = t / NV, v = t % NV;
       const int m = m0 + wr * WTM + i * 16 + fr;
@@ -235,6 +239,10 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       };
       if (has_res) ldv(rvA[b], p.resid);
       if constexpr (bnr) {
+        if (has_mb) {   // o is a multiple of VW: the store's channels are bits (o & 7) .. +VW-1 of byte o/8
+          const unsigned byte = ok ? p.bn_mbits[o >> 3] : 0u;
+          mbA[b] = VW == 8 ? byte : ((byte >> (o & 4)) & 0xfu);
+        }
         if (has_mk) ldv(mkA[b], p.bn_mask);
         ldv(xvA[b], p.bn_x);
         if constexpr (bnr2) ldv(xv2A[b], p.bn_x2);
@@ -308,7 +316,10 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           if constexpr (bnr) {
             const float xa = __uint_as_float(xvA[b][q] << 16), xb = __uint_as_float(xvA[b][q] & 0xffff0000u);
             // g = round(dgrad) masked by the forward ReLU output (> 0: sign clear and nonzero)
-            if (has_mk) {
+            if (has_mb) {
+              const unsigned bits = mbA[b] >> ce;
+              u &= ((bits & 1u) ? 0x0000ffffu : 0u) | ((bits & 2u) ? 0xffff0000u : 0u);
+            } else if (has_mk) {
               const unsigned y = mkA[b][q];
               const unsigned keep = (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
                                     (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
@@ -1200,6 +1211,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.stats2 = nullptr;
   p.bn_mask = nullptr; p.bn_x = nullptr; p.bn_mean = nullptr; p.bn_istd = nullptr;
   p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr; p.bn_msc = nullptr; p.bn_msh = nullptr;
+  p.bn_mbits = nullptr;
   p.stats_cap = 0;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
 }
@@ -1283,6 +1295,7 @@ static at::Tensor transpose_taps(const at::Tensor& w, int r0, int s0, int rstep,
 // that class of output pixels (no MFMA work on structural zeros); their epilogues accumulate in
 // place into the residual buffer, which is CONSUMED (its memory becomes dx).
 struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (see IgemmParams)
+  const uint8_t* mbits = nullptr;
   const __bf16* mask = nullptr;
   const __bf16* x = nullptr;
   const float* mean = nullptr;
@@ -1313,6 +1326,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     q.bn_mask = bn->mask; q.bn_x = bn->x; q.bn_mean = bn->mean; q.bn_istd = bn->istd;
     q.bn_x2 = bn->x2; q.bn_mean2 = bn->mean2; q.bn_istd2 = bn->istd2;
     q.bn_msc = bn->msc; q.bn_msh = bn->msh;
+    q.bn_mbits = bn->mbits;
   };
   auto fopts = dy.options().dtype(at::kFloat);
   const bool two = bn && bn->x2;
@@ -1436,7 +1450,8 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& invstd2,
                                        const c10::optional<at::Tensor>& mscale,
                                        const c10::optional<at::Tensor>& mshift,
-                                       const c10::optional<at::Tensor>& wt) {
+                                       const c10::optional<at::Tensor>& wt,
+                                       const c10::optional<at::Tensor>& ymask_bits) {
   const int64_t n = (int64_t)dy.size(0) * H * W * w.size(3);
   auto chk = [&](const at::Tensor& t, const char* nm) {
     PCMP_CHECK_BF16(t); PCMP_CHECK_CONTIG(t);
@@ -1447,12 +1462,17 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
   PCMP_CHECK_F32(mean); PCMP_CHECK_F32(invstd);
   a.x = ptr<__bf16>(x); a.mean = ptr<float>(mean); a.istd = ptr<float>(invstd);
   if (ymask.has_value() && ymask->defined()) { chk(*ymask, "ymask"); a.mask = ptr<__bf16>(*ymask); }
+  if (ymask_bits.has_value() && ymask_bits->defined()) {
+    TORCH_CHECK(ymask_bits->scalar_type() == at::kByte && ymask_bits->is_contiguous() && ymask_bits->numel() * 8 == n,
+                "conv_dgrad_bnr: ymask_bits must be contiguous uint8 with one byte per 8 elements");
+    a.mbits = ymask_bits->data_ptr<uint8_t>();
+  }
   if (x2.has_value() && x2->defined()) {
     chk(*x2, "x2");
     TORCH_CHECK(mean2.has_value() && invstd2.has_value(), "conv_dgrad_bnr: mean2/invstd2 required with x2");
     a.x2 = ptr<__bf16>(*x2); a.mean2 = ptr<float>(*mean2); a.istd2 = ptr<float>(*invstd2);
   }
-  if (!a.mask && mscale.has_value() && mscale->defined()) {
+  if (!a.mask && !a.mbits && mscale.has_value() && mscale->defined()) {
     TORCH_CHECK(mshift.has_value() && mshift->defined(), "conv_dgrad_bnr: mshift required with mscale");
     PCMP_CHECK_F32(*mscale); PCMP_CHECK_F32(*mshift);
     a.msc = ptr<float>(*mscale); a.msh = ptr<float>(*mshift);
@@ -1589,7 +1609,7 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::conv_dgrad);
   m.def("conv_dgrad_bnr(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? ymask, "
         "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2, Tensor? mscale, "
-        "Tensor? mshift, Tensor? wt=None) -> Tensor[]",
+        "Tensor? mshift, Tensor? wt=None, Tensor? ymask_bits=None) -> Tensor[]",
         &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
         &pcmp::conv_wgrad);

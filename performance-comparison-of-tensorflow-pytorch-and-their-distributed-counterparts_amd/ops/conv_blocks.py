@@ -109,10 +109,11 @@ class _TailBN:
     ReLU, which is all this block's backward consumes."""
 
     __slots__ = ("out_ptr", "out_shape", "c", "mean", "invstd", "cd", "meand", "invstdd", "g_ptr", "parts",
-                 "__weakref__")
+                 "mbits", "__weakref__")
 
-    def __init__(self, out, c, mean, invstd, cd, meand, invstdd):
+    def __init__(self, out, c, mean, invstd, cd, meand, invstdd, mbits=None):
         self.out_ptr, self.out_shape = out.data_ptr(), tuple(out.shape)
+        self.mbits = mbits   # out > 0 as bits (1 byte / 8 channels): the next block's dgrad mask
         self.c, self.mean, self.invstd = c, mean, invstd
         self.cd, self.meand, self.invstdd = cd, meand, invstdd
         self.g_ptr = None
@@ -131,8 +132,10 @@ def _link_prev_tail(x):
 
 def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
     """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue."""
-    r = K.conv_dgrad_bnr(dh, w, H, W, L.stride, L.pad, resid, x, prev.c, prev.mean, prev.invstd,
-                         prev.cd, prev.meand, prev.invstdd, None, None, compute_weight_t(L.weight, dh.dtype))
+    mask = None if prev.mbits is not None else x
+    r = K.conv_dgrad_bnr(dh, w, H, W, L.stride, L.pad, resid, mask, prev.c, prev.mean, prev.invstd,
+                         prev.cd, prev.meand, prev.invstdd, None, None, compute_weight_t(L.weight, dh.dtype),
+                         prev.mbits)
     prev.parts = r[1:]
     prev.g_ptr = r[0].data_ptr()
     return r[0]
@@ -165,15 +168,18 @@ class ResidualBlockFn(torch.autograd.Function):
                 acts.append(h)
             else:
                 last = (sc, sh)
+        # the block output's ReLU mask as bits, for the next block's fused dgrad epilogue
+        mbits = (torch.empty(cs[-1].numel() // 8, dtype=torch.uint8, device=x.device)
+                 if any(ctx.needs_input_grad) and cs[-1].shape[-1] % 8 == 0 else None)
         if down is not None:
             cd, meand, invstdd, scd, shd = _conv_bn_train(x, down, dtype)
-            out = K.bn_apply(cs[-1], last[0], last[1], cd, scd, shd, True)
+            out = K.bn_apply(cs[-1], last[0], last[1], cd, scd, shd, True, mbits)
         else:
             cd = meand = invstdd = None
-            out = K.bn_apply(cs[-1], last[0], last[1], x, None, None, True)
+            out = K.bn_apply(cs[-1], last[0], last[1], x, None, None, True, mbits)
         if any(ctx.needs_input_grad):
             ctx.prev_tail = _link_prev_tail(x) if ctx.needs_input_grad[0] else None
-            tail = _TailBN(out, cs[-1], stats[-1][0], stats[-1][1], cd, meand, invstdd)
+            tail = _TailBN(out, cs[-1], stats[-1][0], stats[-1][1], cd, meand, invstdd, mbits)
             _LAST_TAIL[0] = weakref.ref(tail)
             ctx.tail = tail
             ctx.save_for_backward(x, out)

@@ -47,8 +47,10 @@ def conv_dgrad(dy, w, H, W, stride, pad, resid=None, wt=None):
 
 
 def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None,
-                   mscale=None, mshift=None, wt=None):
-    if ymask is None and mscale is not None:      # mask recomputed from x: relu(x * scale + shift) > 0
+                   mscale=None, mshift=None, wt=None, ymask_bits=None):
+    if ymask_bits is not None:                    # mask as bits (bn_apply mbits)
+        ymask = unpack_mask_bits(ymask_bits, x.shape)
+    elif ymask is None and mscale is not None:    # mask recomputed from x: relu(x * scale + shift) > 0
         ymask = (x.float() * mscale + mshift).reshape(x.shape)
     g = _masked(conv_dgrad(dy, w, H, W, stride, pad, resid, wt), ymask).to(dy.dtype).contiguous()
     return [g] + bn_bwd_reduce(g, None, x, mean, invstd, x2, mean2, invstd2)
@@ -95,13 +97,32 @@ def bn_eval_coeff(gamma, beta, running_mean, running_var, eps):
     return [scale, b - running_mean.float() * scale]
 
 
-def bn_apply(x, scale, shift, x2=None, scale2=None, shift2=None, relu=False):
+_BIT_WEIGHTS = {}
+
+
+def pack_mask_bits(y):
+    """uint8 [numel/8]: bit e of byte i = y.flatten()[8i+e] > 0 (the backward ReLU mask)."""
+    w = _BIT_WEIGHTS.get(y.device)
+    if w is None:
+        w = _BIT_WEIGHTS[y.device] = (2 ** torch.arange(8, device=y.device)).to(torch.int32)
+    return ((y.reshape(-1, 8).float() > 0).to(torch.int32) * w).sum(1).to(torch.uint8)
+
+
+def unpack_mask_bits(bits, shape):
+    b = bits.to(torch.int32).reshape(-1, 1) >> torch.arange(8, device=bits.device).to(torch.int32)
+    return (b & 1).to(torch.float32).reshape(shape)
+
+
+def bn_apply(x, scale, shift, x2=None, scale2=None, shift2=None, relu=False, mbits=None):
     y = x.float() * scale + shift
     if x2 is not None:
         y = y + (x2.float() * scale2 + shift2 if scale2 is not None else x2.float())
     if relu:
         y = torch.relu(y)
-    return y.to(x.dtype)
+    y = y.to(x.dtype)
+    if mbits is not None:
+        mbits.copy_(pack_mask_bits(y))
+    return y
 
 
 def _masked(dy, ymask):

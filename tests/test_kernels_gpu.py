@@ -106,6 +106,12 @@ def test_conv_dgrad_bn_reduce_fused(gpu, shape):
     assert (out[0][ymask <= 0] == 0).all()
     for a, b in zip(out[1:], outr[1:]):
         close(a.sum(0), b.sum(0), rtol=2e-2, atol=2e-1)
+    # block-output form: the mask as bits (bn_apply mbits) gives exactly the tensor-mask result
+    bits = ref.pack_mask_bits(ymask)
+    outb = _ops().conv_dgrad_bnr(dy, w, H, W, s, p, res.clone() if has_res else None, None, x, mean, invstd,
+                                 x2, mean2, invstd2, None, None, None, bits)
+    for a, b in zip(outb, out):
+        assert torch.equal(a, b)
     if not dual:
         # intermediate-layer form: ReLU mask recomputed from x (relu(x * scale + shift) > 0)
         sc, sh = torch.randn(C, device=gpu), torch.randn(C, device=gpu) * 0.5
@@ -164,6 +170,9 @@ def test_bn_forward_backward(gpu, C):
     y = _ops().bn_apply(x, sc, sh, x2, None, None, True)
     yr = ref.bn_apply(x, scr, shr, x2, None, None, True)
     close(y, yr)
+    mb = torch.empty(y.numel() // 8, dtype=torch.uint8, device=gpu)
+    assert torch.equal(_ops().bn_apply(x, sc, sh, x2, None, None, True, mb), y)
+    assert torch.equal(mb, ref.pack_mask_bits(y))
     dy = rnd(M, C, dev=gpu)
     p1 = _ops().bn_bwd_reduce(dy, y, x, mean, invstd, None, None, None)[0]
     # the ReLU mask comes from the kernel's own y on both sides: a bf16 rounding flip of y at 0 would

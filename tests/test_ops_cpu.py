@@ -101,3 +101,15 @@ def test_batched_weight_transpose_reference():
     w = compute_weight(ps[0], torch.bfloat16)
     assert torch.equal(K.conv_dgrad(dy, w, 5, 5, 1, 1, None, compute_weight_t(ps[0], torch.bfloat16)),
                        K.conv_dgrad(dy, w, 5, 5, 1, 1, None))
+
+
+def test_mask_bits_roundtrip_reference():
+    y = torch.randn(3, 5, 16).relu().to(torch.bfloat16)
+    bits = ref.pack_mask_bits(y)
+    assert bits.dtype == torch.uint8 and bits.numel() == y.numel() // 8
+    assert torch.equal(ref.unpack_mask_bits(bits, y.shape) > 0, y.float() > 0)
+    mb = torch.empty_like(bits)
+    x = torch.randn(3, 5, 16).to(torch.bfloat16)
+    sc, sh = torch.randn(16), torch.randn(16)
+    out = ref.bn_apply(x, sc, sh, None, None, None, True, mb)
+    assert torch.equal(mb, ref.pack_mask_bits(out))
