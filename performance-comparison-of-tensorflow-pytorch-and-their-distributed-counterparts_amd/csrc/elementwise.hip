@@ -31,9 +31,13 @@ static int grid_for(int64_t n, int block = 256, int cap = 4096) {
 
 // ---------------------------------------------------------------- max pool (NHWC) -------------
 // y[n,p,q,c] = max over window; idx[n,p,q,c] = argmax position inside the window (uint8)
+// Optional fused BatchNorm(+ReLU) prologue (sc/sh non-null): the pooled value is
+// bf16(relu(x * sc + sh)), exactly what a separate bn_apply would have stored -- the stem's
+// normalised activation is never written (ResNet stem: conv -> BN -> ReLU -> maxpool).
 __global__ void maxpool_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
                                    uint8_t* __restrict__ idx, int N, int H, int W, int C, int P, int Q,
-                                   int k, int s, int pad) {
+                                   int k, int s, int pad, const float* __restrict__ sc,
+                                   const float* __restrict__ sh) {
   const int CV = C / 8;
   const int64_t total = (int64_t)N * P * Q * CV;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -43,10 +47,14 @@ __global__ void maxpool_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restr
     const int q = t % Q; t /= Q;
     const int p = t % P;
     const int n = t / P;
-    float best[8];
+    float best[8], a[8], b[8];
     int bi[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY; bi[e] = 0;
+      a[e] = sc ? sc[cv * 8 + e] : 1.f;
+      b[e] = sc ? sh[cv * 8 + e] : 0.f;
+    }
     for (int r = 0; r < k; ++r) {
       const int h = p * s - pad + r;
       if ((unsigned)h >= (unsigned)H) continue;
@@ -55,6 +63,10 @@ __global__ void maxpool_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restr
         if ((unsigned)w >= (unsigned)W) continue;
         float v[8];
         ld8(x + (((size_t)n * H + h) * W + w) * C + cv * 8, v);
+        if (sc) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = bf2f(f2bf(fmaxf(v[e] * a[e] + b[e], 0.f)));
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (v[e] > best[e] || (v[e] != v[e])) { best[e] = v[e]; bi[e] = r * k + c; }
@@ -104,6 +116,84 @@ __global__ void maxpool_bwd_kernel(const __bf16* __restrict__ dy, const uint8_t*
       }
     }
     st8(dx + i * 8, acc);
+  }
+}
+
+// Stem backward fused: gather-form maxpool backward + ReLU mask recomputed from the pre-BN input
+// c (relu(c * sc + sh) > 0) + the BatchNorm-backward partial sums of that BN, per block of rows:
+// writes g = bf16(sum of dy over the windows whose argmax is the pixel) * mask and part [T][2][C]
+// = (sum g, sum g * (c - mean) * invstd).  Replaces maxpool_bwd + bn_bwd_reduce (which re-read the
+// gradient and the normalised activation).  Block = 256 threads = rpp pixel rows x tpr channel
+// vectors (C/8 <= 256).
+__global__ void maxpool_bwd_bnr_kernel(const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                       const __bf16* __restrict__ cx, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, const float* __restrict__ sc,
+                                       const float* __restrict__ sh, __bf16* __restrict__ g_out,
+                                       float* __restrict__ part, int N, int H, int W, int C, int P, int Q, int k,
+                                       int s, int pad, int rows_per_block) {
+  extern __shared__ float red[];   // [rpp][2][C]
+  const int CV = C / 8;
+  const int tpr = CV, rpp = 256 / CV;
+  const int tid = threadIdx.x;
+  const int tr = tid / tpr, cv = tid % tpr;
+  const int M = N * H * W;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], is[8], a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[cv * 8 + e]; is[e] = invstd[cv * 8 + e];
+    a[e] = sc[cv * 8 + e]; b[e] = sh[cv * 8 + e];
+  }
+  if (tr < rpp) {
+    for (int row = r0 + tr; row < r1; row += rpp) {
+      const int w = row % W;
+      const int t = row / W;
+      const int h = t % H;
+      const int n = t / H;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
+      const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
+      for (int p = p_lo; p <= p_hi; ++p) {
+        const int r = h - (p * s - pad);
+        if (r < 0 || r >= k) continue;
+        for (int q = q_lo; q <= q_hi; ++q) {
+          const int c = w - (q * s - pad);
+          if (c < 0 || c >= k) continue;
+          const size_t o = (((size_t)n * P + p) * Q + q) * C + cv * 8;
+          const uint64_t packed = *reinterpret_cast<const uint64_t*>(idx + o);
+          float gg[8];
+          ld8(dy + o, gg);
+          const int pos = r * k + c;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((int)((packed >> (8 * e)) & 0xff) == pos) acc[e] += gg[e];
+        }
+      }
+      const size_t oi = (size_t)row * C + cv * 8;
+      float xv[8];
+      ld8(cx + oi, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gr = bf2f(f2bf(acc[e]));
+        acc[e] = (xv[e] * a[e] + b[e] > 0.f) ? gr : 0.f;
+        sg[e] += acc[e];
+        sgx[e] += acc[e] * (xv[e] - mu[e]) * is[e];
+      }
+      st8(g_out + oi, acc);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(tr * 2 + 0) * C + cv * 8 + e] = sg[e];
+      red[(tr * 2 + 1) * C + cv * 8 + e] = sgx[e];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * C; i += blockDim.x) {
+    const int which = i / C, c = i % C;
+    float t = 0.f;
+    for (int r = 0; r < rpp; ++r) t += red[(r * 2 + which) * C + c];
+    part[(size_t)blockIdx.x * 2 * C + i] = t;
   }
 }
 
@@ -321,8 +411,15 @@ __global__ void nchw_to_nhwc_kernel(const T* __restrict__ x, __bf16* __restrict_
 }
 
 // ---------------------------------------------------------------- host ---------------------------
-std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx) {
+std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
+                                    const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift) {
   PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
+  const bool bn = scale.has_value() && scale->defined();
+  if (bn) {
+    PCMP_CHECK_F32(*scale);
+    TORCH_CHECK(shift.has_value() && shift->defined() && scale->numel() == x.size(3) && shift->numel() == x.size(3),
+                "maxpool_fwd: fused BN needs per-channel scale and shift");
+  }
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   TORCH_CHECK(C % 8 == 0 && k * k <= 255, "maxpool: C%8 / k");
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
@@ -331,7 +428,7 @@ std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, i
   const int64_t total = (int64_t)N * P * Q * (C / 8);
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
                      ptr<__bf16>(y), want_idx ? ptr<uint8_t>(idx) : nullptr, N, H, W, C, P, Q, (int)k, (int)s,
-                     (int)pad);
+                     (int)pad, bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr);
   PCMP_LAUNCH_CHECK();
   if (want_idx) return {y, idx};
   return {y};
@@ -347,6 +444,34 @@ at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, i
                      ptr<uint8_t>(idx), ptr<__bf16>(dx), N, (int)H, (int)W, C, P, Q, (int)k, (int)s, (int)pad);
   PCMP_LAUNCH_CHECK();
   return dx;
+}
+
+// fused stem backward (see maxpool_bwd_bnr_kernel): returns [g, part]
+std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& cx,
+                                        const at::Tensor& mean, const at::Tensor& invstd, const at::Tensor& scale,
+                                        const at::Tensor& shift, int64_t k, int64_t s, int64_t pad) {
+  PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy); PCMP_CHECK_BF16(cx); PCMP_CHECK_CONTIG(cx);
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.numel() == dy.numel(), "maxpool_bwd_bnr: idx");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  const int H = cx.size(1), W = cx.size(2);
+  TORCH_CHECK(cx.size(0) == N && cx.size(3) == C && C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0,
+              "maxpool_bwd_bnr: channel layout");
+  for (const at::Tensor* t : {&mean, &invstd, &scale, &shift}) {
+    PCMP_CHECK_F32(*t);
+    TORCH_CHECK(t->numel() == C, "maxpool_bwd_bnr: per-channel vectors");
+  }
+  const int M = N * H * W, rpp = 256 / (C / 8);
+  int rpb = std::max(rpp, ceil_div(M, 2048));
+  rpb = ceil_div(rpb, rpp) * rpp;
+  const int T = ceil_div(M, rpb);
+  auto g = at::empty_like(cx);
+  auto part = at::empty({T, 2, C}, cx.options().dtype(at::kFloat));
+  hipLaunchKernelGGL(maxpool_bwd_bnr_kernel, dim3(T), dim3(256), (size_t)rpp * 2 * C * sizeof(float), cur_stream(),
+                     ptr<__bf16>(dy), ptr<uint8_t>(idx), ptr<__bf16>(cx), ptr<float>(mean), ptr<float>(invstd),
+                     ptr<float>(scale), ptr<float>(shift), ptr<__bf16>(g), ptr<float>(part), N, H, W, C, P, Q,
+                     (int)k, (int)s, (int)pad, rpb);
+  PCMP_LAUNCH_CHECK();
+  return {g, part};
 }
 
 at::Tensor gap_fwd(const at::Tensor& x) {
@@ -465,7 +590,11 @@ at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad, double scale, const c
 }  // namespace pcmp
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
-  m.def("maxpool_fwd(Tensor x, int k, int s, int pad, bool want_idx) -> Tensor[]", &pcmp::maxpool_fwd);
+  m.def("maxpool_fwd(Tensor x, int k, int s, int pad, bool want_idx, Tensor? scale=None, Tensor? shift=None) -> Tensor[]",
+        &pcmp::maxpool_fwd);
+  m.def("maxpool_bwd_bnr(Tensor dy, Tensor idx, Tensor cx, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, "
+        "int k, int s, int pad) -> Tensor[]",
+        &pcmp::maxpool_bwd_bnr);
   m.def("maxpool_bwd(Tensor dy, Tensor idx, int H, int W, int k, int s, int pad) -> Tensor", &pcmp::maxpool_bwd);
   m.def("gap_fwd(Tensor x) -> Tensor", &pcmp::gap_fwd);
   m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor", &pcmp::gap_bwd);

@@ -274,7 +274,9 @@ class ResidualBlockFn(torch.autograd.Function):
 
 
 class StemFn(torch.autograd.Function):
-    """y = maxpool3x3/2( relu( BN( conv7x7/2(x) ) ) )."""
+    """y = maxpool3x3/2( relu( BN( conv7x7/2(x) ) ) ): conv (+BN statistics) -> finalize -> pooling with
+    the BN + ReLU applied in its prologue; backward = one fused pooling/mask/BN-reduction pass, the
+    BN-backward apply, WGRAD."""
 
     @staticmethod
     def forward(ctx, x, stem, *params):
@@ -284,11 +286,11 @@ class StemFn(torch.autograd.Function):
             return K.maxpool_fwd(_conv_bn_eval(x, L, dtype, True), 3, 2, 1, False)[0]
         _params.WEIGHT_GEN[0] += 1
         c, mean, invstd, sc, sh = _conv_bn_train(x, L, dtype)
-        a = K.bn_apply(c, sc, sh, None, None, None, True)
-        y, idx = K.maxpool_fwd(a, 3, 2, 1, True)
+        # BN + ReLU fused into the pooling prologue: the normalised activation is never stored
+        y, idx = K.maxpool_fwd(c, 3, 2, 1, True, sc, sh)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(x)
-            ctx.state = (c, a, idx, mean, invstd)
+            ctx.state = (c, sc, sh, idx, mean, invstd)
             ctx.stem = stem
             ctx.params = params
         else:
@@ -298,11 +300,12 @@ class StemFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
-        c, a, idx, mean, invstd = ctx.state
+        c, sc, sh, idx, mean, invstd = ctx.state
         L = ctx.stem.conv
         grads = {}
-        da = K.maxpool_bwd(dy.contiguous(), idx, a.shape[1], a.shape[2], 3, 2, 1)
-        outs, gr = _bn_backward(da, a, c, mean, invstd, L)
+        # pooling backward + ReLU mask (recomputed from c) + BN-backward partials in one pass
+        r = K.maxpool_bwd_bnr(dy.contiguous(), idx, c, mean, invstd, sc, sh, 3, 2, 1)
+        outs, gr = _bn_backward(r[0], None, c, mean, invstd, L, parts=r[1:])
         grads.update(gr)
         dc = outs[0]
         _wgrad(L, dc, x, grads)

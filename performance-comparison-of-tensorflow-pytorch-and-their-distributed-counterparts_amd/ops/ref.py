@@ -169,7 +169,9 @@ def bn_bwd_apply(dy, ymask, x, coef, x2=None, coef2=None, want_g=False):
 
 
 # ------------------------------------------------------------------------------ pooling
-def maxpool_fwd(x, k, s, pad, want_idx):
+def maxpool_fwd(x, k, s, pad, want_idx, scale=None, shift=None):
+    if scale is not None:     # fused BN + ReLU prologue
+        x = torch.relu(x.float() * scale + shift).to(x.dtype)
     N, H, W, C = x.shape
     y, gidx = F.max_pool2d(_nchw(x), k, s, pad, return_indices=True)
     P, Q = y.shape[2], y.shape[3]
@@ -195,6 +197,14 @@ def maxpool_bwd(dy, idx, H, W, k, s, pad):
     dx = torch.zeros(N, C, H * W, dtype=torch.float32, device=dy.device)
     dx.scatter_add_(2, gidx.reshape(N, C, -1), _nchw(dy).reshape(N, C, -1))
     return _nhwc(dx.view(N, C, H, W)).to(dy.dtype).contiguous()
+
+
+def maxpool_bwd_bnr(dy, idx, cx, mean, invstd, scale, shift, k, s, pad):
+    """Stem backward: g = maxpool_bwd(dy) masked by relu(cx * scale + shift) > 0, plus the BN-backward
+    partials [1, 2, C] = (sum g, sum g * (cx - mean) * invstd)."""
+    g = maxpool_bwd(dy, idx, cx.shape[1], cx.shape[2], k, s, pad)
+    g = _masked(g, (cx.float() * scale + shift)).to(dy.dtype).contiguous()
+    return [g] + bn_bwd_reduce(g, None, cx, mean, invstd)
 
 
 def gap_fwd(x):

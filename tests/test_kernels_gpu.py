@@ -353,3 +353,28 @@ def test_batched_weight_transpose_and_dgrad_with_pretransposed(gpu):
         a = _ops().conv_dgrad(dy, w, H, W, s, pad, None)
         b = _ops().conv_dgrad(dy, w, H, W, s, pad, None, compute_weight_t(p, torch.bfloat16))
         assert torch.equal(a, b)
+
+
+def test_stem_fused_bn_maxpool(gpu):
+    """Fused stem: maxpool with the BN+ReLU prologue == bn_apply then maxpool (bit-exact values and
+    argmax); fused backward == maxpool_bwd then the masked BN-backward reduction."""
+    torch.manual_seed(3)
+    N, H, W, C = 4, 28, 28, 64
+    c = rnd(N, H, W, C, dev=gpu)
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3
+    a = _ops().bn_apply(c, sc, sh, None, None, None, True)
+    y0, i0 = _ops().maxpool_fwd(a, 3, 2, 1, True)
+    y1, i1 = _ops().maxpool_fwd(c, 3, 2, 1, True, sc, sh)
+    assert torch.equal(y0, y1)
+    assert torch.equal(i0, i1)
+    dy = rnd(*y1.shape, dev=gpu)
+    mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    g, part = _ops().maxpool_bwd_bnr(dy, i1, c, mean, invstd, sc, sh, 3, 2, 1)
+    da = _ops().maxpool_bwd(dy, i1, H, W, 3, 2, 1)
+    gr = torch.where(a.float() > 0, da.float(), torch.zeros_like(da.float())).to(torch.bfloat16)
+    assert torch.equal(g, gr)
+    pr = ref.bn_bwd_reduce(gr, None, c, mean, invstd)[0]
+    close(part.sum(0), pr.sum(0), rtol=1e-3, atol=1e-2)
+    gref, pref = ref.maxpool_bwd_bnr(dy, i1, c, mean, invstd, sc, sh, 3, 2, 1)
+    close(g, gref)
+    close(part.sum(0), pref.sum(0), rtol=1e-3, atol=1e-2)
