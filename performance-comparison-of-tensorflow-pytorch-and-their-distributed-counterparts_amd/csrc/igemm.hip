@@ -1127,11 +1127,14 @@ static void launch8(IgemmParams& p, hipStream_t st) {
 // multiple of BK), no split-K, enough K-tiles for the phase pipeline, and a grid that still covers
 // most CUs with BM = 256 tiles: >= 160 tiles (ResNet-50 layer3 at B=256 has 196 and runs 20-28 %
 // faster than on the 4-wave kernel's 784 tiles; layer4's 98 tiles run 25-35 % slower, measured
-// profiles/r1_igemm8_mintiles_ab.txt).  PCMP_IGEMM8=0 disables it (A/B runs).
+// profiles/r1_igemm8_mintiles_ab.txt), and >= 8 K-tiles: with one block per CU a short main loop
+// cannot hide the load / epilogue latency that two 4-wave blocks per CU overlap (1x1 convs over
+// 256 input channels ran 6-12 % faster on the 4-wave kernel, profiles/r1_igemm8_ab_v2.txt).
+// PCMP_IGEMM8=0 disables it (A/B runs).
 static int use_igemm8(int mode, const IgemmParams& p) {
   if (!igemm8_mode() || mode == MODE_WGRAD || p.nsplit != 1) return 0;
   const int cin = mode == MODE_FWD ? p.C : p.K;
-  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < 4 || p.gn < 256) return 0;
+  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < 8 || p.gn < 256) return 0;
   // (measured: the BN=128 variant does not beat the 4-wave 128x128 kernel; the dual BN-reduce
   //  epilogue of a 128x64 wave tile spills)
   if (mode == MODE_DGRAD && p.bn_x2) return 0;
