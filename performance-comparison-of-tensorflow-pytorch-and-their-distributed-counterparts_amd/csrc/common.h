@@ -99,6 +99,7 @@ inline T* optr(const c10::optional<at::Tensor>& t) {
 
 // Deterministic column reduction of fp32 partials: out[l] (+)= sum_t part[t][l]  (L % 4 == 0).
 // Defined in elementwise.hip; shared by the bias-gradient and LayerNorm-backward reductions.
-void launch_col_reduce(const float* part, int T, int L, float* out, bool accumulate, hipStream_t st);
+void launch_col_reduce(const float* part, int T, int L, float* out, bool accumulate, hipStream_t st,
+                       float* out2 = nullptr, int L1 = -1);
 
 }  // namespace pcmp

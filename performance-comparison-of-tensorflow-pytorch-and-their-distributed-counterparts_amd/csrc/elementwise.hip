@@ -348,8 +348,9 @@ __global__ void colsum_partial_kernel(const __bf16* __restrict__ x, float* __res
 }
 
 // out[l] (+)= sum_t part[t][l]: block = 64 column quads x 4 row groups, float4 loads
+// columns [0, L1) go to out, [L1, L) to out2 (a null destination skips its columns)
 __global__ void col_reduce_kernel(const float* __restrict__ part, int T, int L, float* __restrict__ out,
-                                  int accumulate) {
+                                  int accumulate, float* __restrict__ out2, int L1) {
   const int L4 = L / 4;
   const int q = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -369,16 +370,22 @@ __global__ void col_reduce_kernel(const float* __restrict__ part, int T, int L, 
   __syncthreads();
   if (g == 0 && q < L4) {
     s = (sh[0][threadIdx.x] + sh[1][threadIdx.x]) + (sh[2][threadIdx.x] + sh[3][threadIdx.x]);
-    f32x4* o = reinterpret_cast<f32x4*>(out);
-    if (accumulate) s += o[q];
-    o[q] = s;
+    const int L14 = L1 / 4;
+    f32x4* o = q < L14 ? reinterpret_cast<f32x4*>(out) + q : (out2 ? reinterpret_cast<f32x4*>(out2) + (q - L14) : nullptr);
+    if (q < L14 && !out) o = nullptr;
+    if (o) {
+      if (accumulate) s += *o;
+      *o = s;
+    }
   }
 }
 
-void launch_col_reduce(const float* part, int T, int L, float* out, bool accumulate, hipStream_t st) {
-  TORCH_CHECK(L % 4 == 0, "col_reduce: L % 4");
+void launch_col_reduce(const float* part, int T, int L, float* out, bool accumulate, hipStream_t st, float* out2,
+                       int L1) {
+  if (L1 < 0) L1 = L;
+  TORCH_CHECK(L % 4 == 0 && L1 % 4 == 0, "col_reduce: L % 4");
   hipLaunchKernelGGL(col_reduce_kernel, dim3(ceil_div(L / 4, 64)), dim3(256), 0, st, part, T, L, out,
-                     (int)accumulate);
+                     (int)accumulate, out2, L1);
   PCMP_LAUNCH_CHECK();
 }
 

@@ -559,21 +559,28 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& xs, const at::T
   const int D = xs.size(-1);
   const int M = xs.numel() / D;
   auto dx = at::empty_like(xs);
-  const int rpb = std::max(4, ceil_div(M, 512));
+  static const int target_blocks = [] {   // PCMP_LN_BLOCKS overrides (A/B runs)
+    const char* e = std::getenv("PCMP_LN_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 256;
+  }();
+  const int rpb = std::max(4, ceil_div(M, target_blocks));
   const int T = ceil_div(M, rpb);
   auto part = at::empty({T, 2, D}, mean.options());
   hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(T), dim3(256), (size_t)8 * D * sizeof(float), cur_stream(),
                      ptr<__bf16>(dyc), ptr<__bf16>(xs), ptr<float>(mean), ptr<float>(rstd), ptr<float>(g),
                      ptr<__bf16>(dx), ptr<float>(part), M, D, rpb);
   PCMP_LAUNCH_CHECK();
-  auto red = at::empty({2 * D}, mean.options());
-  launch_col_reduce(ptr<float>(part), T, 2 * D, ptr<float>(red), false, cur_stream());
-  if (dg.has_value() && dg->defined()) {
-    if (accumulate) dg->add_(red.narrow(0, 0, D)); else dg->copy_(red.narrow(0, 0, D));
+  // dgamma / dbeta reduced straight into their (flat-gradient) destinations
+  float* dgp = nullptr;
+  float* dbp = nullptr;
+  for (auto [t, d] : {std::make_pair(&dg, &dgp), std::make_pair(&db, &dbp)}) {
+    if (t->has_value() && (*t)->defined()) {
+      PCMP_CHECK_F32(**t); PCMP_CHECK_CONTIG(**t);
+      TORCH_CHECK((*t)->numel() == D, "layernorm_bwd: dgamma/dbeta size");
+      *d = ptr<float>(**t);
+    }
   }
-  if (db.has_value() && db->defined()) {
-    if (accumulate) db->add_(red.narrow(0, D, D)); else db->copy_(red.narrow(0, D, D));
-  }
+  if (dgp || dbp) launch_col_reduce(ptr<float>(part), T, 2 * D, dgp, accumulate, cur_stream(), dbp, D);
   return dx;
 }
 

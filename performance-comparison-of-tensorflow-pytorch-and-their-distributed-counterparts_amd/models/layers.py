@@ -93,6 +93,7 @@ class Linear(nn.Module):
         wp = torch.zeros(self.out_pad, in_features)
         wp[:out_features] = w
         self.weight = nn.Parameter(wp)
+        self.weight._pcmp_dgrad_t = True   # DGRAD reads a batched transposed shadow (utils/flat.py)
         if bias:
             bound = 1 / math.sqrt(in_features)
             b = torch.zeros(self.out_pad)

@@ -13,7 +13,7 @@ import itertools
 import torch
 
 from .kernels import K
-from .params import compute_weight, emit_grad
+from .params import compute_weight, compute_weight_t, emit_grad
 
 
 class _RNG:
@@ -71,7 +71,8 @@ class LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             w = compute_weight(weight, dy.dtype)
-            dx = K.conv_dgrad(dy4, w.reshape(Nout, 1, 1, Cin), 1, 1, 1, 0, None).reshape(M, Cin)
+            dx = K.conv_dgrad(dy4, w.reshape(Nout, 1, 1, Cin), 1, 1, 1, 0, None,
+                              compute_weight_t(weight, dy.dtype)).reshape(M, Cin)
         return dx, gw, gb, None
 
 

@@ -65,9 +65,12 @@ class FlatParams:
             return
         rows, off, blocks = [], 0, 0
         for p, o in zip(self.params, self.offsets):
-            if p.dim() != 4:
+            if p.dim() == 4:
+                K, R, S, C = p.shape
+            elif p.dim() == 2 and getattr(p, "_pcmp_dgrad_t", False):   # Linear weight [Nout, Cin]
+                (K, C), R, S = p.shape, 1, 1
+            else:
                 continue
-            K, R, S, C = p.shape
             rows.append([o, off, K, R * S, C, blocks])
             p._t_slice = (off, (C, R, S, K))
             blocks += R * S * ((K + 63) // 64) * ((C + 63) // 64)
