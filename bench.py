@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--num-classes", type=int, default=1000)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here")
+    ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over all ranks (SyncBN)")
     ap.add_argument("--local_rank", "--local-rank", type=int, default=None)
     return ap.parse_args()
 
@@ -58,6 +59,9 @@ def build_hip(args, env):
 
     torch.manual_seed(1234)
     model = getattr(resnet, args.model)(num_classes=args.num_classes).to(env.device).train()
+    if getattr(args, "sync_bn", False) and env.world_size > 1:
+        from pcmp.parallel.ddp import convert_sync_batchnorm
+        convert_sync_batchnorm(model)
     flat = FlatParams(model.parameters())
     opt = SGD(flat, lr=args.lr, momentum=0.9, weight_decay=5e-5)
     ddp = DistributedDataParallel(model, flat) if env.world_size > 1 else None
@@ -83,6 +87,8 @@ def build_torch(args, env):
 
     torch.manual_seed(1234)
     model = TorchResNet(args.model, args.num_classes).to(env.device).to(memory_format=torch.channels_last).train()
+    if getattr(args, "sync_bn", False) and env.world_size > 1:
+        model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
     if env.world_size > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[env.local_rank], bucket_cap_mb=32)
     opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5, fused=True)

@@ -410,10 +410,19 @@ std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const
                                     const c10::optional<at::Tensor>& beta,
                                     const c10::optional<at::Tensor>& running_mean,
                                     const c10::optional<at::Tensor>& running_var, double momentum, double eps) {
-  PCMP_CHECK_F32(part);
   const int T = part.size(0), C = part.size(2);
-  auto opts = part.options();
+  auto opts = part.options().dtype(at::kFloat);
   auto out = at::empty({4, C}, opts);
+  if (part.scalar_type() == at::kDouble) {   // pre-reduced (e.g. all-reduced SyncBN) fp64 sums
+    TORCH_CHECK(part.is_contiguous(), "bn_finalize: contiguous partials");
+    hipLaunchKernelGGL(bn_finalize_kernel<double>, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(), ptr<double>(part),
+                       T, C, (double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
+                       optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
+                       ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C);
+    PCMP_LAUNCH_CHECK();
+    return {out[0], out[1], out[2], out[3]};
+  }
+  PCMP_CHECK_F32(part);
   int T2;
   at::Tensor red = reduce_partials(part, T2);
   if (red.defined())
@@ -500,7 +509,16 @@ at::Tensor bn_bwd_finalize(const at::Tensor& part, int64_t count, const c10::opt
                            const c10::optional<at::Tensor>& dgamma, const c10::optional<at::Tensor>& dbeta,
                            bool accumulate) {
   const int T = part.size(0), C = part.size(2);
-  auto coef = at::empty({3, C}, part.options());
+  auto coef = at::empty({3, C}, part.options().dtype(at::kFloat));
+  if (part.scalar_type() == at::kDouble) {   // pre-reduced (e.g. all-reduced SyncBN) fp64 sums
+    TORCH_CHECK(part.is_contiguous(), "bn_bwd_finalize: contiguous partials");
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<double>, dim3(ceil_div(C, 64)), dim3(256), 0, cur_stream(),
+                       ptr<double>(part), T, C, (double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
+                       optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef));
+    PCMP_LAUNCH_CHECK();
+    return coef;
+  }
+  PCMP_CHECK_F32(part);
   int T2;
   at::Tensor red = reduce_partials(part, T2);
   if (red.defined())

@@ -21,10 +21,28 @@ from __future__ import annotations
 import weakref
 
 import torch
+import torch.distributed as dist
 
 from . import params as _params
 from .kernels import K
 from .params import compute_weight, compute_weight_t, emit_grad, sink_or_temp
+
+
+def _sync_group(L):
+    """SyncBN process group of a BN layer (``True`` = default group), or None when not syncing."""
+    g = getattr(L, "sync_group", None)
+    if g is None or not dist.is_available() or not dist.is_initialized():
+        return None
+    return g
+
+
+def _global_sums(part, count, group):
+    """SyncBN: per-tile partials [T,2,C] -> fp64 sums over every rank's batch [1,2,C] and the global
+    element count (ranks hold equal per-rank batches, as DistributedSampler shards guarantee)."""
+    grp = None if group is True else group
+    s = part.double().sum(0, keepdim=True)
+    dist.all_reduce(s, group=grp)
+    return s, count * dist.get_world_size(grp)
 
 
 def _conv_bn_train(x, L, dtype):
@@ -32,6 +50,9 @@ def _conv_bn_train(x, L, dtype):
     w = compute_weight(L.weight, dtype)
     c, part = K.conv_fwd(x, w, L.stride, L.pad, None, None, False, True)
     count = c.numel() // c.shape[-1]
+    grp = _sync_group(L)
+    if grp is not None:   # SyncBN: batch statistics over all ranks
+        part, count = _global_sums(part, count, grp)
     track = L.track_running_stats
     mean, invstd, scale, shift = K.bn_finalize(part, count, L.gamma, L.beta,
                                                L.running_mean if track else None,
@@ -74,15 +95,26 @@ def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=Non
     if parts is None:
         parts = K.bn_bwd_reduce(dy, ymask, x, mean, invstd, x2, mean2, invstd2)
     count = x.numel() // x.shape[-1]
+
+    def finalize(part, Lk, mu, isd, gout, bout, acc):
+        grp = _sync_group(Lk)
+        if grp is None:
+            return K.bn_bwd_finalize(part, count, Lk.gamma, mu, isd, gout, bout, acc)
+        # SyncBN: dgamma/dbeta from this rank's sums (DDP averages them, as torch SyncBatchNorm);
+        # the input-gradient coefficients from the sums over every rank's batch
+        K.bn_bwd_finalize(part, count, Lk.gamma, mu, isd, gout, bout, acc)
+        gsum, gcount = _global_sums(part, count, grp)
+        return K.bn_bwd_finalize(gsum, gcount, Lk.gamma, mu, isd, None, None, False)
+
     gout, acc, fin = sink_or_temp(L.gamma)
     bout, bacc, bfin = sink_or_temp(L.beta)
-    coef = K.bn_bwd_finalize(parts[0], count, L.gamma, mean, invstd, gout, bout, acc or bacc)
+    coef = finalize(parts[0], L, mean, invstd, gout, bout, acc or bacc)
     grads = {L.gamma: fin(), L.beta: bfin()}
     coef2 = None
     if x2 is not None:
         gout2, acc2, fin2 = sink_or_temp(L2.gamma)
         bout2, bacc2, bfin2 = sink_or_temp(L2.beta)
-        coef2 = K.bn_bwd_finalize(parts[1], count, L2.gamma, mean2, invstd2, gout2, bout2, acc2 or bacc2)
+        coef2 = finalize(parts[1], L2, mean2, invstd2, gout2, bout2, acc2 or bacc2)
         grads[L2.gamma] = fin2()
         grads[L2.beta] = bfin2()
     outs = K.bn_bwd_apply(dy, ymask, x, coef, x2, coef2, want_g)

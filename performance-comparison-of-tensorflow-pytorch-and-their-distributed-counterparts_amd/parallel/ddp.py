@@ -155,3 +155,17 @@ class DistributedDataParallel(torch.nn.Module):
 
     def grad_scale(self) -> float:
         return 1.0 / self.world if (self.average and self.world > 1) else 1.0
+
+
+def convert_sync_batchnorm(module: torch.nn.Module, process_group=None) -> torch.nn.Module:
+    """SyncBN option ("per-rank batch statistics, as DDP's default; make SyncBN an
+    option"): every fused conv+BN layer of ``module`` computes its training-mode batch statistics,
+    and its backward reduction, over all ranks of ``process_group`` (default: the world) with one
+    fp64 all-reduce of the per-channel sums each way.  Running statistics are then identical on
+    every rank.  Returns ``module`` (modified in place), like torch.nn.SyncBatchNorm.convert_sync_batchnorm."""
+    from ..models.layers import ConvBN
+    for m in module.modules():
+        if isinstance(m, ConvBN):
+            m.sync_group = process_group if process_group is not None else True
+    return module
+

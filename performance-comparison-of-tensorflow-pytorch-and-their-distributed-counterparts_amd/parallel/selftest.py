@@ -22,6 +22,9 @@ def _build(kind, seed=0):
     if kind == "bilstm":
         from ..models.bilstm import BiLSTMClassifier
         return BiLSTMClassifier(300, 32, 32, 1, 2, 0.0)
+    if kind == "resnet_syncbn":
+        from ..models.resnet import resnet18
+        return resnet18(num_classes=10)
     raise ValueError(kind)
 
 
@@ -29,6 +32,8 @@ def _batch(kind, n, seed=1):
     g = torch.Generator().manual_seed(seed)
     if kind == "mlp":
         return torch.randn(n, 64, generator=g), torch.randint(0, 5, (n,), generator=g)
+    if kind == "resnet_syncbn":
+        return torch.rand(n, 3, 32, 32, generator=g), torch.randint(0, 10, (n,), generator=g)
     ids = torch.randint(1, 300, (n, 10), generator=g)
     ids[::3, 6:] = 0
     return ids, torch.randint(0, 2, (n,), generator=g)
@@ -51,6 +56,10 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     if dev.type == "cuda":
         torch.cuda.set_device(0)
     model = _build(kind, seed=rank).to(dev)      # different init per rank: DDP must broadcast rank 0's
+    if kind == "resnet_syncbn":
+        # BN statistics over both shards == the single-process full batch: gradients match exactly
+        from .ddp import convert_sync_batchnorm
+        convert_sync_batchnorm(model)
     flat = FlatParams(model.parameters(), shadow_dtype=None if dev.type == "cpu" else torch.bfloat16)
     ddp = DistributedDataParallel(model, flat, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
     opt = optim.SGD(flat, lr=0.05, momentum=0.9)
@@ -58,8 +67,8 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     N = 8 * world
     x, y = _batch(kind, N)
     x, y = x.to(dev), y.to(dev)
-    if dev.type == "cuda" and x.is_floating_point():
-        x = x.to(torch.bfloat16)                 # GPU activations are bf16
+    if dev.type == "cuda" and x.is_floating_point() and kind != "resnet_syncbn":
+        x = x.to(torch.bfloat16)                 # GPU activations are bf16 (ResNet converts its fp32 images)
     shard = slice(rank * 8, (rank + 1) * 8)
     # reference: single-process gradient on the full batch with rank 0's initial weights
     ref = _build(kind, seed=0).to(dev)
@@ -71,7 +80,9 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     _loss(model, kind, x[shard], y[shard]).backward()
     ddp.finish_gradient_sync()
     avg = flat.grad * ddp.grad_scale()
-    if dev.type == "cpu":
+    if dev.type == "cpu" and kind == "resnet_syncbn":   # deep net: compare relative to the gradient norm
+        ok_grad = bool((avg - ref_grad).norm() <= 1e-4 * ref_grad.norm())
+    elif dev.type == "cpu":
         ok_grad = torch.allclose(avg, ref_grad, atol=1e-5, rtol=1e-4)
     else:   # bf16 compute: compare at the bf16 noise level relative to the gradient norm
         ok_grad = bool((avg - ref_grad).norm() <= 2e-2 * ref_grad.norm() + 1e-6)
@@ -83,6 +94,11 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     gathered = [torch.zeros_like(flat.master) for _ in range(world)]
     dist.all_gather(gathered, flat.master)
     ok_sync = all(torch.equal(gathered[0], g) for g in gathered)
+    if kind == "resnet_syncbn":   # SyncBN: identical running statistics on every rank
+        rm = torch.cat([b.flatten().float() for n_, b in model.named_buffers() if "running" in n_])
+        grm = [torch.zeros_like(rm) for _ in range(world)]
+        dist.all_gather(grm, rm)
+        ok_sync = ok_sync and all(torch.equal(grm[0], g) for g in grm)
     torch.save({"ok_grad": ok_grad, "ok_sync": ok_sync, "nbuckets": len(ddp.buckets),
                 "maxdiff": float((avg - ref_grad).abs().max())}, os.path.join(out_dir, f"rank{rank}.pt"))
     if dev.type == "cuda":

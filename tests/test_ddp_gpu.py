@@ -23,7 +23,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("kind", ["mlp", "bilstm"])
+@pytest.mark.parametrize("kind", ["mlp", "bilstm", "resnet_syncbn"])
 def test_ddp_equivalence_on_gpu(gpu, tmp_path, kind):
     from pcmp.parallel.selftest import ddp_equivalence_worker
     os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
