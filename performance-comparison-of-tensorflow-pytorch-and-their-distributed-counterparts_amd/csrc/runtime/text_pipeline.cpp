@@ -17,77 +17,11 @@
 #include <torch/extension.h>
 
 #include <string>
-#include <unordered_map>
 #include <vector>
 
+#include "runtime/text_core.h"
+
 namespace pcmp_rt {
-
-static inline bool is_ws(unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
-static inline bool is_punct(unsigned char c) {
-  return (c >= 33 && c <= 47) || (c >= 58 && c <= 64) || (c >= 91 && c <= 96) || (c >= 123 && c <= 126);
-}
-
-// strip HTML tags: every '<...>' span becomes a single space (regex '<[^>]+>' semantics)
-static std::string strip_tags(const std::string& s) {
-  std::string out;
-  out.reserve(s.size());
-  size_t i = 0;
-  while (i < s.size()) {
-    if (s[i] == '<') {
-      size_t j = s.find('>', i + 1);
-      if (j != std::string::npos && j > i + 1) {
-        out.push_back(' ');
-        i = j + 1;
-        continue;
-      }
-    }
-    out.push_back(s[i++]);
-  }
-  return out;
-}
-
-// BERT BasicTokenizer (ASCII punctuation split; bytes >= 0x80 kept inside words)
-static void basic_tokenize(const std::string& text, bool lower, std::vector<std::string>& toks) {
-  std::string cur;
-  for (unsigned char c : text) {
-    if (c == 0 || c == 0xfd) continue;
-    if (is_ws(c)) {
-      if (!cur.empty()) { toks.push_back(cur); cur.clear(); }
-    } else if (is_punct(c)) {
-      if (!cur.empty()) { toks.push_back(cur); cur.clear(); }
-      toks.emplace_back(1, (char)c);
-    } else {
-      cur.push_back(lower && c < 128 ? (char)std::tolower(c) : (char)c);
-    }
-  }
-  if (!cur.empty()) toks.push_back(cur);
-}
-
-struct Vocab {
-  std::unordered_map<std::string, int64_t> map;
-  int64_t unk = 100, cls = 101, sep = 102;
-};
-
-static void wordpiece(const std::string& w, const Vocab& v, std::vector<int64_t>& out) {
-  if (w.size() > 100) { out.push_back(v.unk); return; }
-  std::vector<int64_t> pieces;
-  size_t start = 0;
-  while (start < w.size()) {
-    size_t end = w.size();
-    int64_t found = -1;
-    while (start < end) {
-      std::string sub = w.substr(start, end - start);
-      if (start > 0) sub = "##" + sub;
-      auto it = v.map.find(sub);
-      if (it != v.map.end()) { found = it->second; break; }
-      --end;
-    }
-    if (found < 0) { out.push_back(v.unk); return; }
-    pieces.push_back(found);
-    start = end;
-  }
-  out.insert(out.end(), pieces.begin(), pieces.end());
-}
 
 std::vector<at::Tensor> text_encode(const std::vector<std::string>& texts, const std::vector<std::string>& vocab,
                                     int64_t max_len, bool lower, bool strip) {
@@ -105,23 +39,7 @@ std::vector<at::Tensor> text_encode(const std::vector<std::string>& texts, const
   int64_t* ip = ids.data_ptr<int64_t>();
   int64_t* mp = mask.data_ptr<int64_t>();
 #pragma omp parallel for schedule(dynamic, 16)
-  for (int64_t n = 0; n < N; ++n) {
-    std::vector<std::string> toks;
-    basic_tokenize(strip ? strip_tags(texts[n]) : texts[n], lower, toks);
-    std::vector<int64_t> wp;
-    wp.reserve(toks.size() + 4);
-    for (const auto& t : toks) {
-      wordpiece(t, v, wp);
-      if ((int64_t)wp.size() >= max_len) break;
-    }
-    const int64_t body = std::min<int64_t>((int64_t)wp.size(), max_len - 2);  // truncate (post)
-    int64_t* row = ip + n * max_len;
-    int64_t k = 0;
-    row[k++] = v.cls;
-    for (int64_t i = 0; i < body; ++i) row[k++] = wp[i];
-    row[k++] = v.sep;
-    for (int64_t i = 0; i < max_len; ++i) mp[n * max_len + i] = row[i] > 0 ? 1 : 0;  // padding 'post' = 0
-  }
+  for (int64_t n = 0; n < N; ++n) encode_row(texts[n], v, max_len, lower, strip, ip + n * max_len, mp + n * max_len);
   return {ids, mask};
 }
 

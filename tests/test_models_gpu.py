@@ -112,3 +112,36 @@ def test_resnet18_loss_decreases(gpu):
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0] * 0.5, losses
+
+
+def test_training_is_bitwise_deterministic(gpu):
+    """SURVEY §5.2 deterministic mode: two identical ResNet-18 training runs give bitwise-identical
+    losses, gradients and weights (BN statistics, split-K WGRAD and bias reductions use no atomics;
+    autotuned split counts are cached per shape, so both runs use the same schedule)."""
+    from pcmp.models.resnet import resnet18
+    from pcmp.ops import cross_entropy
+    from pcmp.optim import SGD
+    from pcmp.utils.flat import FlatParams
+
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.rand(16, 3, 64, 64, device=gpu, generator=g)
+    y = torch.randint(0, 10, (16,), device=gpu, generator=g)
+
+    def run():
+        torch.manual_seed(11)
+        m = resnet18(num_classes=10).to(gpu).train()
+        flat = FlatParams(m.parameters())
+        opt = SGD(flat, lr=0.01, momentum=0.9)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = cross_entropy(m.forward_logits(x), y)
+            loss.backward()
+            opt.step()
+            losses.append(loss.detach().clone())
+        torch.cuda.synchronize()
+        return torch.stack(losses), flat.grad.clone(), flat.master.clone()
+
+    a, b = run(), run()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
