@@ -20,6 +20,8 @@ VGG loop zeroes gradients (§0.2-2).  ``reference_compat=True`` reproduces the p
 """
 from __future__ import annotations
 
+import contextlib
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -32,6 +34,8 @@ from ..parallel.metrics import all_reduce_max, all_reduce_sum
 from ..utils import report as R
 from ..utils.checkpoint import BestCheckpoint
 from ..utils.flat import FlatParams
+from ..utils.misc import roctx_range
+from ..utils.timer import PhaseTimer
 
 
 @dataclass
@@ -43,22 +47,48 @@ class TrainState:
     sched: object = None
     clip: float | None = None
     history: dict = field(default_factory=lambda: {"train_loss": [], "test_loss": [], "test_acc": []})
+    timer: PhaseTimer | None = None   # per-phase device time, PCMP_PHASE_TIMES=1
+
+    def phase(self, name):
+        """Phase bracket: HIP-event device time + a roctx range for rocprofv3 (when timing)."""
+        if self.timer is None:
+            return contextlib.nullcontext()
+        stack = contextlib.ExitStack()
+        stack.enter_context(roctx_range(name))
+        stack.enter_context(self.timer.phase(name))
+        return stack
 
     def zero_grad(self):
         self.opt.zero_grad()
 
     def backward_step(self, loss):
-        loss.backward()
+        with self.phase("backward"):
+            loss.backward()
         if self.ddp is not None:
-            self.ddp.finish_gradient_sync()
-        scale = self.ddp.grad_scale() if self.ddp is not None else 1.0
-        if self.clip is not None:
-            self.opt.clip_grad_norm(self.clip, pre_scale=scale, post_scale=scale)
-        else:
-            self.opt.set_grad_scale(scale if scale != 1.0 else None)
-        self.opt.step()
-        if self.sched is not None:
-            self.sched.step()
+            with self.phase("comm"):     # join of the bucket all-reduces overlapped with backward
+                self.ddp.finish_gradient_sync()
+        with self.phase("optimizer"):
+            scale = self.ddp.grad_scale() if self.ddp is not None else 1.0
+            if self.clip is not None:
+                self.opt.clip_grad_norm(self.clip, pre_scale=scale, post_scale=scale)
+            else:
+                self.opt.set_grad_scale(scale if scale != 1.0 else None)
+            self.opt.step()
+            if self.sched is not None:
+                self.sched.step()
+        if self.timer is not None:
+            self.timer.step()
+
+    def phase_report(self, printer=None):
+        """Summarise the per-phase device times into ``history['phases']`` (and print one line)."""
+        if self.timer is None:
+            return None
+        summ = self.timer.summary()
+        self.history["phases"] = summ
+        if printer is not None:
+            parts = [f"{k} {v.get('device_ms_mean', 0.0):.3f} ms" for k, v in summ.items()]
+            printer("[phase times, device mean per step] " + ", ".join(parts))
+        return summ
 
 
 def make_state(model, optimizer="sgd", lr=0.1, distributed=False, clip=None, shadow_dtype=None, **opt_kw):
@@ -70,7 +100,9 @@ def make_state(model, optimizer="sgd", lr=0.1, distributed=False, clip=None, sha
     flat = FlatParams(params, shadow_dtype=shadow_dtype)
     opt = pcmp_optim.build(optimizer, flat, lr=lr, **opt_kw)
     ddp = DistributedDataParallel(model, flat) if distributed else None
-    return TrainState(model, flat, opt, ddp, clip=clip)
+    timer = PhaseTimer(warmup_steps=int(os.environ.get("PCMP_PHASE_WARMUP", "2"))) \
+        if os.environ.get("PCMP_PHASE_TIMES") == "1" else None
+    return TrainState(model, flat, opt, ddp, clip=clip, timer=timer)
 
 
 def _logits(model, x):
@@ -114,12 +146,19 @@ def train_image_classifier(state: TrainState, trainloader, testloader, epochs=1,
     for epoch in range(epochs):
         if hasattr(trainloader, "set_epoch") and not reference_compat:
             trainloader.set_epoch(epoch)
-        for x, y in trainloader:
+        it = iter(trainloader)
+        while True:
+            with state.phase("data"):
+                batch = next(it, None)
+            if batch is None:
+                break
+            x, y = batch
             steps += 1
             if verbose_steps:
                 printer(steps)
             state.zero_grad()
-            loss = cross_entropy(_logits(model, x), y)
+            with state.phase("forward"):
+                loss = cross_entropy(_logits(model, x), y)
             state.backward_step(loss)
             running += loss.detach().double()
             n_in_window += 1
@@ -151,6 +190,7 @@ def train_image_classifier(state: TrainState, trainloader, testloader, epochs=1,
         save_fn(model)
     elapsed = all_reduce_max(time.time() - t1)
     printer(R.training_time_line(elapsed))
+    state.phase_report(printer)
     return elapsed
 
 
@@ -178,8 +218,9 @@ def train_text_classifier(state: TrainState, train_loader, val_loader=None, epoc
                 printer(R.batch_progress_line(step, nsteps, R.format_time(time.time() - t0)))
             ids, mask, labels = batch
             state.zero_grad()
-            loss = model(ids, None, mask, labels)[0] if _is_bert(model) else cross_entropy(
-                model.forward_logits(ids, mask), labels)
+            with state.phase("forward"):
+                loss = model(ids, None, mask, labels)[0] if _is_bert(model) else cross_entropy(
+                    model.forward_logits(ids, mask), labels)
             total += loss.detach().double()
             n += 1
             state.backward_step(loss)
@@ -200,6 +241,7 @@ def train_text_classifier(state: TrainState, train_loader, val_loader=None, epoc
             printer(R.val_took_line(R.format_time(time.time() - t0)))
     printer("")
     printer(R.TRAINING_COMPLETE)
+    state.phase_report(printer)
     return times
 
 

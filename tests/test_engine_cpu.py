@@ -139,3 +139,24 @@ def test_label_tables_and_decode():
     top = decode_topk(logits, ["x", "y", "z"], k=2)
     assert [t[0] for t in top[0]] == [1, 2] and top[0][0][1] == "y"
     assert abs(sum(torch.softmax(logits, -1)[0].tolist()) - 1) < 1e-6
+
+
+def test_phase_timer_wiring(monkeypatch):
+    """PCMP_PHASE_TIMES=1 brackets data / forward / backward / optimizer phases."""
+    monkeypatch.setenv("PCMP_PHASE_TIMES", "1")
+    monkeypatch.setenv("PCMP_PHASE_WARMUP", "0")
+    import torch
+    from pcmp.engine.trainer import make_state, train_image_classifier
+    from pcmp.models.layers import MLPHead
+
+    torch.manual_seed(0)
+    m = MLPHead(16, 32, 4, p=0.0)
+    st = make_state(m, "sgd", lr=0.1)
+    assert st.timer is not None
+    data = [(torch.randn(8, 16), torch.randint(0, 4, (8,))) for _ in range(3)]
+    lines = []
+    train_image_classifier(st, data, data[:1], epochs=1, printer=lambda *a: lines.append(" ".join(map(str, a))))
+    ph = st.history["phases"]
+    for k in ("data", "forward", "backward", "optimizer"):
+        assert k in ph and ph[k]["host_s_total"] >= 0.0
+    assert any(l.startswith("[phase times") for l in lines)
