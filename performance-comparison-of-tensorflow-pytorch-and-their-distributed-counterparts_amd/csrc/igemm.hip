@@ -1165,9 +1165,22 @@ static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
   BN = p.gn <= 64 ? 64 : 128;
 }
 
+// FWD/DGRAD grids of fewer 128x128 tiles than CUs (BERT-base's M=4096 token GEMMs with N=768:
+// 192 tiles) run 64x128 tiles instead: twice the workgroups, every CU busy.  PCMP_BM64_SMALLGRID=0
+// disables it (A/B runs).
+static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
+  static const int v = [] {
+    const char* e = std::getenv("PCMP_BM64_SMALLGRID");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v && mode != MODE_WGRAD && p.nsplit == 1 && p.gm > 64 && p.gn > 64 &&
+         ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
+}
+
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
 static int igemm_bm(int mode, const IgemmParams& p) {
   if (use_igemm8(mode, p)) return BM8;
+  if (use_bm64_smallgrid(mode, p)) return 64;
   return p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
 }
 
@@ -1180,6 +1193,9 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
     const int w = wgrad_wide(p);
     if (w == 1) { launch_cfg<MODE, 64, 256, 1, 4>(p, st); return; }
     if (w == 2) { launch_cfg<MODE, 256, 64, 4, 1>(p, st); return; }
+  }
+  if constexpr (MODE != MODE_WGRAD) {
+    if (use_bm64_smallgrid(MODE, p)) { launch_cfg<MODE, 64, 128, 2, 2>(p, st); return; }
   }
   // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)
   if (p.gm <= 32) {
@@ -1540,7 +1556,7 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
     if (it != cache.end()) return it->second;
   }
   std::vector<int> cands;
-  for (int t : {256, 512, 768, 1024, 1536, 2048}) {
+  for (int t : {64, 128, 256, 512, 768, 1024, 1536, 2048}) {
     const int ns = nsplit_for(t);
     if (std::find(cands.begin(), cands.end(), ns) == cands.end()) cands.push_back(ns);
   }

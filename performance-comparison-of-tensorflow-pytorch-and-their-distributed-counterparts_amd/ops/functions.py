@@ -12,6 +12,7 @@ import itertools
 
 import torch
 
+from . import autotune
 from .kernels import K
 from .params import compute_weight, compute_weight_t, emit_grad
 
@@ -46,8 +47,20 @@ class LinearFn(torch.autograd.Function):
         Nout = weight.shape[0]
         w = compute_weight(weight, x.dtype)
         b = bias.detach().float() if bias is not None else None
-        y = K.conv_fwd(x.reshape(M, 1, 1, Cin), w.reshape(Nout, 1, 1, Cin), 1, 0, b, None, relu, False)[0]
-        y = y.reshape(M, Nout)
+
+        def ours():
+            return K.conv_fwd(x.reshape(M, 1, 1, Cin), w.reshape(Nout, 1, 1, Cin), 1, 0, b, None, relu,
+                              False)[0].reshape(M, Nout)
+
+        def blas():   # hipBLASLt: plain GEMM + bias epilogue
+            y = torch.addmm(b.to(x.dtype), x, w.t()) if b is not None else torch.mm(x, w.t())
+            return torch.relu_(y) if relu else y
+
+        if x.is_cuda and x.dtype == torch.bfloat16 and \
+                autotune.pick(("linear_fwd", M, Cin, Nout, b is not None, relu), ours, blas) == "blas":
+            y = blas()
+        else:
+            y = ours()
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(x, y)
             ctx.weight, ctx.bias, ctx.relu = weight, bias, relu
@@ -71,8 +84,19 @@ class LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             w = compute_weight(weight, dy.dtype)
-            dx = K.conv_dgrad(dy4, w.reshape(Nout, 1, 1, Cin), 1, 1, 1, 0, None,
-                              compute_weight_t(weight, dy.dtype)).reshape(M, Cin)
+
+            def ours():
+                return K.conv_dgrad(dy4, w.reshape(Nout, 1, 1, Cin), 1, 1, 1, 0, None,
+                                    compute_weight_t(weight, dy.dtype)).reshape(M, Cin)
+
+            def blas():   # hipBLASLt: dX = dY W
+                return torch.mm(dy, w)
+
+            if dy.is_cuda and dy.dtype == torch.bfloat16 and \
+                    autotune.pick(("linear_dgrad", M, Nout, Cin), ours, blas) == "blas":
+                dx = blas()
+            else:
+                dx = ours()
         return dx, gw, gb, None
 
 
