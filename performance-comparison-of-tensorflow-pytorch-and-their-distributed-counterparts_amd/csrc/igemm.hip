@@ -509,6 +509,41 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
     wb_s = rs % p.S;
     wb_r = rs / p.S;
   }
+  // WGRAD operand walks, advanced incrementally by BK reduction rows per K-step (no per-step
+  // divisions / 32-bit multiplies: those made the loader VALU-bound, profiles/r1_pmc_mix.txt):
+  //   A' row m: element offset m*K + co;
+  //   B' row m = (n, pp, qq): im2col base ((n*H + pp*st)*W + qq*st)*C, kept with ps = pp*st and
+  //   qs = qq*st; +BK rows = (+dn, +dp, +dq) with at most one carry into pp and one into n.
+  int wa_off[MODE == MODE_WGRAD ? NVA : 1];
+  int wb_off[MODE == MODE_WGRAD ? NVB : 1], wb_ps[MODE == MODE_WGRAD ? NVB : 1], wb_qs[MODE == MODE_WGRAD ? NVB : 1];
+  int wg_dqs = 0, wg_Qs = 0, wg_dps = 0, wg_Ps = 0, wg_A0 = 0, wg_A1 = 0, wg_A2 = 0, wb_coloff = 0;
+  if constexpr (MODE == MODE_WGRAD) {
+    const int st = p.stride;
+    const int dq = BK % p.Q, dp = (BK / p.Q) % p.P, dn = BK / (p.P * p.Q);
+    wg_dqs = dq * st; wg_Qs = p.Q * st; wg_dps = dp * st; wg_Ps = p.P * st;
+    const int WC = p.W * p.C;
+    wg_A0 = dq * st * p.C + dp * st * WC + dn * p.H * WC;
+    wg_A1 = st * WC - p.Q * st * p.C;
+    wg_A2 = p.H * WC - p.P * st * WC;
+    wb_coloff = ((wb_r - p.pad) * p.W + (wb_s - p.pad)) * p.C + wb_c;
+#pragma unroll
+    for (int i = 0; i < NVA; ++i) {
+      const int row = (tid + NT * i) / CPR_A;
+      wa_off[i] = (kbeg + row) * p.K + m0 + wa_col;
+    }
+#pragma unroll
+    for (int i = 0; i < NVB; ++i) {
+      const int row = (tid + NT * i) / CPR_B;
+      const int m = min(kbeg + row, p.gk);   // rows past gk are masked; keep the decomposition in range
+      const int n = fdiv(m, p.fd_PQ);
+      const int rem = m - n * p.P * p.Q;
+      const int pp = fdiv(rem, p.fd_Q);
+      const int qq = rem - pp * p.Q;
+      wb_ps[i] = pp * st;
+      wb_qs[i] = qq * st;
+      wb_off[i] = ((n * p.H + pp * st) * p.W + qq * st) * p.C;
+    }
+  }
 
   auto load_stage = [&](int kt) {
     const int k0 = kbeg + kt * BK;
@@ -565,31 +600,32 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       }
     } else {
       // A': rows = reduction index m, cols = output channel co (dy rows are contiguous in co)
+      const bool co_ok = m0 + wa_col < p.gm;
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
-        const int v = tid + NT * i;
-        const int row = v / CPR_A;
-        const int m = k0 + row;
-        const int co = m0 + wa_col;
-        const bool ok = m < kend && co < p.gm;
-        ra[i] = bload16(rsA, ok ? (unsigned)(m * p.K + co) * 2u : kOOB);
+        const int row = (tid + NT * i) / CPR_A;
+        const bool ok = co_ok && k0 + row < kend;
+        ra[i] = bload16(rsA, ok ? (unsigned)wa_off[i] * 2u : kOOB);
+        wa_off[i] += BK * p.K;
       }
       // B': rows = m, cols = j=(r,s,c): im2col gather of x
 #pragma unroll
       for (int i = 0; i < NVB; ++i) {
-        const int v = tid + NT * i;
-        const int row = v / CPR_B;
-        const int m = k0 + row;
-        bool ok = wb_ok && m < kend;
-        const int mm = ok ? m : 0;
-        const int n = fdiv(mm, p.fd_PQ);
-        const int rem = mm - n * p.P * p.Q;
-        const int pp = fdiv(rem, p.fd_Q);
-        const int qq = rem - pp * p.Q;
-        const int yy = pp * p.stride - p.pad + wb_r;
-        const int xx = qq * p.stride - p.pad + wb_s;
-        ok = ok && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-        rb[i] = bload16(rsB, ok ? (unsigned)(((n * p.H + yy) * p.W + xx) * p.C + wb_c) * 2u : kOOB);
+        const int row = (tid + NT * i) / CPR_B;
+        const int yy = wb_ps[i] - p.pad + wb_r;
+        const int xx = wb_qs[i] - p.pad + wb_s;
+        const bool ok = wb_ok && k0 + row < kend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        rb[i] = bload16(rsB, ok ? (unsigned)(wb_off[i] + wb_coloff) * 2u : kOOB);
+        // advance the walk by BK rows
+        int qs = wb_qs[i] + wg_dqs;
+        const bool c1 = qs >= wg_Qs;
+        qs -= c1 ? wg_Qs : 0;
+        int ps = wb_ps[i] + wg_dps + (c1 ? p.stride : 0);
+        const bool c2 = ps >= wg_Ps;
+        ps -= c2 ? wg_Ps : 0;
+        wb_qs[i] = qs;
+        wb_ps[i] = ps;
+        wb_off[i] += wg_A0 + (c1 ? wg_A1 : 0) + (c2 ? wg_A2 : 0);
       }
     }
   };
