@@ -107,14 +107,31 @@ __device__ __forceinline__ float tanh_f(float x) {
   return copysignf(r, x);
 }
 
+// Per-step exchange (cdna_hip_programming.md §6 Guideline 16, recipe R1 with sc1 loads): the
+// handed-off tile (h_t / dgates_t) is stored WRITE-THROUGH (16-B buffer stores with aux = sc1) by
+// one wave, every wave drains (s_waitcnt vmcnt(0)), the workgroup barrier, then ONE lane adds to the
+// direction's arrival counter (relaxed, agent scope); consumers poll that counter relaxed and read
+// the tile with sc1 buffer loads ONLY -- so neither a release (L2 write-back of every dirty line,
+// including the bulk activations this kernel streams out) nor an acquire (L1 invalidate) is needed
+// per step.  Every other load of the kernel reads bytes no workgroup writes in this launch.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rnn_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4v{v.x, v.y, v.z, v.w}, r, (int)off, 0, 16);   // aux 16 = sc1
+}
+__device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);                // aux 16 = sc1
+  return uint4{v[0], v[1], v[2], v[3]};
+}
+
 // grid barrier among the workgroups of one direction: arrive + wait for `target` arrivals
-__device__ __forceinline__ bool dir_barrier(unsigned* counter, unsigned target, unsigned* err) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+__device__ __forceinline__ bool dir_barrier(unsigned* counter, unsigned target, unsigned* err, bool drain = true) {
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave that stored payload drains
   __syncthreads();
   bool ok = true;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add((gu32*)counter, 1u, RLX_AGENT);
     unsigned spins = 0;
     while (__hip_atomic_load((gu32*)counter, RLX_AGENT) < target) {
@@ -125,9 +142,8 @@ __device__ __forceinline__ bool dir_barrier(unsigned* counter, unsigned target, 
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: tile loads are sc1
   __syncthreads();
   return ok;
 }
@@ -154,6 +170,8 @@ __global__ void __launch_bounds__(LT) lstm_fwd_persistent(const LstmFwdParams p)
   __bf16* sW = reinterpret_cast<__bf16*>(smem);
   __bf16* sH = sW + 4 * LJ * H;
   float* sG = reinterpret_cast<float*>(sH + LB * H);
+  __bf16* sHo = reinterpret_cast<__bf16*>(sG + LB * 4 * LJ);   // [LB][LJ] this workgroup's h_t slice
+  const __amdgpu_buffer_rsrc_t rsH = rnn_rsrc(p.hbuf, (unsigned)(4 * LB * H * 2));
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < 4 * LJ * H / 8; i += LT) {
     const int r = i / (H / 8), c8 = i % (H / 8);
@@ -167,6 +185,28 @@ __global__ void __launch_bounds__(LT) lstm_fwd_persistent(const LstmFwdParams p)
   __syncthreads();
   unsigned* cnt = p.counters + dir;
   const int nwg_dir = nub;
+  // input projections and masks of the NEXT step are loaded during the current one (they do not
+  // depend on the recurrence), so only the h exchange sits on the per-step critical path
+  float gxn[2][4];
+  bool vn[2];
+  auto fetch = [&](int stp) {
+    const int tt = dir == 0 ? stp : p.S - 1 - stp;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = tid + LT * k;
+      const int b = q / LJ, j = j0 + q % LJ;
+      vn[k] = false;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gxn[k][g] = 0.f;
+      if (b < p.B) {
+        vn[k] = p.ids[(size_t)b * p.S + tt] > 0;
+        const size_t gb = (((size_t)b * p.S + tt) * 2 + dir) * 4 * H;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) gxn[k][g] = bf2f(reinterpret_cast<const unsigned short*>(p.gx)[gb + g * H + j]);
+      }
+    }
+  };
+  fetch(0);
   for (int step = 0; step < p.S; ++step) {
     const int t = dir == 0 ? step : p.S - 1 - step;
     const int cur = step & 1;
@@ -174,8 +214,8 @@ __global__ void __launch_bounds__(LT) lstm_fwd_persistent(const LstmFwdParams p)
     if (step == 0) {
       for (int i = tid; i < LB * H / 8; i += LT) reinterpret_cast<uint4*>(sH)[i] = uint4{0, 0, 0, 0};
     } else {
-      const __bf16* src = p.hbuf + ((size_t)(cur ^ 1) * 2 + dir) * LB * H;
-      for (int i = tid; i < LB * H / 8; i += LT) reinterpret_cast<uint4*>(sH)[i] = reinterpret_cast<const uint4*>(src)[i];
+      const unsigned src = (unsigned)(((cur ^ 1) * 2 + dir) * LB * H) * 2u;
+      for (int i = tid; i < LB * H / 8; i += LT) reinterpret_cast<uint4*>(sH)[i] = ld16_sc1(rsH, src + i * 16u);
     }
     __syncthreads();
     // ---- pre-activations [LB=32][4LJ=64] = h @ Wslice^T : wave w -> m-tile (w&1), n-tiles 2*(w>>1)+{0,1}
@@ -201,19 +241,17 @@ __global__ void __launch_bounds__(LT) lstm_fwd_persistent(const LstmFwdParams p)
     }
     __syncthreads();
     // ---- cell update for (b, jj): pair q = tid + LT*k
-    __bf16* hdst = p.hbuf + ((size_t)cur * 2 + dir) * LB * H;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int q = tid + LT * k;
       const int b = q / LJ, jj = q % LJ, j = j0 + jj;
       float hn = 0.f;
       if (b < p.B) {
-        const bool valid = p.ids[(size_t)b * p.S + t] > 0;
+        const bool valid = vn[k];
         const size_t gbase = (((size_t)b * p.S + t) * 2 + dir) * 4 * H;
         float pre[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          pre[g] = sG[b * 4 * LJ + g * LJ + jj] + bf2f(reinterpret_cast<const unsigned short*>(p.gx)[gbase + g * H + j]);
+        for (int g = 0; g < 4; ++g) pre[g] = sG[b * 4 * LJ + g * LJ + jj] + gxn[k][g];
         const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanh_f(pre[2]), og = sigm(pre[3]);
         float cn, hv;
         if (valid) {
@@ -233,10 +271,18 @@ __global__ void __launch_bounds__(LT) lstm_fwd_persistent(const LstmFwdParams p)
         p.cst[(((size_t)b * p.S + t) * 2 + dir) * H + j] = cn;
         reinterpret_cast<unsigned short*>(p.hout)[((size_t)b * p.S + t) * 2 * H + dir * H + j] = f2bf(hv);
       }
-      reinterpret_cast<unsigned short*>(hdst)[b * H + j] = f2bf(hn);
+      reinterpret_cast<unsigned short*>(sHo)[b * LJ + jj] = f2bf(hn);
     }
     if (step + 1 < p.S) {
-      if (!dir_barrier(cnt, (unsigned)(step + 1) * nwg_dir, p.err)) return;
+      __syncthreads();
+      if (wid == 0) {   // publish h_t[:, j0:j0+LJ]: 32 rows x 32 B = 64 lanes x 16 B, write-through
+        const int b = lane >> 1, half = lane & 1;
+        const uint4 v = *reinterpret_cast<const uint4*>(sHo + b * LJ + half * 8);
+        st16_sc1(rsH, (unsigned)((cur * 2 + dir) * LB * H + b * H + j0 + half * 8) * 2u, v);
+      }
+      fetch(step + 1);
+      // only wave 0 stored payload; the other waves' loads / bulk stores stay in flight
+      if (!dir_barrier(cnt, (unsigned)(step + 1) * nwg_dir, p.err, wid == 0)) return;
     }
   }
 }
@@ -266,6 +312,8 @@ __global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p)
   __bf16* sWt = reinterpret_cast<__bf16*>(smem);
   __bf16* sD = sWt + LJ * G4;
   float* sR = reinterpret_cast<float*>(sD + LB * G4);
+  __bf16* sDo = reinterpret_cast<__bf16*>(sR + LB * LJ);   // [LB][4][LJ] this workgroup's dgates_t slice
+  const __amdgpu_buffer_rsrc_t rsD = rnn_rsrc(p.dgbuf, (unsigned)(4 * LB * G4 * 2));
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < LJ * G4; i += LT) {
     const int jj = i / G4, r = i % G4;
@@ -276,27 +324,51 @@ __global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p)
   float dhcarry[2] = {0.f, 0.f};  // dh flowing to the previous step (recurrent part)
   __syncthreads();
   unsigned* cnt = p.counters + dir;
+  // per-step inputs that do not depend on the recurrence (mask, output gradient, saved gates and
+  // cell states) are loaded one step ahead
+  float fin[2][7];   // dh_out, i, f, g, o, c, c_prev
+  bool vin[2];
+  auto fetch = [&](int stp) {
+    const int tt = dir == 0 ? p.S - 1 - stp : stp;
+    const int tp = dir == 0 ? tt - 1 : tt + 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = tid + LT * k;
+      const int b = q / LJ, j = j0 + q % LJ;
+      vin[k] = false;
+#pragma unroll
+      for (int u = 0; u < 7; ++u) fin[k][u] = 0.f;
+      if (b < p.B) {
+        vin[k] = p.ids[(size_t)b * p.S + tt] > 0;
+        const size_t gb = (((size_t)b * p.S + tt) * 2 + dir) * 4 * H;
+        fin[k][0] = bf2f(reinterpret_cast<const unsigned short*>(p.dhout)[((size_t)b * p.S + tt) * 2 * H + dir * H + j]);
+        fin[k][1] = p.gates[gb + j];
+        fin[k][2] = p.gates[gb + H + j];
+        fin[k][3] = p.gates[gb + 2 * H + j];
+        fin[k][4] = p.gates[gb + 3 * H + j];
+        fin[k][5] = p.cst[(((size_t)b * p.S + tt) * 2 + dir) * H + j];
+        fin[k][6] = (tp >= 0 && tp < p.S) ? p.cst[(((size_t)b * p.S + tp) * 2 + dir) * H + j] : 0.f;
+      }
+    }
+  };
+  fetch(0);
   for (int step = 0; step < p.S; ++step) {
     const int t = dir == 0 ? p.S - 1 - step : step;      // reverse of the forward order
-    const int tprev = dir == 0 ? t - 1 : t + 1;          // forward predecessor of t
     const int cur = step & 1;
-    __bf16* dst = p.dgbuf + ((size_t)cur * 2 + dir) * LB * G4;
+    const unsigned dst = (unsigned)((cur * 2 + dir) * LB * G4) * 2u;   // byte offset of dgates_t in dgbuf
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int q = tid + LT * k;
       const int b = q / LJ, jj = q % LJ, j = j0 + jj;
       float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
       if (b < p.B) {
-        const bool valid = p.ids[(size_t)b * p.S + t] > 0;
+        const bool valid = vin[k];
         const size_t gbase = (((size_t)b * p.S + t) * 2 + dir) * 4 * H;
-        const float dh = bf2f(reinterpret_cast<const unsigned short*>(p.dhout)[((size_t)b * p.S + t) * 2 * H + dir * H + j]) +
-                         dhcarry[k];
+        const float dh = fin[k][0] + dhcarry[k];
         if (valid) {
-          const float ig = p.gates[gbase + j], fg = p.gates[gbase + H + j], gg = p.gates[gbase + 2 * H + j],
-                      og = p.gates[gbase + 3 * H + j];
-          const float c = p.cst[(((size_t)b * p.S + t) * 2 + dir) * H + j];
-          const bool has_prev = tprev >= 0 && tprev < p.S;
-          const float cprev = has_prev ? p.cst[(((size_t)b * p.S + tprev) * 2 + dir) * H + j] : 0.f;
+          const float ig = fin[k][1], fg = fin[k][2], gg = fin[k][3], og = fin[k][4];
+          const float c = fin[k][5];
+          const float cprev = fin[k][6];
           const float tc = tanh_f(c);
           const float dc = dcreg[k] + dh * og * (1.f - tc * tc);
           dgo = dh * tc * og * (1.f - og);
@@ -315,16 +387,24 @@ __global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p)
         reinterpret_cast<unsigned short*>(dg)[2 * H + j] = f2bf(dgg);
         reinterpret_cast<unsigned short*>(dg)[3 * H + j] = f2bf(dgo);
       }
-      unsigned short* d16 = reinterpret_cast<unsigned short*>(dst) + b * G4;
-      d16[j] = f2bf(dgi);
-      d16[H + j] = f2bf(dgf);
-      d16[2 * H + j] = f2bf(dgg);
-      d16[3 * H + j] = f2bf(dgo);
+      unsigned short* d16 = reinterpret_cast<unsigned short*>(sDo) + b * 4 * LJ + jj;
+      d16[0] = f2bf(dgi);
+      d16[LJ] = f2bf(dgf);
+      d16[2 * LJ] = f2bf(dgg);
+      d16[3 * LJ] = f2bf(dgo);
     }
     if (step + 1 == p.S) break;
-    if (!dir_barrier(cnt, (unsigned)(step + 1) * nub, p.err)) return;
-    // ---- gather dgates_t of all units of this direction [LB][4H] into LDS
-    for (int i = tid; i < LB * G4 / 8; i += LT) reinterpret_cast<uint4*>(sD)[i] = reinterpret_cast<const uint4*>(dst)[i];
+    __syncthreads();
+    {   // publish dgates_t[:, g*H + j0 .. +LJ] for the 4 gates: LB x 4 x 2 chunks of 16 B, write-through
+      const int b = tid >> 3, g = (tid >> 1) & 3, half = tid & 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(sDo + (b * 4 + g) * LJ + half * 8);
+      st16_sc1(rsD, dst + (unsigned)(b * G4 + g * H + j0 + half * 8) * 2u, v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave stored payload: drain before the arrival
+    fetch(step + 1);
+    if (!dir_barrier(cnt, (unsigned)(step + 1) * nub, p.err, false)) return;
+    // ---- gather dgates_t of all units of this direction [LB][4H] into LDS (sc1 loads)
+    for (int i = tid; i < LB * G4 / 8; i += LT) reinterpret_cast<uint4*>(sD)[i] = ld16_sc1(rsD, dst + i * 16u);
     __syncthreads();
     // ---- dh_rec[b][jj] = sum_r dgates[b][r] * W[r][j0+jj] : M=32 (2 tiles), N=16 (1 tile), K=4H
     //      waves 0,1 -> m-tile 0,1 with K split in two halves (waves 2,3 take the upper K half)
@@ -435,7 +515,7 @@ std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh
   LstmFwdParams p{ptr<__bf16>(gx), ptr<__bf16>(whh), idc.data_ptr<int64_t>(), ptr<__bf16>(hout), ptr<float>(gates),
                   ptr<float>(cst), ptr<__bf16>(hbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
                   reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H};
-  const size_t smem = (size_t)4 * LJ * H * 2 + (size_t)LB * H * 2 + (size_t)LB * 4 * LJ * 4;
+  const size_t smem = (size_t)4 * LJ * H * 2 + (size_t)LB * H * 2 + (size_t)LB * 4 * LJ * 4 + (size_t)LB * LJ * 2;
   TORCH_CHECK(smem <= 160 * 1024, "lstm_seq_fwd: LDS budget exceeded");
   hipLaunchKernelGGL(lstm_fwd_persistent, dim3(2 * (H / LJ)), dim3(LT), smem, cur_stream(), p);
   PCMP_LAUNCH_CHECK();
@@ -456,7 +536,7 @@ std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& 
   LstmBwdParams p{ptr<float>(gates), ptr<float>(cst), ptr<__bf16>(whh), idc.data_ptr<int64_t>(), ptr<__bf16>(dh),
                   ptr<__bf16>(dgates), ptr<__bf16>(dgbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
                   reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H};
-  const size_t smem = (size_t)LJ * 4 * H * 2 + (size_t)LB * 4 * H * 2 + (size_t)LB * LJ * 4;
+  const size_t smem = (size_t)LJ * 4 * H * 2 + (size_t)LB * 4 * H * 2 + (size_t)LB * LJ * 4 + (size_t)LB * 4 * LJ * 2;
   TORCH_CHECK(smem <= 160 * 1024, "lstm_seq_bwd: LDS budget exceeded");
   hipLaunchKernelGGL(lstm_bwd_persistent, dim3(2 * (H / LJ)), dim3(LT), smem, cur_stream(), p);
   PCMP_LAUNCH_CHECK();
