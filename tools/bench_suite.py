@@ -71,6 +71,28 @@ def resnet18_train():
     emit(bench="resnet18_train", impl="torch", img_s=B / t, ms=t * 1e3, batch=B)
 
 
+def resnet50_tl_train(B=64):
+    """The reference's measured workload (BASELINE P1): ResNet-50 transfer learning -- frozen
+    backbone with BN in train mode, head Linear(2048,512)-ReLU-Dropout(0.2)-Linear(512,10), Adam 3e-3
+    on the head, NLL loss, batch 64 of 224x224 images."""
+    from pcmp.models.resnet import resnet50_transfer
+    from pcmp.models.torch_ref import TorchResNet
+    x = torch.rand(B, 3, 224, 224, device=dev)
+    y = torch.randint(0, 10, (B,), device=dev)
+    m = resnet50_transfer(10).to(dev).train()
+    t = timeit(hip_train_step(m, lambda: cross_entropy(m.forward_logits(x), y), "adam", 3e-3))
+    emit(bench="resnet50_tl_train", impl="hip", img_s=B / t, ms=t * 1e3, batch=B, vs_reference_P1a=round(B / t / 1.43, 1))
+    head = torch.nn.Sequential(torch.nn.Linear(2048, 512), torch.nn.ReLU(), torch.nn.Dropout(0.2),
+                               torch.nn.Linear(512, 10), torch.nn.LogSoftmax(dim=1))
+    tm = TorchResNet("resnet50", head=head).to(dev).to(memory_format=torch.channels_last).train()
+    for n_, p_ in tm.named_parameters():
+        p_.requires_grad_(n_.startswith("fc."))
+    o = torch.optim.Adam([p_ for p_ in tm.parameters() if p_.requires_grad], lr=3e-3, fused=True)
+    xc = x.contiguous(memory_format=torch.channels_last)
+    t = timeit(torch_train_step(tm, lambda: torch.nn.functional.nll_loss(tm(xc).float(), y), o))
+    emit(bench="resnet50_tl_train", impl="torch", img_s=B / t, ms=t * 1e3, batch=B)
+
+
 def resnet50_infer(n=300):
     from pcmp.engine.inference import Batch1Predictor
     from pcmp.models.resnet import resnet50
@@ -158,7 +180,7 @@ def bert_train():
 
 
 if __name__ == "__main__":
-    names = sys.argv[1:] or ["resnet18_train", "resnet50_infer", "bilstm_train", "bert_train"]
+    names = sys.argv[1:] or ["resnet18_train", "resnet50_tl_train", "resnet50_infer", "bilstm_train", "bert_train"]
     for n in names:
         try:
             globals()[n]()
