@@ -128,8 +128,15 @@ def _bnr_ok(L):
 
 
 def _wgrad(L, dy, x, grads):
-    g = emit_grad(L.weight, lambda out, acc: K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad, acc))
-    grads[L.weight] = g
+    w = L.weight
+    if dy.is_cuda and w.requires_grad and getattr(w, "main_grad", None) is not None and _params.side_stream_enabled():
+        # into the flat gradient buffer on the WGRAD stream, concurrent with this layer's DGRAD
+        _params.run_on_side(lambda: emit_grad(w, lambda out, acc: K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad,
+                                                                                acc)), (dy, x))
+        grads[w] = None
+        return
+    g = emit_grad(w, lambda out, acc: K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad, acc))
+    grads[w] = g
 
 
 class _TailBN:

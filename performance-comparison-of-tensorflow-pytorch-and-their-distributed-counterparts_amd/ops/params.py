@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Callable
 
 import torch
@@ -93,3 +94,49 @@ def sink_or_temp(p: torch.Tensor | None):
         return mg, acc, finish
     tmp = torch.empty(p.shape, dtype=torch.float32, device=p.device)
     return tmp, False, (lambda: tmp)
+
+
+# ------------------------------------------------------------------------------------------------
+# Weight-gradient side stream.  Within a block's backward, WGRAD(L) and DGRAD(L) both depend only on
+# the layer's output gradient, so WGRAD runs on a second HIP stream and fills the CUs that the
+# DGRAD chain leaves idle (small grids, tile tails, the latency-bound BN finalize launches).  The
+# compute stream joins the side stream at the end of every backward pass (autograd engine
+# callback), and the data-parallel bucket launch orders the all-reduce after both streams.
+# PCMP_WGRAD_STREAM=0 keeps everything on one stream.
+_SIDE: dict = {}
+_JOIN_QUEUED = [False]
+
+
+def side_stream_enabled() -> bool:
+    return os.environ.get("PCMP_WGRAD_STREAM", "1") != "0"
+
+
+def active_streams(device):
+    """(compute stream, wgrad stream) pair in use on ``device`` this backward, or ()."""
+    return _SIDE.get(("active", torch.device(device).index), ())
+
+
+def _join(main, side, key):
+    main.wait_stream(side)
+    _SIDE.pop(key, None)
+    _JOIN_QUEUED[0] = False
+
+
+def run_on_side(fn: Callable[[], None], keep_alive) -> None:
+    """Run ``fn`` (kernel launches) on the device's WGRAD stream, ordered after the compute stream's
+    work so far; ``keep_alive`` tensors are recorded on the side stream for the caching allocator."""
+    dev = keep_alive[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev.index)
+    if side is None:
+        side = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    key = ("active", dev.index)
+    _SIDE[key] = (main, side)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        fn()
+    for t in keep_alive:
+        t.record_stream(side)
+    if not _JOIN_QUEUED[0]:
+        _JOIN_QUEUED[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(main, side, key))

@@ -138,6 +138,14 @@ class DistributedDataParallel(torch.nn.Module):
         if self.world <= 1 or not self.require_sync:
             return
         view = self.flat.grad[b.start:b.end]
+        if view.is_cuda:
+            # gradients of a bucket may come from the compute stream (BN, Linear, torch layers) and
+            # from the WGRAD side stream (conv weights): the collective is ordered after both
+            from ..ops.params import active_streams
+            cur = torch.cuda.current_stream(view.device)
+            for s in active_streams(view.device):
+                if s != cur:
+                    cur.wait_stream(s)
         b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def finish_gradient_sync(self):
