@@ -749,21 +749,21 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
 
 
 // ------------------------------------------------------------------------------------------------
-// 8-wave LDS-DMA kernel for the large FWD/DGRAD GEMMs (BM = 256 pixels x BN = 256|128 channels,
-// 512 threads, ~1 block per CU).  Operand tiles are staged global -> LDS by buffer_load ... lds
-// (LDS-DMA: no VGPR round trip, hardware zero-fill for padding / tails through the buffer range
-// check); the XOR swizzle of the row-read image is applied to the per-lane SOURCE chunk and undone
-// on the ds_read (cdna_hip_programming.md §5.4 rule 21).  Each K-tile (BK = 64) is computed in
-// four phases, one output quadrant per phase (16/8 MFMAs per wave); during phase p of tile t the
-// p-th half-tile of tile t+1 is DMA'd into the other LDS buffer, and counted s_waitcnt vmcnt(N)
-// waits retire exactly the half-tile the next phase reads, so operand loads stay in flight across
-// the barriers instead of draining every K-step.  Half-tile issue order (A0, B0, B1, A1) follows
-// the quadrant order (0,0) (0,1) (1,1) (1,0) of the consumer.
+// LDS-DMA kernel for FWD/DGRAD GEMMs with the block-uniform tap walk.  Two instantiations:
+//   8 waves, BM = 256 x BN = 256 (2x4 waves, 128x64 wave tiles), 1 block per CU -- large grids;
+//   4 waves, BM x BN = 128x128 / 256x64 (64x64 wave tiles), 2 blocks per CU -- everything else.
+// Operand tiles are staged global -> LDS by buffer_load ... lds (LDS-DMA: no VGPR round trip and no
+// ds_write -- the register-staged kernel's 16-B LDS stores transfer at ~79 B/clk/CU, a third of the
+// ds_read_b128 rate -- and hardware zero-fill for padding / tails through the buffer range check);
+// the XOR swizzle of the row-read image is applied to the per-lane SOURCE chunk and undone on the
+// ds_read (cdna_hip_programming.md §5.4 rule 21).  Each K-tile (BK = 64) is computed in four
+// phases, one output quadrant per phase; during phase p of tile t the p-th half-tile of tile t+1
+// is DMA'd into the other LDS buffer, and counted s_waitcnt vmcnt(N) waits retire exactly the
+// half-tile the next phase reads, so operand loads stay in flight across the barriers instead of
+// draining every K-step.  Half-tile issue order (A0, B0, B1, A1) follows the quadrant order
+// (0,0) (0,1) (1,1) (1,0) of the consumer.
 constexpr int NT8 = 512;
 constexpr int BM8 = 256;
-template <int BN> struct G8Cfg;
-template <> struct G8Cfg<256> { static constexpr int WM = 2, WN = 4; };
-template <> struct G8Cfg<128> { static constexpr int WM = 4, WN = 2; };   // (not dispatched: see use_igemm8)
 
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
@@ -775,20 +775,22 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int MODE, int BN, int EPI, bool PRIO>
-__global__ void __launch_bounds__(NT8, 1) igemm8_kernel(const IgemmParams p) {
-  constexpr int BM = BM8;
-  constexpr int WM = G8Cfg<BN>::WM, WN = G8Cfg<BN>::WN;
-  constexpr int WTM = BM / WM, WTN = BN / WN;   // 128x64 (BN 256) or 64x64 (BN 128)
+template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI>
+__global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams p) {
+  constexpr int NW = NTHR / 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int TMH = TM / 2, TNH = TN / 2;     // fragments per quadrant
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int NA = 2;                         // LDS-DMA instructions per thread per A half-tile
-  constexpr int NB = BN / 128;                  // ... per B half-tile (BN/2 rows)
-  constexpr int AH = WTM / 2;                   // rows of one wave-row segment of an A half
+  constexpr int NA = BM / 16 / NW;              // LDS-DMA instructions (8 rows each) per wave per A half-tile
+  constexpr int NB = BN / 16 / NW;              // ... per B half-tile
+  constexpr int AH = WTM / 2, BH = WTN / 2;     // rows of one wave-row / wave-column segment of a half
   static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
-  static_assert(TM % 2 == 0 && TN % 2 == 0, "quadrants");
+  static_assert(WM * WN == NW, "one wave tile per wave");
+  static_assert(NA >= 1 && NB >= 1 && NA * NW * 16 == BM && NB * NW * 16 == BN, "loader slots");
+  static_assert(AH % 8 == 0 && BH % 8 == 0 && TM % 2 == 0 && TN % 2 == 0, "quadrants");
+  static_assert(WTN % 32 == 0, "PAIR channel permutation works on 32-row groups");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -849,7 +851,7 @@ __global__ void __launch_bounds__(NT8, 1) igemm8_kernel(const IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int h0 = wid * (8 * NB) + i * 8;
-      const int rho0 = (h0 / 32) * WTN + nh * 32 + h0 % 32;
+      const int rho0 = (h0 / BH) * WTN + nh * BH + h0 % BH;
       b_lds[nh][i] = A_BYTES + rho0 * (BK * 2);
       const int n = n0 + chan_perm<true>(rho0 + (lane >> 3));
       b_off[nh][i] = n < p.gn ? n * p.gk + gch * 8 : -1;
@@ -908,12 +910,11 @@ __global__ void __launch_bounds__(NT8, 1) igemm8_kernel(const IgemmParams p) {
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int j = 0; j < TNH; ++j) {
-        const int row = wc * WTN + nh * 32 + j * 16 + (lane & 15);
+        const int row = wc * WTN + nh * BH + j * 16 + (lane & 15);
         fb[nh][j][kk] = *reinterpret_cast<const bf16x8*>(sB + rr_off(row, kk * 4 + (lane >> 4)));
       }
   };
   auto mma = [&](int mh, int nh) {
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -922,7 +923,6 @@ __global__ void __launch_bounds__(NT8, 1) igemm8_kernel(const IgemmParams p) {
         for (int i = 0; i < TMH; ++i)
           acc[nh * TNH + j][mh * TMH + i] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][j][kk], fa[i][kk], acc[nh * TNH + j][mh * TMH + i], 0, 0, 0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // ---- prologue: tile 0 complete in buffer 0
@@ -957,7 +957,7 @@ __global__ void __launch_bounds__(NT8, 1) igemm8_kernel(const IgemmParams p) {
     if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A0(t+1), B0(t+1)
     lds_barrier();
   }
-  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT8>(p, acc, smem, tid, m0, n0, tile_m, 0);
+  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR>(p, acc, smem, tid, m0, n0, tile_m, 0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1120,43 +1120,77 @@ static int igemm8_min_tiles() {
   return v;
 }
 
-template <int MODE, int BN>
-static void launch8(IgemmParams& p, hipStream_t st) {
-  constexpr int WM = G8Cfg<BN>::WM, WN = G8Cfg<BN>::WN;
-  p.tiles_m = ceil_div(p.gm, BM8);
+template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB>
+static void launch_dma(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
-  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm8: partial-stats buffer too small");
+  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_dma: partial-stats buffer too small");
+  TORCH_CHECK(p.nsplit == 1 && p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0,
+              "igemm_dma: needs the block-uniform tap walk and no split-K");
   const int grid = p.tiles_m * p.tiles_n;
-  size_t smem = (size_t)2 * (BM8 + BN) * BK * 2;
+  size_t smem = (size_t)2 * (BM + BN) * BK * 2;
   const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
   if (epi_red) {
     const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
-    smem = std::max(smem, (size_t)((NT8 / 64) * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
+    smem = std::max(smem, (size_t)((NTHR / 64) * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
   }
   int epi = EPI_PLAIN;
   if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
-#define PCMP_IGEMM8_LAUNCH_P(E, PR)                                                                    \
+#define PCMP_DMA_LAUNCH(E)                                                                              \
   do {                                                                                                \
+    auto kfn = &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E>;                                \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
-      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm8_kernel<MODE, BN, E, PR>), \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
       attr_set = true;                                                                                \
     }                                                                                                 \
-    hipLaunchKernelGGL((igemm8_kernel<MODE, BN, E, PR>), dim3(grid), dim3(NT8), smem, st, p);         \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(NTHR), smem, st, p);                                     \
   } while (0)
-#define PCMP_IGEMM8_LAUNCH(E) PCMP_IGEMM8_LAUNCH_P(E, false)
   if constexpr (MODE == MODE_FWD) {
-    if (epi == EPI_STATS) PCMP_IGEMM8_LAUNCH(EPI_STATS); else PCMP_IGEMM8_LAUNCH(EPI_PLAIN);
+    if (epi == EPI_STATS) PCMP_DMA_LAUNCH(EPI_STATS); else PCMP_DMA_LAUNCH(EPI_PLAIN);
   } else {
-    TORCH_CHECK(epi != EPI_BNR2, "igemm8: dual BN-reduce epilogue not instantiated");
-    if (epi == EPI_BNR) PCMP_IGEMM8_LAUNCH(EPI_BNR);
-    else PCMP_IGEMM8_LAUNCH(EPI_PLAIN);
+    if (epi == EPI_BNR) PCMP_DMA_LAUNCH(EPI_BNR);
+    else if (epi == EPI_BNR2) {
+      if constexpr (NTHR == 256) PCMP_DMA_LAUNCH(EPI_BNR2);
+      else TORCH_CHECK(false, "igemm8: dual BN-reduce epilogue not instantiated");
+    } else PCMP_DMA_LAUNCH(EPI_PLAIN);
   }
-#undef PCMP_IGEMM8_LAUNCH
-#undef PCMP_IGEMM8_LAUNCH_P
+#undef PCMP_DMA_LAUNCH
   PCMP_LAUNCH_CHECK();
+}
+
+// 4-wave LDS-DMA kernel (2 blocks per CU) in place of the register-staged 4-wave kernel for the
+// FWD/DGRAD GEMMs with the block-uniform tap walk and >= 3 K-tiles (measured
+// profiles/r1_dma4_ab.txt: 3x3 layers 10-16 % faster, e.g. layer4 3x3 DGRAD 97 -> 84 us; GEMMs
+// of 2 K-tiles ran up to 9 % slower).  PCMP_DMA4=0 disables it (A/B runs); PCMP_DMA4_N64 picks
+// the narrow-output (gn <= 64) tile: 1 = 128x64 (2x2 waves of 64x32, the default: 6 % faster than
+// 256x64 on the layer1 3x3), 2 = 256x64 (4x1 waves of 64x64), 0 = register-staged kernel.
+static int dma4_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("PCMP_DMA4");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+static int dma4_n64() {
+  static const int v = [] {
+    const char* e = std::getenv("PCMP_DMA4_N64");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+// 0: register-staged kernel; 1: 128x128; 2: 128x64; 3: 256x64
+static int use_dma4(int mode, const IgemmParams& p) {
+  if (!dma4_mode() || mode == MODE_WGRAD || p.nsplit != 1) return 0;
+  const int cin = mode == MODE_FWD ? p.C : p.K;
+  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < 3 || p.gm <= 64) return 0;
+  if (p.gn <= 64) {
+    const int v = dma4_n64();
+    return v == 1 ? 2 : (v == 2 ? 3 : 0);
+  }
+  return 1;
 }
 
 // 8-wave LDS-DMA kernel eligibility: FWD/DGRAD with the block-uniform tap walk (source channels a
@@ -1217,13 +1251,14 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 static int igemm_bm(int mode, const IgemmParams& p) {
   if (use_igemm8(mode, p)) return BM8;
   if (use_bm64_smallgrid(mode, p)) return 64;
+  if (use_dma4(mode, p) == 3) return 256;
   return p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
 }
 
 template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE != MODE_WGRAD) {
-    if (use_igemm8(MODE, p) == 256) { launch8<MODE, 256>(p, st); return; }
+    if (use_igemm8(MODE, p) == 256) { launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st); return; }
   }
   if constexpr (MODE == MODE_WGRAD) {
     const int w = wgrad_wide(p);
@@ -1232,6 +1267,12 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
   }
   if constexpr (MODE != MODE_WGRAD) {
     if (use_bm64_smallgrid(MODE, p)) { launch_cfg<MODE, 64, 128, 2, 2>(p, st); return; }
+    switch (use_dma4(MODE, p)) {
+      case 1: launch_dma<MODE, 128, 128, 2, 2, NT, 2>(p, st); return;
+      case 2: launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st); return;
+      case 3: launch_dma<MODE, 256, 64, 4, 1, NT, 2>(p, st); return;
+      default: break;
+    }
   }
   // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)
   if (p.gm <= 32) {

@@ -11,6 +11,6 @@ tail -2 gpurun_out/iter_tests.log
 timeout -k 10 300 python bench.py ${BENCH_ARGS:---steps 20 --warmup 5} > gpurun_out/iter_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/iter_bench.log; exit 1; }
 tail -1 gpurun_out/iter_bench.log
 if [ "${PROFILE:-1}" = "1" ]; then
-  timeout -k 10 300 python tools/layer_profile.py > gpurun_out/iter_layer_profile.txt 2>&1 || { echo "layer profile failed"; tail -20 gpurun_out/iter_layer_profile.txt; exit 1; }
+  PCMP_WGRAD_STREAM=0 timeout -k 10 300 python tools/layer_profile.py > gpurun_out/iter_layer_profile.txt 2>&1 || { echo "layer profile failed"; tail -20 gpurun_out/iter_layer_profile.txt; exit 1; }
   head -22 gpurun_out/iter_layer_profile.txt
 fi
