@@ -417,6 +417,47 @@ __global__ void nchw_to_nhwc_kernel(const T* __restrict__ x, __bf16* __restrict_
   }
 }
 
+// Stem space-to-depth.  A 7x7 / stride-2 / pad-p convolution over X equals a 4x4 / stride-1 /
+// unpadded convolution over S[n][i][j][(dy*2+dx)*4 + c] = X[n][c][2i+dy-p][2j+dx-p] (zero outside
+// the image and for c >= Cin) with the 7x7 filter embedded in an 8x8 one (ops/conv_blocks.py
+// s2d_weight): the GEMM reduction shrinks from 7*7*8 (Cin padded to 8 for 16-B chunks) to
+// 4*4*16 = 256, four full K-tiles, and every 16-B chunk still holds one tap's channels.
+// One thread per S pixel (16 channels = two 16-B stores).  NHWC: X is [N,H,W,Cs] bf16 (the
+// 8-channel padded stem input) instead of [N,Cin,H,W] f32/u8.
+template <typename T, bool NHWC>
+__global__ void image_to_s2d_kernel(const T* __restrict__ x, __bf16* __restrict__ y, int N, int Cin, int H, int W,
+                                    int Cs, int Hs, int Ws, int pad, float scale, const float* __restrict__ mean,
+                                    const float* __restrict__ stdv) {
+  const int64_t total = (int64_t)N * Hs * Ws;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int j = t % Ws;
+    const int64_t r = t / Ws;
+    const int i = r % Hs, n = r / Hs;
+    float v[16];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int h = 2 * i + (d >> 1) - pad, w = 2 * j + (d & 1) - pad;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float a = 0.f;
+        if (ok && c < Cin) {
+          if constexpr (NHWC) {
+            a = (float)x[(((size_t)n * H + h) * W + w) * Cs + c];
+          } else {
+            a = (float)x[(((size_t)n * Cin + c) * H + h) * W + w] * scale;
+            if (mean) a = (a - mean[c]) / stdv[c];
+          }
+        }
+        v[d * 4 + c] = a;
+      }
+    }
+    st8(y + t * 16, v);
+    st8(y + t * 16 + 8, v + 8);
+  }
+}
+
 // ---------------------------------------------------------------- host ---------------------------
 std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
                                     const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift) {
@@ -594,6 +635,36 @@ at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad, double scale, const c
   return y;
 }
 
+at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c10::optional<at::Tensor>& mean,
+                        const c10::optional<at::Tensor>& stdv, bool nhwc) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4, "image_to_s2d: 4-D input");
+  const int N = x.size(0);
+  const int Cin = nhwc ? std::min<int>(4, x.size(3)) : x.size(1);
+  const int H = nhwc ? x.size(1) : x.size(2), W = nhwc ? x.size(2) : x.size(3);
+  const int Cs = nhwc ? x.size(3) : 0;
+  TORCH_CHECK(Cin <= 4 && pad >= 0, "image_to_s2d: at most 4 input channels");
+  const int Hs = (H + 2 * pad + 1) / 2, Ws = (W + 2 * pad + 1) / 2;
+  auto y = at::empty({N, Hs, Ws, 16}, x.options().dtype(at::kBFloat16));
+  const int64_t total = (int64_t)N * Hs * Ws;
+  if (nhwc) {
+    PCMP_CHECK_BF16(x);
+    hipLaunchKernelGGL((image_to_s2d_kernel<__bf16, true>), dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+                       ptr<__bf16>(x), ptr<__bf16>(y), N, Cin, H, W, Cs, Hs, Ws, (int)pad, 1.f, nullptr, nullptr);
+  } else if (x.scalar_type() == at::kFloat) {
+    hipLaunchKernelGGL((image_to_s2d_kernel<float, false>), dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+                       ptr<float>(x), ptr<__bf16>(y), N, Cin, H, W, 0, Hs, Ws, (int)pad, (float)scale,
+                       optr<float>(mean), optr<float>(stdv));
+  } else {
+    TORCH_CHECK(x.scalar_type() == at::kByte, "image_to_s2d: f32 or u8 NCHW input");
+    hipLaunchKernelGGL((image_to_s2d_kernel<uint8_t, false>), dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+                       ptr<uint8_t>(x), ptr<__bf16>(y), N, Cin, H, W, 0, Hs, Ws, (int)pad, (float)scale,
+                       optr<float>(mean), optr<float>(stdv));
+  }
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
 }  // namespace pcmp
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
@@ -612,4 +683,5 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &pcmp::relu_bwd);
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()", &pcmp::colsum);
   m.def("nchw_to_nhwc(Tensor x, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor", &pcmp::nchw_to_nhwc);
+  m.def("image_to_s2d(Tensor x, int pad, float scale, Tensor? mean, Tensor? stdv, bool nhwc) -> Tensor", &pcmp::image_to_s2d);
 }

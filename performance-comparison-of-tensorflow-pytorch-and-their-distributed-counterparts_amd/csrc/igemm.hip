@@ -1222,7 +1222,7 @@ static int wgrad_wide(const IgemmParams& p) {
     return e ? std::atoi(e) : 1;
   }();
   if (!v) return 0;
-  if (p.gm > 32 && p.gm <= 64 && p.gn >= 256 && p.C == 8) return 1;   // 64 x 256 (stem)
+  if (p.gm > 32 && p.gm <= 64 && p.gn >= 256 && (p.C == 8 || p.C == 16)) return 1;   // 64 x 256 (stem)
   if (p.gn > 32 && p.gn <= 64 && p.gm >= 256) return 2;   // 256 x 64
   return 0;
 }

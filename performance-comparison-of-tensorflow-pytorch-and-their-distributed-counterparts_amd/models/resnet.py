@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from ..ops.conv_blocks import ResidualBlockFn, StemFn
+from ..ops.conv_blocks import ResidualBlockFn, StemFn, stem_s2d_wanted
 from ..ops.kernels import K
 from .layers import Conv2d, ConvBN, GlobalAvgPool, Linear, MLPHead
 
@@ -125,13 +125,18 @@ class ResNet(nn.Module):
         return torch.bfloat16 if device.type == "cuda" else torch.float32
 
     def prepare_input(self, x):
-        """NCHW float/uint8 images -> NHWC compute-dtype, channels padded to 8."""
+        """NCHW float/uint8 images -> NHWC compute-dtype, channels padded to 8 (on the GPU: the
+        16-channel space-to-depth image the stem convolves, see ops/conv_blocks.py)."""
         dt = self._cdtype(x.device)
         if x.dim() == 4 and x.shape[-1] == STEM_CIN_PAD and x.shape[1] != STEM_CIN_PAD:
             h = x
         elif dt == torch.bfloat16:
             scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
-            h = K.nchw_to_nhwc(x.contiguous(), STEM_CIN_PAD, scale, None, None)
+            if x.shape[1] <= 4 and stem_s2d_wanted(x.device):
+                # straight to the space-to-depth layout of the GPU stem (ops/conv_blocks.py)
+                h = K.image_to_s2d(x.contiguous(), self.stem.conv.pad, scale, None, None, False)
+            else:
+                h = K.nchw_to_nhwc(x.contiguous(), STEM_CIN_PAD, scale, None, None)
         else:  # fp32 parity path (CPU): no bf16 rounding of the input
             h = x.float().permute(0, 2, 3, 1)
             h = torch.nn.functional.pad(h, (0, STEM_CIN_PAD - h.shape[-1])).contiguous()

@@ -45,10 +45,13 @@ def _global_sums(part, count, group):
     return s, count * dist.get_world_size(grp)
 
 
-def _conv_bn_train(x, L, dtype):
-    """conv (+stats) -> finalize.  Returns c, mean, invstd, scale, shift."""
-    w = compute_weight(L.weight, dtype)
-    c, part = K.conv_fwd(x, w, L.stride, L.pad, None, None, False, True)
+def _conv_bn_train(x, L, dtype, w=None, stride=None, pad=None):
+    """conv (+stats) -> finalize.  Returns c, mean, invstd, scale, shift.  (``w``/``stride``/``pad``
+    override the layer's: the space-to-depth stem.)"""
+    if w is None:
+        w = compute_weight(L.weight, dtype)
+    c, part = K.conv_fwd(x, w, L.stride if stride is None else stride, L.pad if pad is None else pad, None, None,
+                         False, True)
     count = c.numel() // c.shape[-1]
     grp = _sync_group(L)
     if grp is not None:   # SyncBN: batch statistics over all ranks
@@ -127,16 +130,67 @@ def _bnr_ok(L):
     return L.stride == 1 or (L.stride == 2 and L.R >= 2 and L.S >= 2)
 
 
-def _wgrad(L, dy, x, grads):
+def _wgrad(L, dy, x, grads, fill=None):
+    """Weight gradient of layer ``L`` (``fill(out, accumulate)`` overrides the plain conv WGRAD)."""
     w = L.weight
+    if fill is None:
+        def fill(out, acc):
+            K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad, acc)
     if dy.is_cuda and w.requires_grad and getattr(w, "main_grad", None) is not None and _params.side_stream_enabled():
         # into the flat gradient buffer on the WGRAD stream, concurrent with this layer's DGRAD
-        _params.run_on_side(lambda: emit_grad(w, lambda out, acc: K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad,
-                                                                                acc)), (dy, x))
+        _params.run_on_side(lambda: emit_grad(w, fill), (dy, x))
         grads[w] = None
         return
-    g = emit_grad(w, lambda out, acc: K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad, acc))
-    grads[w] = g
+    grads[w] = emit_grad(w, fill)
+
+
+# ---- space-to-depth stem --------------------------------------------------------------------------
+# On the GPU the 7x7/2 (pad 3) stem conv runs as a 4x4/1 unpadded conv over the 2x2 space-to-depth
+# image S[n,i,j,(dy*2+dx)*4+c] = X[n,c,2i+dy-3,2j+dx-3] (``K.image_to_s2d``) with the 7x7 filter
+# embedded in an 8x8 one: a 256-deep GEMM reduction (4 full K-tiles) instead of 7*7*8 = 392 (7
+# K-tiles, 5 of every 8 input channels padding), same products, same output.  PCMP_STEM_S2D=0
+# keeps the direct 7x7 conv (A/B runs).
+S2D_CH = 16
+
+
+def stem_s2d_wanted(device) -> bool:
+    import os
+    return device.type == "cuda" and os.environ.get("PCMP_STEM_S2D", "1") != "0"
+
+
+def stem_s2d_enabled(x, L) -> bool:
+    return (x.dtype == torch.bfloat16 and L.R == 7 and L.S == 7 and L.stride == 2 and
+            x.shape[-1] in (8, S2D_CH) and stem_s2d_wanted(x.device))
+
+
+def s2d_weight(w):
+    """[Co,7,7,Cp>=4] stem filter -> [Co,4,4,16] filter of the space-to-depth conv."""
+    co = w.shape[0]
+    w8 = torch.nn.functional.pad(w[..., :4], (0, 0, 0, 1, 0, 1))           # [Co,8,8,4], r = 2r'+dy
+    return w8.reshape(co, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(co, 4, 4, S2D_CH).contiguous()
+
+
+def s2d_weight_grad(g4):
+    """[Co,4,4,16] gradient of the space-to-depth filter -> [Co,7,7,4] gradient of the 7x7 filter."""
+    co = g4.shape[0]
+    return g4.reshape(co, 4, 4, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(co, 8, 8, 4)[:, :7, :7, :]
+
+
+def s2d_input_grad(gs, H, W, pad, cpad):
+    """Gradient w.r.t. the space-to-depth image -> gradient w.r.t. the [N,H,W,cpad] stem input."""
+    N, Hs, Ws, _ = gs.shape
+    g = gs.reshape(N, Hs, Ws, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, 2 * Hs, 2 * Ws, 4)
+    g = g[:, pad:pad + H, pad:pad + W, :]
+    return torch.nn.functional.pad(g, (0, cpad - 4)).contiguous()
+
+
+def _folded_s2d(L, dtype):
+    w, b = _folded(L, dtype)
+    f = getattr(L, "_fold_s2d", None)
+    if f is None or f[0] is not w:
+        f = (w, s2d_weight(w))
+        L._fold_s2d = f
+    return f[1], b
 
 
 class _TailBN:
@@ -321,15 +375,28 @@ class StemFn(torch.autograd.Function):
     def forward(ctx, x, stem, *params):
         L = stem.conv
         dtype = x.dtype
+        s2d = stem_s2d_enabled(x, L)
+        xin = x
+        if s2d and x.shape[-1] != S2D_CH:   # NHWC input padded to 8 channels
+            x = K.image_to_s2d(x, L.pad, 1.0, None, None, True)
         if not stem.training:
-            return K.maxpool_fwd(_conv_bn_eval(x, L, dtype, True), 3, 2, 1, False)[0]
+            if s2d:
+                w4, b = _folded_s2d(L, dtype)
+                c = K.conv_fwd(x, w4, 1, 0, b, None, True, False)[0]
+            else:
+                c = _conv_bn_eval(x, L, dtype, True)
+            return K.maxpool_fwd(c, 3, 2, 1, False)[0]
         _params.WEIGHT_GEN[0] += 1
-        c, mean, invstd, sc, sh = _conv_bn_train(x, L, dtype)
+        if s2d:
+            c, mean, invstd, sc, sh = _conv_bn_train(x, L, dtype, s2d_weight(compute_weight(L.weight, dtype)), 1, 0)
+        else:
+            c, mean, invstd, sc, sh = _conv_bn_train(x, L, dtype)
         # BN + ReLU fused into the pooling prologue: the normalised activation is never stored
         y, idx = K.maxpool_fwd(c, 3, 2, 1, True, sc, sh)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(x)
             ctx.state = (c, sc, sh, idx, mean, invstd)
+            ctx.s2d = (tuple(xin.shape) if xin is not x else None) if s2d else False
             ctx.stem = stem
             ctx.params = params
         else:
@@ -347,11 +414,30 @@ class StemFn(torch.autograd.Function):
         outs, gr = _bn_backward(r[0], None, c, mean, invstd, L, parts=r[1:])
         grads.update(gr)
         dc = outs[0]
-        _wgrad(L, dc, x, grads)
+        if ctx.s2d is False:
+            _wgrad(L, dc, x, grads)
+        else:
+            def fill(out, acc):
+                g4 = torch.empty(out.shape[0], 4, 4, S2D_CH, dtype=torch.float32, device=out.device)
+                K.conv_wgrad(dc, x, g4, 4, 4, 1, 0, False)
+                g = s2d_weight_grad(g4)
+                if acc:
+                    out[..., :4].add_(g)
+                else:
+                    out[..., :4].copy_(g)
+                    out[..., 4:].zero_()
+            _wgrad(L, dc, x, grads, fill)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = K.conv_dgrad(dc, compute_weight(L.weight, dc.dtype), x.shape[1], x.shape[2], L.stride, L.pad, None,
-                              compute_weight_t(L.weight, dc.dtype))
+            if ctx.s2d is False:
+                dx = K.conv_dgrad(dc, compute_weight(L.weight, dc.dtype), x.shape[1], x.shape[2], L.stride, L.pad,
+                                  None, compute_weight_t(L.weight, dc.dtype))
+            else:
+                dx = K.conv_dgrad(dc, s2d_weight(compute_weight(L.weight, dc.dtype)), x.shape[1], x.shape[2], 1, 0,
+                                  None, None)
+                if ctx.s2d is not None:   # input was the 8-channel NHWC image
+                    N, H, W, cp = ctx.s2d
+                    dx = s2d_input_grad(dx, H, W, L.pad, cp)
         ctx.state = None
         return (dx, None) + tuple(grads.get(p) for p in ctx.params)
 

@@ -296,6 +296,23 @@ def nchw_to_nhwc(x, cpad, scale, mean=None, stdv=None):
     return y.to(torch.bfloat16).contiguous()
 
 
+def image_to_s2d(x, pad, scale, mean=None, stdv=None, nhwc=False):
+    """Stem space-to-depth (csrc/elementwise.hip image_to_s2d_kernel):
+    S[n,i,j,(dy*2+dx)*4+c] = X[n,c,2i+dy-pad,2j+dx-pad] (zero outside / c >= Cin)."""
+    if nhwc:
+        h = x.float()[..., :4]
+    else:
+        h = x.float() * scale
+        if mean is not None:
+            h = (h - mean.view(1, -1, 1, 1)) / stdv.view(1, -1, 1, 1)
+        h = h.permute(0, 2, 3, 1)
+    N, H, W, C = h.shape
+    Hs, Ws = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
+    h = F.pad(h, (0, 4 - C, pad, 2 * Ws - W - pad, pad, 2 * Hs - H - pad))
+    h = h.reshape(N, Hs, 2, Ws, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, Hs, Ws, 16)
+    return h.to(torch.bfloat16).contiguous()
+
+
 # ------------------------------------------------------------------------------ optimizers
 def sgd_flat(w, g, mom, shadow, mask, lr, gscale, momentum, dampening, wd, nesterov, first_step):
     gs = gscale.float() if gscale is not None else 1.0

@@ -378,3 +378,19 @@ def test_stem_fused_bn_maxpool(gpu):
     gref, pref = ref.maxpool_bwd_bnr(dy, i1, c, mean, invstd, sc, sh, 3, 2, 1)
     close(g, gref)
     close(part.sum(0), pref.sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("src", ["f32", "u8", "nhwc"])
+def test_image_to_s2d(gpu, src):
+    """Stem space-to-depth kernel == the PyTorch reference (NCHW f32 / u8 with scale, NHWC bf16)."""
+    torch.manual_seed(0)
+    if src == "f32":
+        x, scale, nhwc = torch.rand(3, 3, 37, 30, device=gpu), 1.0, False
+    elif src == "u8":
+        x, scale, nhwc = torch.randint(0, 256, (3, 3, 30, 37), device=gpu, dtype=torch.uint8), 1 / 255, False
+    else:
+        x, scale, nhwc = rnd(3, 31, 36, 8, dev=gpu), 1.0, True
+    y = _ops().image_to_s2d(x, 3, scale, None, None, nhwc)
+    yr = ref.image_to_s2d(x, 3, scale, None, None, nhwc)
+    assert y.shape == yr.shape
+    assert torch.equal(y, yr)

@@ -113,3 +113,34 @@ def test_mask_bits_roundtrip_reference():
     sc, sh = torch.randn(16), torch.randn(16)
     out = ref.bn_apply(x, sc, sh, None, None, None, True, mb)
     assert torch.equal(mb, ref.pack_mask_bits(out))
+
+
+@pytest.mark.parametrize("hw", [20, 21])
+def test_stem_space_to_depth_equivalence(hw):
+    """7x7/2 pad-3 conv == 4x4/1 unpadded conv over the 2x2 space-to-depth image with the filter
+    embedded in 8x8 (the GPU stem); the filter / input gradients map back exactly."""
+    from pcmp.ops.conv_blocks import s2d_input_grad, s2d_weight, s2d_weight_grad
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, hw, hw).bfloat16().float()          # bf16-exact: the s2d image is bf16
+    w = torch.zeros(5, 7, 7, 8)
+    w[..., :3] = torch.randn(5, 7, 7, 3)
+    y7 = torch.nn.functional.conv2d(x, w.permute(0, 3, 1, 2)[:, :3], stride=2, padding=3)
+    xs = ref.image_to_s2d(x, 3, 1.0, None, None, False).float()
+    assert xs.shape == (2, (hw + 7) // 2, (hw + 7) // 2, 16)
+    xs_nhwc = ref.image_to_s2d(torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 5)).bfloat16(), 3, 1.0, None,
+                               None, True).float()
+    assert torch.equal(xs, xs_nhwc)
+    w4 = s2d_weight(w).requires_grad_(True)
+    xs_ = xs.permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    y4 = torch.nn.functional.conv2d(xs_, w4.permute(0, 3, 1, 2))
+    assert y4.shape == y7.shape
+    torch.testing.assert_close(y4, y7, rtol=1e-5, atol=1e-4)
+    # gradients: through the s2d conv, mapped back, equal the direct conv's
+    dy = torch.randn_like(y7)
+    y4.backward(dy)
+    w7 = w.clone().requires_grad_(True)
+    x7 = torch.nn.functional.pad(x.permute(0, 2, 3, 1), (0, 5)).contiguous().requires_grad_(True)
+    torch.nn.functional.conv2d(x7.permute(0, 3, 1, 2), w7.permute(0, 3, 1, 2), stride=2, padding=3).backward(dy)
+    torch.testing.assert_close(s2d_weight_grad(w4.grad), w7.grad[..., :4], rtol=1e-4, atol=1e-3)
+    gx = s2d_input_grad(xs_.grad.permute(0, 2, 3, 1), hw, hw, 3, 8)
+    torch.testing.assert_close(gx[..., :3], x7.grad[..., :3], rtol=1e-4, atol=1e-3)
