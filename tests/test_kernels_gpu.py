@@ -38,6 +38,7 @@ CONV_SHAPES = [
     (2, 14, 14, 128, 128, 3, 2, 1),   # 3x3 stride 2
     (2, 14, 14, 256, 512, 1, 2, 0),   # 1x1 stride-2 downsample
     (3, 7, 7, 512, 512, 3, 1, 1),     # layer4 3x3 (M not a multiple of the tile)
+    (2, 14, 14, 24, 136, 3, 1, 1),    # channel counts off the tile grid (WGRAD gn = 216, gm = 136)
     (1, 7, 7, 512, 2048, 1, 1, 0),    # batch-1 inference: split-K forward
     (1, 14, 14, 256, 256, 3, 1, 1),   # batch-1 inference 3x3: split-K forward
     (5, 1, 1, 2048, 16, 1, 1, 0),     # linear, tiny M, N

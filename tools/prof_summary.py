@@ -14,6 +14,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--steps", type=int, default=0, help="steps profiled (prints ms/step)")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--last", type=float, default=0.5, help="trailing fraction of the trace for the idle-gap count")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True)
     if not files:
@@ -31,6 +32,40 @@ def main():
     if a.steps:
         msg += f" ({tot / 1e6 / a.steps:.2f} ms/step over {a.steps} steps)"
     print(msg)
+    gaps(a.dir, a.last)
+
+
+def gaps(d, last):
+    """GPU idle time between kernels (union of kernel intervals over all queues) in the window of the
+    last ``last`` kernels-per-step... approximated as the trailing 50 % of the trace (timed steps)."""
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        return
+    iv = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                s, e = r.get("Start_Timestamp"), r.get("End_Timestamp")
+                if s and e:
+                    iv.append((int(s), int(e)))
+    if not iv:
+        return
+    iv.sort()
+    iv = iv[int(len(iv) * (1 - last)):]
+    busy, cur_s, cur_e, n_gap, small = 0, iv[0][0], iv[0][1], 0, 0
+    for s, e in iv[1:]:
+        if s > cur_e:
+            busy += cur_e - cur_s
+            n_gap += 1
+            if s - cur_e < 5000:
+                small += s - cur_e
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    span = iv[-1][1] - iv[0][0]
+    print(f"trailing {100 * last:.0f}% of the trace: {len(iv)} kernels, span {span / 1e6:.2f} ms, busy {busy / 1e6:.2f} ms, "
+          f"idle {(span - busy) / 1e6:.2f} ms in {n_gap} gaps ({small / 1e6:.2f} ms in gaps < 5 us)")
 
 
 if __name__ == "__main__":
