@@ -395,3 +395,22 @@ def test_image_to_s2d(gpu, src):
     yr = ref.image_to_s2d(x, 3, scale, None, None, nhwc)
     assert y.shape == yr.shape
     assert torch.equal(y, yr)
+
+
+def test_splitk_fwd_repeated(gpu):
+    """Batch-1 split-K FWD (fp32 partial slabs + reduction/epilogue pass): repeated launches of several
+    shapes with and without bias / residual / ReLU; bitwise reproducible."""
+    torch.manual_seed(0)
+    for rep in range(3):
+        for (H, C, K, R) in [(7, 512, 2048, 1), (14, 256, 256, 3), (7, 2048, 512, 1), (7, 512, 512, 3)]:
+            p = R // 2
+            x = rnd(1, H, H, C, dev=gpu)
+            w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+            bias = torch.randn(K, device=gpu)
+            res = rnd(1, H, H, K, dev=gpu) if rep != 1 else None
+            relu = rep != 2
+            y = _ops().conv_fwd(x, w, 1, p, bias, res, relu, False)[0]
+            yr = ref.conv_fwd(x, w, 1, p, bias, res, relu, False)[0]
+            close(y, yr)
+            # bitwise reproducible (fixed split order)
+            assert torch.equal(y, _ops().conv_fwd(x, w, 1, p, bias, res, relu, False)[0])
