@@ -234,6 +234,14 @@ def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
     return r[0]
 
 
+def _side_branch_ok(t, L) -> bool:
+    """Independent branch of a block on the side stream (GPU; not with SyncBN, whose statistics
+    all-reduce runs on the compute stream).  PCMP_DOWN_STREAM=0 keeps it on the compute stream."""
+    import os
+    return (t.is_cuda and _params.side_stream_enabled() and _sync_group(L) is None and
+            os.environ.get("PCMP_DOWN_STREAM", "1") != "0")
+
+
 class ResidualBlockFn(torch.autograd.Function):
     """out = relu( BN_L(conv_L(...relu(BN_1(conv_1(x)))...)) + shortcut(x) )."""
 
@@ -249,6 +257,11 @@ class ResidualBlockFn(torch.autograd.Function):
             return _conv_bn_eval(h, main[-1], dtype, True, r)
 
         _params.WEIGHT_GEN[0] += 1      # running statistics move in training mode
+        # the downsample conv (+ BN statistics / finalize) is independent of the main branch: it runs
+        # on the side stream, concurrently with conv1..convL
+        dfork = None
+        if down is not None and _side_branch_ok(x, down):
+            dfork = _params.fork_side(lambda: _conv_bn_train(x, down, dtype), (x,))
         acts, cs, stats, coefs = [x], [], [], []
         h = x
         for i, L in enumerate(main):
@@ -265,7 +278,10 @@ class ResidualBlockFn(torch.autograd.Function):
         mbits = (torch.empty(cs[-1].numel() // 8, dtype=torch.uint8, device=x.device)
                  if any(ctx.needs_input_grad) and cs[-1].shape[-1] % 8 == 0 else None)
         if down is not None:
-            cd, meand, invstdd, scd, shd = _conv_bn_train(x, down, dtype)
+            if dfork is not None:
+                cd, meand, invstdd, scd, shd = _params.join_side(*dfork)
+            else:
+                cd, meand, invstdd, scd, shd = _conv_bn_train(x, down, dtype)
             out = K.bn_apply(cs[-1], last[0], last[1], cd, scd, shd, True, mbits)
         else:
             cd = meand = invstdd = None
@@ -321,6 +337,15 @@ class ResidualBlockFn(torch.autograd.Function):
         grads.update(gr)
         need_dx = ctx.needs_input_grad[0]
         dx = None
+        # downsample dgrad (the shortcut's input gradient, added in conv1's dgrad epilogue) on the side
+        # stream, concurrently with the main branch's backward chain
+        prev0 = ctx.prev_tail if (need_dx and _bnr_ok(main[0])) else None
+        tfork = None
+        if down is not None and prev0 is not None and _side_branch_ok(dcd, down):
+            wd = compute_weight(down.weight, dcd.dtype)
+            wdt = compute_weight_t(down.weight, dcd.dtype)
+            tfork = _params.fork_side(lambda: K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt),
+                                      (dcd, wd, wdt))
         for i in range(len(main) - 1, -1, -1):
             L = main[i]
             _wgrad(L, dh, acts[i], grads)
@@ -349,7 +374,10 @@ class ResidualBlockFn(torch.autograd.Function):
                         wd = compute_weight(down.weight, dh.dtype)
                         wdt = compute_weight_t(down.weight, dh.dtype)
                         if prev is not None:
-                            t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt)
+                            if tfork is not None:
+                                t = _params.join_side(*tfork)
+                            else:
+                                t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt)
                             dx = _dgrad_into_prev(dh, wcomp, H, W, L, t, x, prev)
                         else:
                             t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None, wt)

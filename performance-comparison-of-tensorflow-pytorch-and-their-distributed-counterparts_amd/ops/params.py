@@ -122,6 +122,37 @@ def _join(main, side, key):
     _JOIN_QUEUED[0] = False
 
 
+def fork_side(fn: Callable[[], object], keep_alive):
+    """Run ``fn`` on the device's side stream, ordered after the compute stream's work so far, and
+    return ``(result, event)``: the compute stream must ``wait_event(event)`` (``join_side``) before
+    it consumes the result.  For independent branches inside one autograd node (a residual block's
+    downsample conv next to its main branch)."""
+    dev = keep_alive[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev.index)
+    if side is None:
+        side = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in keep_alive:
+        if t is not None:
+            t.record_stream(side)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    return out, ev
+
+
+def join_side(result, ev):
+    """Make the compute stream wait for a ``fork_side`` result and register its tensors with it."""
+    ts = [t for t in (result if isinstance(result, (tuple, list)) else (result,)) if isinstance(t, torch.Tensor)]
+    main = torch.cuda.current_stream(ts[0].device)
+    main.wait_event(ev)
+    for t in ts:
+        t.record_stream(main)
+    return result
+
+
 def run_on_side(fn: Callable[[], None], keep_alive) -> None:
     """Run ``fn`` (kernel launches) on the device's WGRAD stream, ordered after the compute stream's
     work so far; ``keep_alive`` tensors are recorded on the side stream for the caching allocator."""
