@@ -223,6 +223,20 @@ __device__ __forceinline__ bf16x8 frag_row(const __bf16* X, int ld, int row, int
   return *reinterpret_cast<const bf16x8*>(X + row * ld + k0);
 }
 
+// bf16 fragment of X^T for an LDS tile stored row-major X[k][m] (ld elements per row): M/N index
+// mbase + (lane & 15), reduction indices k0 + 8*(lane >> 4) .. +7 (k0 a multiple of 32), read with
+// two ds_read_b64_tr_b16 (each lane addresses 4 consecutive m of one k row; the 16-lane groups
+// transpose) -- no transposed copy of the tile and no per-element LDS gathers.
+__device__ __forceinline__ bf16x8 frag_tr(const __bf16* X, int ld, int k0, int mbase) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+  const int lane = threadIdx.x & 63;
+  const int row = k0 + 8 * (lane >> 4) + ((lane >> 2) & 3), col = mbase + (lane & 3) * 4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(X + row * ld + col));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(X + (row + 4) * ld + col));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 __device__ __forceinline__ float drop_scale(const AttnParams& p, int bh, int q, int k) {
   if (p.p_drop <= 0.f) return 1.f;
   const uint64_t idx = ((uint64_t)bh * p.S + q) * p.S + k;
@@ -352,21 +366,20 @@ __global__ void __launch_bounds__(256) attention_bwd_kernel(const AttnParams p) 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const int S = p.S, D3 = 3 * p.D;
+  // Q, K, V, dO row-major; their transposed operands are read with frag_tr
   __bf16* sQ = reinterpret_cast<__bf16*>(smem);   // [S][ADP]
-  __bf16* sQt = sQ + AS * ADP;                     // [AD][ASP]
-  __bf16* sK = sQt + AD * ASP;                     // [S][ADP]
+  __bf16* sK = sQ + AS * ADP;                      // [S][ADP]
   __bf16* sV = sK + AS * ADP;                      // [S][ADP]
   __bf16* sdO = sV + AS * ADP;                     // [S][ADP]
-  __bf16* sdOt = sdO + AS * ADP;                   // [AD][ASP]
-  __bf16* sT = sdOt + AD * ASP;                    // [S keys][ASP] : Pd^T then dS^T tiles (wave w: keys 32w..)
+  __bf16* sT = sdO + AS * ADP;                     // [S keys][ASP] : Pd^T then dS^T tiles (wave w: keys 32w..)
   float* sL = reinterpret_cast<float*>(sT + AS * ASP);  // lse [S]
   float* sDd = sL + AS;                                  // D [S]
   float* sMask = sDd + AS;                               // [S]
   const __bf16* base = p.qkv + (size_t)b * S * D3 + h * AD;
-  stage_head(base, D3, S, sQ, sQt);
+  stage_head(base, D3, S, sQ, nullptr);
   stage_head(base + p.D, D3, S, sK, nullptr);
   stage_head(base + 2 * p.D, D3, S, sV, nullptr);
-  stage_head(p.dout + (size_t)b * S * p.D + h * AD, p.D, S, sdO, sdOt);
+  stage_head(p.dout + (size_t)b * S * p.D + h * AD, p.D, S, sdO, nullptr);
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
     sL[s] = p.lse[(size_t)bh * S + s];
     sMask[s] = (p.ids && p.ids[(size_t)b * S + s] <= 0) ? -1e30f : 0.f;
@@ -446,7 +459,7 @@ __global__ void __launch_bounds__(256) attention_bwd_kernel(const AttnParams p) 
       const bf16x8 a0 = frag_row(T, ASP, lane & 15, k0), a1 = frag_row(T, ASP, 16 + (lane & 15), k0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bf16x8 bb = frag_row(sdOt, ASP, j * 16 + (lane & 15), k0);
+        const bf16x8 bb = frag_tr(sdO, ADP, kk, j * 16);
         dv[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb, dv[0][j], 0, 0, 0);
         dv[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb, dv[1][j], 0, 0, 0);
       }
@@ -473,7 +486,7 @@ __global__ void __launch_bounds__(256) attention_bwd_kernel(const AttnParams p) 
       const bf16x8 a0 = frag_row(T, ASP, lane & 15, k0), a1 = frag_row(T, ASP, 16 + (lane & 15), k0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bf16x8 bb = frag_row(sQt, ASP, j * 16 + (lane & 15), k0);
+        const bf16x8 bb = frag_tr(sQ, ADP, kk, j * 16);
         dk[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb, dk[0][j], 0, 0, 0);
         dk[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb, dk[1][j], 0, 0, 0);
       }
@@ -501,17 +514,10 @@ __global__ void __launch_bounds__(256) attention_bwd_kernel(const AttnParams p) 
 #pragma unroll
       for (int j = 0; j < 4; ++j) dq[i][j] = f32x4{0, 0, 0, 0};
     for (int kk = 0; kk < S; kk += 32) {
-      const int k0 = kk + 8 * (lane >> 4);
-      bf16x8 a0, a1, bb[4];
+      const bf16x8 a0 = frag_tr(sT, ASP, kk, q0), a1 = frag_tr(sT, ASP, kk, q0 + 16);
+      bf16x8 bb[4];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        a0[t] = sT[(k0 + t) * ASP + q0 + (lane & 15)];
-        a1[t] = sT[(k0 + t) * ASP + q0 + 16 + (lane & 15)];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) bb[j][t] = sK[(k0 + t) * ADP + j * 16 + (lane & 15)];
+      for (int j = 0; j < 4; ++j) bb[j] = frag_tr(sK, ADP, kk, j * 16);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         dq[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb[j], dq[0][j], 0, 0, 0);
@@ -618,7 +624,7 @@ at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b) {
 }
 
 static size_t attn_fwd_smem() { return ((size_t)2 * AS * ADP + AD * ASP + 4 * 32 * ASP) * 2 + AS * 4; }
-static size_t attn_bwd_smem() { return ((size_t)4 * AS * ADP + 2 * AD * ASP + AS * ASP) * 2 + 3 * AS * 4; }
+static size_t attn_bwd_smem() { return ((size_t)4 * AS * ADP + AS * ASP) * 2 + 3 * AS * 4; }
 
 // qkv [B*S][3D] bf16 -> [ctx [B*S][D] bf16, lse [B*H][S] f32]
 std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& ids, int64_t B,

@@ -88,7 +88,7 @@ def test_layernorm_act(gpu):
     close(ops().tanh_bwd(z, t), ref.tanh_bwd(z, t))
 
 
-@pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (64, 0.1)])
+@pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (64, 0.1), (96, 0.0), (32, 0.1)])
 def test_attention(gpu, S, p):
     torch.manual_seed(1)
     B, H, D = 3, 12, 768
