@@ -260,7 +260,7 @@ class ResidualBlockFn(torch.autograd.Function):
         # the downsample conv (+ BN statistics / finalize) is independent of the main branch: it runs
         # on the side stream, concurrently with conv1..convL
         dfork = None
-        if down is not None and _side_branch_ok(x, down):
+        if down is not None and any(ctx.needs_input_grad) and _side_branch_ok(x, down):
             dfork = _params.fork_side(lambda: _conv_bn_train(x, down, dtype), (x,))
         acts, cs, stats, coefs = [x], [], [], []
         h = x
