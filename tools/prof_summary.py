@@ -47,25 +47,37 @@ def gaps(d, last):
             for r in csv.DictReader(fh):
                 s, e = r.get("Start_Timestamp"), r.get("End_Timestamp")
                 if s and e:
-                    iv.append((int(s), int(e)))
+                    iv.append((int(s), int(e), r.get("Kernel_Name", "?")))
     if not iv:
         return
     iv.sort()
     iv = iv[int(len(iv) * (1 - last)):]
     busy, cur_s, cur_e, n_gap, small = 0, iv[0][0], iv[0][1], 0, 0
-    for s, e in iv[1:]:
+    cur_name, by_pair = iv[0][2], {}
+    for s, e, name in iv[1:]:
         if s > cur_e:
             busy += cur_e - cur_s
             n_gap += 1
             if s - cur_e < 5000:
                 small += s - cur_e
-            cur_s, cur_e = s, e
-        else:
-            cur_e = max(cur_e, e)
+            key = (_short(cur_name), _short(name))
+            t, c = by_pair.get(key, (0, 0))
+            by_pair[key] = (t + s - cur_e, c + 1)
+            cur_s, cur_e, cur_name = s, e, name
+        elif e > cur_e:
+            cur_e, cur_name = e, name
     busy += cur_e - cur_s
-    span = iv[-1][1] - iv[0][0]
+    span = max(x[1] for x in iv) - iv[0][0]
     print(f"trailing {100 * last:.0f}% of the trace: {len(iv)} kernels, span {span / 1e6:.2f} ms, busy {busy / 1e6:.2f} ms, "
           f"idle {(span - busy) / 1e6:.2f} ms in {n_gap} gaps ({small / 1e6:.2f} ms in gaps < 5 us)")
+    print("largest idle totals by (kernel that ended last -> next kernel):")
+    for (a, b), (t, c) in sorted(by_pair.items(), key=lambda kv: -kv[1][0])[:15]:
+        print(f"  {t / 1e6:7.3f} ms  n={c:4d} avg={t / c / 1e3:7.1f} us  {a} -> {b}")
+
+
+def _short(name):
+    n = name.split("(")[0].replace("void ", "")
+    return n[:60]
 
 
 if __name__ == "__main__":
