@@ -14,7 +14,9 @@ synchronised data parallelism the north star asks for:
 * buckets are launched strictly in index order on every rank (collective order must match);
 * bucket sizing for 7 point-to-point xGMI links per MI355X: a small first bucket (default 4 MB)
   so communication starts early in backward, then 32 MB buckets so each of RCCL's per-link
-  channel chunks stays >= ~256 KB at world 8 (SURVEY §5.8);
+  channel chunks stays >= ~256 KB at world 8, and a small LAST bucket (default
+  4 MB): the last bucket's all-reduce cannot overlap anything (it waits for the stem's gradient,
+  the end of backward), so only a few MB stay exposed instead of up to a whole 32 MB bucket;
 * the 1/world averaging is folded into the optimizer kernel's gradient scale (no extra pass);
 * initial parameters and buffers are broadcast from rank 0 (DDP constructor semantics).
 """
@@ -38,8 +40,25 @@ class _Bucket:
         self.launched = False
 
 
-def plan_buckets(sizes, first_bucket_elems, bucket_elems):
-    """Greedy contiguous bucketing of consecutive slices -> list of [i0, i1) param index ranges."""
+def plan_buckets(sizes, first_bucket_elems, bucket_elems, last_bucket_elems=0):
+    """Greedy contiguous bucketing of consecutive slices -> list of [i0, i1) param index ranges.
+    With ``last_bucket_elems`` the trailing slices (the last gradients backward produces) are split
+    off first into a tail bucket of about that size."""
+    tail = None
+    if last_bucket_elems > 0 and len(sizes) > 1:
+        acc, j = 0, len(sizes)
+        while j > 1 and acc < last_bucket_elems:
+            j -= 1
+            acc += sizes[j]
+        if acc < sum(sizes):
+            tail, sizes = (j, len(sizes)), sizes[:j]
+    out = _plan_greedy(sizes, first_bucket_elems, bucket_elems)
+    if tail is not None:
+        out.append(tail)
+    return out
+
+
+def _plan_greedy(sizes, first_bucket_elems, bucket_elems):
     out, i0, acc = [], 0, 0
     cap = first_bucket_elems
     for i, n in enumerate(sizes):
@@ -54,7 +73,8 @@ def plan_buckets(sizes, first_bucket_elems, bucket_elems):
 
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, flat: FlatParams, process_group=None, bucket_cap_mb: float = 32.0,
-                 first_bucket_mb: float = 4.0, broadcast_buffers: bool = True, average: bool = True):
+                 first_bucket_mb: float = 4.0, broadcast_buffers: bool = True, average: bool = True,
+                 last_bucket_mb: float = 4.0):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -67,7 +87,8 @@ class DistributedDataParallel(torch.nn.Module):
         offs = flat.offsets + [flat.numel]
         for i in range(len(flat.params)):
             sizes.append(offs[i + 1] - offs[i])
-        ranges = plan_buckets(sizes, int(first_bucket_mb * 2 ** 20 / esz), int(bucket_cap_mb * 2 ** 20 / esz))
+        ranges = plan_buckets(sizes, int(first_bucket_mb * 2 ** 20 / esz), int(bucket_cap_mb * 2 ** 20 / esz),
+                              int(last_bucket_mb * 2 ** 20 / esz))
         self.buckets = []
         self._bucket_of = {}
         for bi, (i0, i1) in enumerate(ranges):

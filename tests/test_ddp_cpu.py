@@ -40,3 +40,14 @@ def test_plan_buckets_small_first_bucket():
     assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
     assert b[-1][1] == 100
     assert sum(e - s for s, e in b) == 100
+
+
+def test_plan_buckets_small_last_bucket():
+    sizes = [10] * 100
+    b = plan_buckets(sizes, 25, 200, 35)
+    assert b[0] == (0, 3)
+    assert b[-1] == (96, 100)                  # tail bucket closes at >= 35 elements from the end
+    assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    assert sum(e - s for s, e in b) == 100
+    assert plan_buckets([5], 25, 200, 35) == [(0, 1)]
+    assert plan_buckets([10, 10], 25, 200, 100) == [(0, 1), (1, 2)]   # the tail never takes slice 0
