@@ -45,8 +45,34 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here")
     ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over all ranks (SyncBN)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the whole training step (forward, backward, optimizer) as one hipGraph "
+                         "after warm-up and replay it (hip impl, one rank)")
     ap.add_argument("--local_rank", "--local-rank", type=int, default=None)
     return ap.parse_args()
+
+
+def graph_step(step, x, y):
+    """Capture one full training step into a hipGraph (static x / y / parameters / optimizer state)
+    and return a replay function.  Autotuning is finished by then (warm-up) and never runs while a
+    graph is captured; the WGRAD / downsample side stream joins the capture through events."""
+    main = torch.cuda.current_stream()
+    s = torch.cuda.Stream()
+    s.wait_stream(main)
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step(x, y)
+    main.wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        loss = step(x, y)
+
+    def replay(x_, y_):
+        assert x_ is x and y_ is y, "graph replay needs the captured input tensors"
+        g.replay()
+        return loss
+
+    return replay
 
 
 def build_hip(args, env):
@@ -132,6 +158,10 @@ def main():
 
     for i in range(args.warmup):
         loss = step(x, y)
+    graphed = bool(args.graph and args.impl == "hip" and env.world_size == 1 and env.device.type == "cuda")
+    if graphed:
+        step = graph_step(step, x, y)
+        loss = step(x, y)
     sync()
     prof = None
     if args.profile and env.is_main:
@@ -170,7 +200,8 @@ def main():
             "config": {"model": args.model, "global_batch": B * env.world_size, "per_gpu_batch": B,
                        "image_size": args.image_size, "num_classes": args.num_classes,
                        "seq_len": None, "parallelism": f"dp{env.world_size}", "impl": args.impl,
-                       "optimizer": "sgd_momentum", "final_loss": round(final_loss, 4)},
+                       "optimizer": "sgd_momentum", "final_loss": round(final_loss, 4),
+                       "hipgraph": graphed},
         }
         print(json.dumps(rec), flush=True)
     launch.shutdown()

@@ -1621,8 +1621,6 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   if (fixed_target) return nsplit_for(fixed_target);
   const int dflt = nsplit_for(1024);
   if (!tune) return dflt;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
   static std::mutex mu;
   static std::unordered_map<std::string, int> cache;
   char key[160];
@@ -1630,8 +1628,10 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
+    if (it != cache.end()) return it->second;   // a graph captured after warm-up keeps the tuned split
   }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
   std::vector<int> cands;
   for (int t : {64, 128, 256, 512, 768, 1024, 1536, 2048}) {
     const int ns = nsplit_for(t);
