@@ -183,6 +183,12 @@ def main():
     ms = dt / args.steps * 1e3
     img_s = B * env.world_size * args.steps / dt
     final_loss = float(loss.float().item())
+    if os.environ.get("PCMP_MEMSTATS") == "1" and env.device.type == "cuda" and env.is_main:
+        ms_ = torch.cuda.memory_stats(env.device)
+        print(f"[bench] mem peak {ms_.get('allocated_bytes.all.peak', 0) / 2**30:.1f} GiB reserved "
+              f"{ms_.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB alloc_retries "
+              f"{ms_.get('num_alloc_retries', 0)} device_allocs {ms_.get('num_device_alloc', 0)} "
+              f"device_frees {ms_.get('num_device_free', 0)}", file=sys.stderr, flush=True)
     if env.is_main:
         rec = {
             "metric": "resnet50_train_images_per_sec" if args.model == "resnet50" else f"{args.model}_train_images_per_sec",
