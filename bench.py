@@ -82,6 +82,7 @@ def build_hip(args, env):
     from pcmp.ops import cross_entropy
     from pcmp.parallel.ddp import DistributedDataParallel
     from pcmp.utils.flat import FlatParams
+    from pcmp.utils.misc import StepThrottle
 
     torch.manual_seed(1234)
     model = getattr(resnet, args.model)(num_classes=args.num_classes).to(env.device).train()
@@ -94,6 +95,10 @@ def build_hip(args, env):
     if ddp is not None:
         opt.set_grad_scale(ddp.grad_scale())
 
+    # host run-ahead bound (PCMP_MAX_INFLIGHT steps): keeps the caching allocator's footprint at a
+    # few steps' worth instead of growing with every step the host gets ahead of the GPU
+    throttle = StepThrottle(env.device)
+
     def step(x, y):
         opt.zero_grad()
         logits = model.forward_logits(x)
@@ -102,6 +107,7 @@ def build_hip(args, env):
         if ddp is not None:
             ddp.finish_gradient_sync()
         opt.step()
+        throttle.tick()
         return loss
 
     return step

@@ -34,7 +34,7 @@ from ..parallel.metrics import all_reduce_max, all_reduce_sum
 from ..utils import report as R
 from ..utils.checkpoint import BestCheckpoint
 from ..utils.flat import FlatParams
-from ..utils.misc import roctx_range
+from ..utils.misc import StepThrottle, roctx_range
 from ..utils.timer import PhaseTimer
 
 
@@ -48,6 +48,7 @@ class TrainState:
     clip: float | None = None
     history: dict = field(default_factory=lambda: {"train_loss": [], "test_loss": [], "test_acc": []})
     timer: PhaseTimer | None = None   # per-phase device time, PCMP_PHASE_TIMES=1
+    throttle: StepThrottle | None = None   # host run-ahead bound (allocator footprint)
 
     def phase(self, name):
         """Phase bracket: HIP-event device time + a roctx range for rocprofv3 (when timing)."""
@@ -78,6 +79,8 @@ class TrainState:
                 self.sched.step()
         if self.timer is not None:
             self.timer.step()
+        if self.throttle is not None:
+            self.throttle.tick()
 
     def phase_report(self, printer=None):
         """Summarise the per-phase device times into ``history['phases']`` (and print one line)."""
@@ -102,7 +105,7 @@ def make_state(model, optimizer="sgd", lr=0.1, distributed=False, clip=None, sha
     ddp = DistributedDataParallel(model, flat) if distributed else None
     timer = PhaseTimer(warmup_steps=int(os.environ.get("PCMP_PHASE_WARMUP", "2"))) \
         if os.environ.get("PCMP_PHASE_TIMES") == "1" else None
-    return TrainState(model, flat, opt, ddp, clip=clip, timer=timer)
+    return TrainState(model, flat, opt, ddp, clip=clip, timer=timer, throttle=StepThrottle(dev))
 
 
 def _logits(model, x):

@@ -91,3 +91,39 @@ class Watchdog:
                 if self.abort:
                     os._exit(3)
                 self.last = time.monotonic()
+
+
+class StepThrottle:
+    """Bounds how many training steps the host may enqueue ahead of the GPU.
+
+    Nothing in a pcmp step synchronises the host (losses stay on device), so the host, which needs
+    8-15 ms to enqueue a ResNet-50 step that takes the GPU 22 ms, runs further and further ahead.
+    Every tensor freed on the host while its kernels are still queued (and every ``record_stream``
+    on the WGRAD side stream) keeps its block out of the caching allocator until the GPU catches
+    up, so the allocator keeps reserving fresh segments: 83 GiB reserved for a 10.7 GiB peak at
+    B=256, 221 GiB at B=1024 (``profiles/r1_alloc_ab.txt``), a few steps away from the 288 GB of
+    HBM.  ``tick()`` after each step records an event on the current stream and, once more than
+    ``depth`` steps are in flight, waits for the oldest; with depth 2 the GPU still always has a
+    whole step queued.  ``PCMP_MAX_INFLIGHT`` overrides the depth (0 disables).  No-op on CPU."""
+
+    def __init__(self, device=None, depth: int | None = None):
+        if depth is None:
+            depth = int(os.environ.get("PCMP_MAX_INFLIGHT", "2"))
+        self.depth = depth
+        self.device = torch.device(device) if device is not None else None
+        self._events = []
+
+    def tick(self) -> None:
+        if self.depth <= 0 or self.device is None or self.device.type != "cuda":
+            return
+        if torch.cuda.is_current_stream_capturing():
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._events.append(ev)
+        while len(self._events) > self.depth:
+            self._events.pop(0).synchronize()
+
+    @property
+    def in_flight(self) -> int:
+        return len(self._events)

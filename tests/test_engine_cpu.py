@@ -160,3 +160,13 @@ def test_phase_timer_wiring(monkeypatch):
     for k in ("data", "forward", "backward", "optimizer"):
         assert k in ph and ph[k]["host_s_total"] >= 0.0
     assert any(l.startswith("[phase times") for l in lines)
+
+
+def test_step_throttle_noop_on_cpu(monkeypatch):
+    from pcmp.utils.misc import StepThrottle
+    t = StepThrottle("cpu", depth=2)
+    for _ in range(5):
+        t.tick()
+    assert t.in_flight == 0
+    monkeypatch.setenv("PCMP_MAX_INFLIGHT", "0")
+    assert StepThrottle("cpu").depth == 0

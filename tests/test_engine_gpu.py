@@ -52,3 +52,17 @@ def test_graph_predictor_matches_eager(gpu):
     with torch.no_grad():
         for i in range(3):
             assert p(x[i:i + 1]) == int(m.forward_logits(x[i:i + 1].to(gpu)).argmax(1))
+
+
+def test_step_throttle_bounds_inflight(gpu):
+    from pcmp.utils.misc import StepThrottle
+    dev = torch.device("cuda", 0)
+    t = StepThrottle(dev, depth=2)
+    a = torch.randn(2048, 2048, device=dev)
+    for _ in range(6):
+        for _ in range(4):
+            a = (a @ a).clamp_(-1, 1)
+        t.tick()
+        assert t.in_flight <= 2
+    torch.cuda.synchronize()
+    assert t.in_flight == 2 and torch.isfinite(a).all()
