@@ -170,3 +170,15 @@ def test_step_throttle_noop_on_cpu(monkeypatch):
     assert t.in_flight == 0
     monkeypatch.setenv("PCMP_MAX_INFLIGHT", "0")
     assert StepThrottle("cpu").depth == 0
+
+
+def test_train_state_has_throttle():
+    from pcmp.engine.trainer import make_state
+    from pcmp.utils.misc import StepThrottle
+    m = torch.nn.Linear(4, 2)
+    st = make_state(m, "sgd", lr=0.1)
+    assert isinstance(st.throttle, StepThrottle)
+    loss = m(torch.randn(3, 4)).square().mean()
+    st.zero_grad()
+    st.backward_step(loss)
+    assert st.throttle.in_flight == 0      # CPU: no events
