@@ -1353,8 +1353,11 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   const int tiles = ceil_div(p.gm, BMsel) * ceil_div(p.gn, BNsel);
   const int ksteps = ceil_div(p.gk, BK);
   int nsplit = 1;
+  // PCMP_FWD_SPLIT_TARGET / PCMP_FWD_SPLIT_MINK: grid target and minimum K-steps per split (A/B knobs)
+  static const int split_target = [] { const char* e = getenv("PCMP_FWD_SPLIT_TARGET"); return e ? atoi(e) : 256; }();
+  static const int split_mink = [] { const char* e = getenv("PCMP_FWD_SPLIT_MINK"); return e ? std::max(1, atoi(e)) : 4; }();
   if (!want_stats && tiles < 128 && ksteps >= 8)
-    nsplit = std::max(1, std::min({ceil_div(256, tiles), ksteps / 4, 32}));
+    nsplit = std::max(1, std::min({ceil_div(split_target, tiles), ksteps / split_mink, 32}));
   if (nsplit > 1) {
     const int steps_per = ceil_div(ksteps, nsplit);
     nsplit = ceil_div(ksteps, steps_per);
