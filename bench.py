@@ -15,6 +15,21 @@ flat SGD-momentum update of all 25.6 M params (+ bf16 shadow refresh).
 
 ``--impl torch`` runs the self-baseline: the same model on stock PyTorch-ROCm (MIOpen convs,
 channels_last, bf16 autocast, torch DDP, torch fused SGD).
+
+After the timed region (outside it) every rank also measures ResNet-50 batch-1 inference latency
+on the trained model (eval mode, BN folded, whole forward replayed from one hipGraph, per image:
+H2D copy of a host image + replay + argmax + D2H index, the reference's predict_image contract,
+SURVEY E1) and rank 0 reports ``inference_p50_ms`` / ``inference_p99_ms`` — the second half of
+BASELINE.json's metric.  ``--infer-images 0`` skips it.
+
+``--ddp-force`` initialises the ``nccl`` (RCCL) process group and issues every gradient bucket's
+all-reduce even at one rank, so the multi-GPU communication path runs on a one-GPU box;
+``--grad-dtype bf16`` all-reduces bf16 gradient copies (half the xGMI bytes).
+
+``vs_baseline`` is null: the reference publishes no full-network training number (its only
+training figure, BASELINE.md P1a = 1.43 img/s, is frozen-backbone transfer learning on a CPU
+Colab runtime), so no like-for-like ratio exists.  ``vs_stock_pytorch`` compares against the
+stock PyTorch-ROCm self-baseline of the same step on the same GPU (BASELINE.md, 6,540 img/s).
 """
 from __future__ import annotations
 
@@ -24,12 +39,16 @@ import os
 import sys
 import time
 
+# before the HIP runtime initialises: one hardware queue per stream (compute, WGRAD side, DDP comm,
+# RCCL) instead of HIP's default 4 shared round-robin (see pcmp/__init__.py)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import torch
 import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-BASELINE_IMG_PER_SEC = 1.43  # ResNet-50 TL training throughput (7,576 img / 5314.1 s)
+STOCK_TORCH_IMG_PER_SEC = {"resnet50": 6540.0, "resnet18": 16850.0}  # BASELINE.md self-baseline, 1 GPU, B=256
 
 
 def parse():
@@ -48,6 +67,12 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="capture the whole training step (forward, backward, optimizer) as one hipGraph "
                          "after warm-up and replay it (hip impl, one rank)")
+    ap.add_argument("--ddp-force", action="store_true",
+                    help="RCCL process group + bucket all-reduces even at one rank (exercises the comm path)")
+    ap.add_argument("--grad-dtype", default=None, choices=["fp32", "bf16"],
+                    help="gradient all-reduce dtype (default fp32, exact)")
+    ap.add_argument("--infer-images", type=int, default=200,
+                    help="batch-1 inference latency images measured after the timed loop (0 = skip)")
     ap.add_argument("--local_rank", "--local-rank", type=int, default=None)
     return ap.parse_args()
 
@@ -91,7 +116,8 @@ def build_hip(args, env):
         convert_sync_batchnorm(model)
     flat = FlatParams(model.parameters())
     opt = SGD(flat, lr=args.lr, momentum=0.9, weight_decay=5e-5)
-    ddp = DistributedDataParallel(model, flat) if env.world_size > 1 else None
+    use_ddp = env.world_size > 1 or (args.ddp_force and env.backend is not None)
+    ddp = DistributedDataParallel(model, flat, force=args.ddp_force, grad_dtype=args.grad_dtype) if use_ddp else None
     if ddp is not None:
         opt.set_grad_scale(ddp.grad_scale())
 
@@ -110,6 +136,7 @@ def build_hip(args, env):
         throttle.tick()
         return loss
 
+    step.model = model
     return step
 
 
@@ -138,12 +165,32 @@ def build_torch(args, env):
     return step
 
 
+def batch1_latency(model, args, env):
+    """Per-image batch-1 latency of the trained model (outside the timed training region)."""
+    from pcmp.engine.inference import Batch1Predictor
+    from pcmp.utils.report import latency_stats
+
+    n = args.infer_images
+    imgs = torch.rand(n, 3, args.image_size, args.image_size, generator=torch.Generator().manual_seed(5))
+    torch.cuda.synchronize()
+    pred = Batch1Predictor(model, imgs[:1].to(env.device), use_graph=True)
+    for i in range(min(20, n)):
+        pred(imgs[i:i + 1])
+    lat = []
+    for i in range(n):
+        ts = time.perf_counter()
+        pred(imgs[i:i + 1])
+        lat.append(time.perf_counter() - ts)
+    model.train()
+    return latency_stats(lat)
+
+
 def main():
     args = parse()
     import pcmp
     from pcmp.parallel import launch
 
-    env = launch.init(args.local_rank)
+    env = launch.init(args.local_rank, force_init=args.ddp_force)
     if env.world_size != args.gpus and env.is_main:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     if env.device.type == "cuda":
@@ -154,6 +201,7 @@ def main():
     y = torch.randint(0, args.num_classes, (B,), device=env.device, generator=g)
 
     step = build_hip(args, env) if args.impl == "hip" else build_torch(args, env)
+    hip_model = getattr(step, "model", None)
 
     def sync():
         if env.device.type == "cuda":
@@ -186,6 +234,9 @@ def main():
     if env.world_size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    infer = None
+    if args.infer_images > 0 and hip_model is not None and env.device.type == "cuda":
+        infer = batch1_latency(hip_model, args, env)
     ms = dt / args.steps * 1e3
     img_s = B * env.world_size * args.steps / dt
     final_loss = float(loss.float().item())
@@ -206,15 +257,24 @@ def main():
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(img_s / BASELINE_IMG_PER_SEC, 1),
+            "vs_baseline": None,
+            "vs_stock_pytorch": (round(img_s / env.world_size / STOCK_TORCH_IMG_PER_SEC[args.model], 3)
+                                 if args.model in STOCK_TORCH_IMG_PER_SEC and B == 256 else None),
             "dtype": "bf16",
             "data": "synthetic",
             "config": {"model": args.model, "global_batch": B * env.world_size, "per_gpu_batch": B,
                        "image_size": args.image_size, "num_classes": args.num_classes,
                        "seq_len": None, "parallelism": f"dp{env.world_size}", "impl": args.impl,
                        "optimizer": "sgd_momentum", "final_loss": round(final_loss, 4),
-                       "hipgraph": graphed},
+                       "hipgraph": graphed, "ddp_force": bool(args.ddp_force),
+                       "grad_allreduce_dtype": args.grad_dtype or "fp32"},
         }
+        if infer is not None:
+            rec["inference_p50_ms"] = round(infer["p50_ms"], 4)
+            rec["inference_p99_ms"] = round(infer["p99_ms"], 4)
+            rec["inference_config"] = {"model": args.model, "batch": 1, "image_size": args.image_size,
+                                       "images": infer["n"], "hipgraph": True, "bn_folded": True,
+                                       "per_image": "h2d copy + graph replay + argmax + d2h index"}
         print(json.dumps(rec), flush=True)
     launch.shutdown()
 

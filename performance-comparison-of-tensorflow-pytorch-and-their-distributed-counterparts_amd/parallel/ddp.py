@@ -19,10 +19,26 @@ synchronised data parallelism the north star asks for:
   the end of backward), so only a few MB stay exposed instead of up to a whole 32 MB bucket;
 * the 1/world averaging is folded into the optimizer kernel's gradient scale (no extra pass);
 * initial parameters and buffers are broadcast from rank 0 (DDP constructor semantics).
+
+Stream ordering (MI355X: compute stream + WGRAD side stream + RCCL's internal stream):
+
+* every gradient-ready hook notes the HIP stream that wrote the gradient (the conv WGRADs run on
+  the side stream, BN gamma/beta and Linear grads on the compute stream);
+* when a bucket completes, an event is recorded on each stream that contributed to it and a
+  dedicated COMM stream waits on exactly those events; the collective is issued with the comm
+  stream current, so RCCL's stream orders after the comm stream only.  The compute stream never
+  waits for the WGRAD stream (or for communication) before the end of backward;
+* ``finish_gradient_sync`` makes the comm stream wait for every collective and the compute
+  stream wait for the comm stream once, right before the optimizer;
+* ``grad_dtype=torch.bfloat16`` all-reduces a bf16 copy of each bucket (cast on the comm stream,
+  half the xGMI bytes) and casts the sum back into the fp32 gradient; fp32 (default) is exact;
+* ``force=True`` (``PCMP_DDP_FORCE=1``) issues every bucket's collective even at world size 1,
+  so the RCCL path (process group, comm stream, events, casts) runs on a one-GPU box.
 """
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.distributed as dist
@@ -31,13 +47,15 @@ from ..utils.flat import FlatParams
 
 
 class _Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched")
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched", "streams", "events")
 
     def __init__(self, index, start, end, params):
         self.index, self.start, self.end, self.params = index, start, end, params
         self.pending = len(params)
         self.work = None
         self.launched = False
+        self.streams = {}       # stream id -> stream that wrote a gradient of this bucket this step
+        self.events = {}        # stream id -> reusable event (recorded when the bucket launches)
 
 
 def plan_buckets(sizes, first_bucket_elems, bucket_elems, last_bucket_elems=0):
@@ -74,7 +92,7 @@ def _plan_greedy(sizes, first_bucket_elems, bucket_elems):
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, flat: FlatParams, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 4.0, broadcast_buffers: bool = True, average: bool = True,
-                 last_bucket_mb: float = 4.0):
+                 last_bucket_mb: float = 4.0, force: bool | None = None, grad_dtype: torch.dtype | str | None = None):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -82,6 +100,22 @@ class DistributedDataParallel(torch.nn.Module):
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.average = average
         self.require_sync = True
+        if force is None:
+            force = os.environ.get("PCMP_DDP_FORCE") == "1"
+        # collectives are issued when there is a peer, or when forced (one-GPU exercise of RCCL)
+        self.active = dist.is_initialized() and (self.world > 1 or bool(force))
+        self.grad_dtype = _parse_dtype(grad_dtype if grad_dtype is not None
+                                       else os.environ.get("PCMP_DDP_GRAD_DTYPE"))
+        self._comm_stream = None
+        self._lowp = None
+        if self.active and flat.grad.is_cuda:
+            # one comm stream per DDP instance; high priority so its short cast kernels and RCCL's
+            # stream hand-offs are not queued behind long conv grids
+            self._comm_stream = torch.cuda.Stream(flat.grad.device, priority=-1)
+            if self.grad_dtype != torch.float32:
+                self._lowp = torch.empty(flat.grad.numel(), dtype=self.grad_dtype, device=flat.grad.device)
+        elif self.grad_dtype != torch.float32 and self.active:
+            self._lowp = torch.empty(flat.grad.numel(), dtype=self.grad_dtype, device=flat.grad.device)
         esz = flat.grad.element_size()
         sizes = []
         offs = flat.offsets + [flat.numel]
@@ -128,6 +162,7 @@ class DistributedDataParallel(torch.nn.Module):
             b.pending = len(b.params)
             b.work = None
             b.launched = False
+            b.streams.clear()
         self._next_launch = 0
 
     @contextlib.contextmanager
@@ -145,6 +180,9 @@ class DistributedDataParallel(torch.nn.Module):
         b = self._bucket_of.get(id(p))
         if b is None:
             return
+        if self._comm_stream is not None:
+            s = torch.cuda.current_stream(p.device)
+            b.streams[s.cuda_stream] = s
         b.pending -= 1
         if b.pending == 0:
             self._launch_ready()
@@ -156,34 +194,65 @@ class DistributedDataParallel(torch.nn.Module):
 
     def _launch(self, b: _Bucket):
         b.launched = True
-        if self.world <= 1 or not self.require_sync:
+        if not self.active or not self.require_sync:
             return
         view = self.flat.grad[b.start:b.end]
-        if view.is_cuda:
-            # gradients of a bucket may come from the compute stream (BN, Linear, torch layers) and
-            # from the WGRAD side stream (conv weights): the collective is ordered after both
-            from ..ops.params import active_streams
-            cur = torch.cuda.current_stream(view.device)
-            for s in active_streams(view.device):
-                if s != cur:
-                    cur.wait_stream(s)
-        b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        cs = self._comm_stream
+        if cs is None:                                   # CPU tensors (gloo)
+            if self._lowp is not None:
+                low = self._lowp[b.start:b.end]
+                low.copy_(view)
+                b.work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            else:
+                b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            return
+        # order the collective after exactly the streams that wrote this bucket's gradients
+        streams = b.streams or {0: torch.cuda.current_stream(view.device)}
+        for key, s in streams.items():
+            ev = b.events.get(key)
+            if ev is None:
+                ev = b.events[key] = torch.cuda.Event()
+            ev.record(s)
+            cs.wait_event(ev)
+        with torch.cuda.stream(cs):
+            if self._lowp is not None:
+                low = self._lowp[b.start:b.end]
+                low.copy_(view)                          # fp32 -> bf16 on the comm stream
+                b.work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            else:
+                b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def finish_gradient_sync(self):
         """Call after ``loss.backward()``: launches buckets whose params produced no gradient
-        (their slices hold zeros from ``zero_grad``), then joins every outstanding all-reduce
-        (the compute stream waits on RCCL's stream; the host does not block for NCCL)."""
+        (their slices hold zeros from ``zero_grad``), then joins every outstanding all-reduce.
+        GPU: the comm stream waits for RCCL, casts low-precision sums back into the fp32 arena,
+        and the compute stream waits for the comm stream once; the host never blocks."""
         for b in self.buckets:
             b.pending = 0
         self._launch_ready()
-        for b in self.buckets:
-            if b.work is not None:
-                b.work.wait()
-                b.work = None
+        cs = self._comm_stream
+        ctx = torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()
+        with ctx:
+            for b in self.buckets:
+                if b.work is not None:
+                    b.work.wait()
+                    if self._lowp is not None:
+                        self.flat.grad[b.start:b.end].copy_(self._lowp[b.start:b.end])
+                    b.work = None
+        if cs is not None:
+            torch.cuda.current_stream(cs.device).wait_stream(cs)
         self._reset()
 
     def grad_scale(self) -> float:
         return 1.0 / self.world if (self.average and self.world > 1) else 1.0
+
+
+def _parse_dtype(d) -> torch.dtype:
+    if d is None or d == "" or d == "fp32" or d == "float32" or d == torch.float32:
+        return torch.float32
+    if d in ("bf16", "bfloat16", torch.bfloat16):
+        return torch.bfloat16
+    raise ValueError(f"unsupported DDP gradient all-reduce dtype: {d!r} (fp32 or bf16)")
 
 
 def convert_sync_batchnorm(module: torch.nn.Module, process_group=None) -> torch.nn.Module:

@@ -63,6 +63,9 @@ def init(local_rank_arg: int | None = None, backend: str | None = None, timeout_
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # RCCL's internal streams at high priority: its ring kernels hold only a few CUs, and a
+        # high-priority queue lets their workgroups start between the conv grids of backward
+        os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         be = backend or ("nccl" if use_gpu else "gloo")
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))

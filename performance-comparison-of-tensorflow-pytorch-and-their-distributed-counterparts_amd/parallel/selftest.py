@@ -44,7 +44,7 @@ def _loss(model, kind, x, y):
     return cross_entropy(model.forward_logits(x), y)
 
 
-def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.01, device="cpu"):
+def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.01, device="cpu", grad_dtype=None):
     """``device='cuda'``: every rank runs the HIP kernels on cuda:0 (one-GPU rehearsal) and the
     gradient buckets are CUDA tensors all-reduced by gloo; tolerances cover bf16 compute."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -61,7 +61,8 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
         from .ddp import convert_sync_batchnorm
         convert_sync_batchnorm(model)
     flat = FlatParams(model.parameters(), shadow_dtype=None if dev.type == "cpu" else torch.bfloat16)
-    ddp = DistributedDataParallel(model, flat, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
+    ddp = DistributedDataParallel(model, flat, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb / 4,
+                                  grad_dtype=grad_dtype)
     opt = optim.SGD(flat, lr=0.05, momentum=0.9)
     opt.set_grad_scale(ddp.grad_scale())
     N = 8 * world
@@ -80,7 +81,9 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     _loss(model, kind, x[shard], y[shard]).backward()
     ddp.finish_gradient_sync()
     avg = flat.grad * ddp.grad_scale()
-    if dev.type == "cpu" and kind == "resnet_syncbn":   # deep net: compare relative to the gradient norm
+    if grad_dtype == "bf16":     # bf16 all-reduce: each rank's shard gradient rounded to 8 mantissa bits
+        ok_grad = bool((avg - ref_grad).norm() <= 2e-2 * ref_grad.norm() + 1e-6)
+    elif dev.type == "cpu" and kind == "resnet_syncbn":   # deep net: compare relative to the gradient norm
         ok_grad = bool((avg - ref_grad).norm() <= 1e-4 * ref_grad.norm())
     elif dev.type == "cpu":
         ok_grad = torch.allclose(avg, ref_grad, atol=1e-5, rtol=1e-4)
@@ -104,3 +107,68 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dist.destroy_process_group()
+
+
+def rccl_force_check(kind: str = "resnet18", grad_dtype: str = "fp32", steps: int = 3) -> dict:
+    """One-GPU exercise of the RCCL data-parallel path (run in its own process).
+
+    Initialises the ``nccl`` process group at world size 1 and wraps the model in the framework's
+    DDP with ``force=True`` so every bucket's all-reduce is issued through RCCL from the comm
+    stream, ordered by events after the compute and WGRAD streams.  The all-reduced gradient of a
+    one-rank job is the local gradient, so with fp32 buckets it must be BIT-identical to the same
+    backward without DDP; with bf16 buckets it must equal the bf16 rounding of it.  Parameters after
+    ``steps`` SGD steps with and without DDP must match the same way."""
+    from ..models import resnet
+    from ..ops import cross_entropy
+    from .. import optim
+    from ..utils.flat import FlatParams
+    from . import launch
+    from .ddp import DistributedDataParallel
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    env = launch.init(force_init=True)
+    assert env.backend == "nccl", env
+    dev = env.device
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.rand(16, 3, 64, 64, device=dev, generator=g)
+    y = torch.randint(0, 10, (16,), device=dev, generator=g)
+
+    def run(use_ddp):
+        torch.manual_seed(0)
+        model = getattr(resnet, kind)(num_classes=10).to(dev).train()
+        flat = FlatParams(model.parameters())
+        ddp = DistributedDataParallel(model, flat, force=True, grad_dtype=grad_dtype,
+                                      bucket_cap_mb=2.0, first_bucket_mb=0.5, last_bucket_mb=0.5) if use_ddp else None
+        opt = optim.SGD(flat, lr=0.01, momentum=0.9)
+        grads = []
+        for _ in range(steps):
+            opt.zero_grad()
+            cross_entropy(model.forward_logits(x), y).backward()
+            if ddp is not None:
+                ddp.finish_gradient_sync()
+            grads.append(flat.grad.clone())
+            opt.step()
+        torch.cuda.synchronize()
+        return grads, flat.master.clone(), (len(ddp.buckets) if ddp else 0)
+
+    ref_g, ref_p, _ = run(False)
+    got_g, got_p, nb = run(True)
+    if grad_dtype == "bf16":
+        first = ref_g[0].to(torch.bfloat16).float()
+        ok_grad = bool(torch.equal(got_g[0], first))
+        ok_param = bool(((got_p - ref_p).norm() <= 1e-2 * ref_p.norm()).item())
+    else:
+        ok_grad = all(torch.equal(a, b) for a, b in zip(ref_g, got_g))
+        ok_param = bool(torch.equal(ref_p, got_p))
+    res = {"ok_grad": ok_grad, "ok_param": ok_param, "nbuckets": nb, "backend": env.backend,
+           "maxdiff": float((got_g[0] - ref_g[0]).abs().max())}
+    launch.shutdown()
+    return res
+
+
+if __name__ == "__main__":
+    import json
+    import sys
+    kind = sys.argv[1] if len(sys.argv) > 1 else "resnet18"
+    gd = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+    print(json.dumps(rccl_force_check(kind, gd)), flush=True)

@@ -93,6 +93,19 @@ class Watchdog:
                 self.last = time.monotonic()
 
 
+def _env_int(name: str, default: int) -> int:
+    """Integer environment knob; a malformed value warns and falls back instead of raising deep
+    inside a training loop."""
+    raw = os.environ.get(name)
+    if raw is None or raw.strip() == "":
+        return default
+    try:
+        return int(raw)
+    except ValueError:
+        print(f"[pcmp] ignoring {name}={raw!r} (not an integer); using {default}", file=sys.stderr)
+        return default
+
+
 class StepThrottle:
     """Bounds how many training steps the host may enqueue ahead of the GPU.
 
@@ -104,12 +117,21 @@ class StepThrottle:
     B=256, 221 GiB at B=1024 (``profiles/r1_alloc_ab.txt``), a few steps away from the 288 GB of
     HBM.  ``tick()`` after each step records an event on the current stream and, once more than
     ``depth`` steps are in flight, waits for the oldest; with depth 2 the GPU still always has a
-    whole step queued.  ``PCMP_MAX_INFLIGHT`` overrides the depth (0 disables).  No-op on CPU."""
+    whole step queued.  ``PCMP_MAX_INFLIGHT`` overrides the depth (0 disables).  No-op on CPU.
+
+    The bound is on run-ahead, not on fragmentation: at depth 2 the allocator still reserves about
+    3.4x the live peak (B=256: 36.9 GiB reserved for a 10.7 GiB peak; B=1024: 145 GiB for 41.5 GiB,
+    ``profiles/r1_throttle_ab.txt``) because blocks recorded on the WGRAD side stream and the
+    comm stream are reusable only once those streams pass them.  Depth 1 cuts B=256 to 25.9 GiB
+    at unchanged throughput (``profiles/r1_inflight_depth_ab.txt``); depth 2 stays the default as
+    margin for slower or contended hosts (8 ranks enqueueing on one node).  The wait uses a
+    blocking event, so a throttled rank sleeps instead of spinning a core that the data loader
+    and RCCL's proxy threads need."""
 
     def __init__(self, device=None, depth: int | None = None):
         if depth is None:
-            depth = int(os.environ.get("PCMP_MAX_INFLIGHT", "2"))
-        self.depth = depth
+            depth = _env_int("PCMP_MAX_INFLIGHT", 2)
+        self.depth = max(0, int(depth))
         self.device = torch.device(device) if device is not None else None
         self._events = []
 
@@ -118,7 +140,7 @@ class StepThrottle:
             return
         if torch.cuda.is_current_stream_capturing():
             return
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(blocking=True)
         ev.record(torch.cuda.current_stream(self.device))
         self._events.append(ev)
         while len(self._events) > self.depth:

@@ -51,3 +51,50 @@ def test_plan_buckets_small_last_bucket():
     assert sum(e - s for s, e in b) == 100
     assert plan_buckets([5], 25, 200, 35) == [(0, 1)]
     assert plan_buckets([10, 10], 25, 200, 100) == [(0, 1), (1, 2)]   # the tail never takes slice 0
+
+
+def test_ddp_bf16_allreduce_cpu(tmp_path):
+    from pcmp.parallel.selftest import ddp_equivalence_worker
+    os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
+    mp.spawn(ddp_equivalence_worker, args=(2, _port(), str(tmp_path), "mlp", 0.01, "cpu", "bf16"), nprocs=2, join=True)
+    for r in range(2):
+        res = torch.load(tmp_path / f"rank{r}.pt", weights_only=True)
+        assert res["ok_grad"], res
+        assert res["ok_sync"], res
+
+
+def _force_worker(rank, port, out):
+    import torch.distributed as dist
+    from pcmp.models.layers import MLPHead
+    from pcmp.ops import cross_entropy
+    from pcmp.parallel import launch
+    from pcmp.parallel.ddp import DistributedDataParallel
+    from pcmp.utils.flat import FlatParams
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    env = launch.init(force_init=True, use_gpu=False)
+    assert env.backend == "gloo" and dist.is_initialized()
+    torch.manual_seed(0)
+    m = MLPHead(16, 32, 4, p=0.0)
+    flat = FlatParams(m.parameters(), shadow_dtype=None)
+    ddp = DistributedDataParallel(m, flat, force=True, bucket_cap_mb=0.001, first_bucket_mb=0.0005)
+    x, y = torch.randn(8, 16), torch.randint(0, 4, (8,))
+    flat.zero_grad()
+    cross_entropy(m.forward_logits(x), y).backward()
+    ref = flat.grad.clone()
+    flat.zero_grad()
+    cross_entropy(m.forward_logits(x), y).backward()
+    issued = sum(b.work is not None for b in ddp.buckets)
+    ddp.finish_gradient_sync()
+    torch.save({"equal": torch.equal(ref, flat.grad), "issued": issued, "n": len(ddp.buckets),
+                "scale": ddp.grad_scale()}, out)
+    launch.shutdown()
+
+
+def test_ddp_force_world1_issues_collectives(tmp_path):
+    os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
+    out = str(tmp_path / "f.pt")
+    mp.spawn(_force_worker, args=(_port(), out), nprocs=1, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res["equal"], res
+    assert res["n"] >= 2 and res["issued"] == res["n"], res    # every bucket went through the collective
+    assert res["scale"] == 1.0
