@@ -44,9 +44,10 @@ def main(argv=None):
     from pcmp.parallel.launch import device_report
     from pcmp.utils.report import rprint
     device_report(env.local_rank, printer=rprint)
-    if args.model == "mlp":
-        return run_mlp_cpu(args, env)
-    return run_image(args, env)
+    with cli.run_context(args, env):
+        if args.model == "mlp":
+            return run_mlp_cpu(args, env)
+        return run_image(args, env)
 
 
 def build_image_model(args, device):
@@ -102,36 +103,56 @@ def run_image(args, env):
 
 
 def run_mlp_cpu(args, env):
-    """BASELINE config 1: the 2-layer MLP head on random IMDB-shaped token tensors, CPU."""
+    """BASELINE config 1: the 2-layer MLP head on random IMDB-shaped token tensors, CPU.
+
+    Train on a sharded 2,048-review split and evaluate on a held-out 512-review split (indices
+    2048..2559 of the same synthetic corpus, so labels follow the same class signatures); the
+    epoch line reports the held-out loss / accuracy, summed over ranks."""
     from pcmp.data.synthetic import BatchLoader, SyntheticIMDB
     from pcmp.engine.trainer import make_state
     from pcmp.models.layers import MLPHead
     from pcmp.ops import cross_entropy
+    from pcmp.parallel.metrics import all_reduce_sum
     from pcmp.parallel.sampler import ShardedSampler
     from pcmp.utils.report import epoch_line, rprint, training_time_line
-    ds = SyntheticIMDB(n=2048, seed=args.seed)
+    n_train, n_test = 2048, 512
+    ds = SyntheticIMDB(n=n_train + n_test, seed=args.seed)
     model = MLPHead(128, 512, 2, 0.2).to(env.device)
     state = make_state(model, "adam", lr=args.lr or 3e-3, distributed=env.distributed)
-    loader = BatchLoader(ds, args.batch_size, ShardedSampler(len(ds)), env.device)
+    loader = BatchLoader(ds, args.batch_size, ShardedSampler(list(range(n_train))), env.device)
+    test_loader = BatchLoader(ds, args.batch_size, ShardedSampler(list(range(n_train, n_train + n_test)), shuffle=False),
+                              env.device)
+
+    def feats(ids):
+        return (ids.float() / ds.VOCAB).to(env.device)
+
     t1 = time.time()
     for epoch in range(args.epochs):
         loader.set_epoch(epoch)
-        tot, n, correct = 0.0, 0, 0
+        model.train()
+        tot, n = 0.0, 0
         for ids, mask, y in loader:
-            x = (ids.float() / ds.VOCAB).to(env.device)
             state.zero_grad()
-            z = model.forward_logits(x)
-            loss = cross_entropy(z, y)
+            loss = cross_entropy(model.forward_logits(feats(ids)), y)
             state.backward_step(loss)
-            tot += float(loss)
+            tot += float(loss.detach())
             n += 1
-            correct += int((z.argmax(1) == y).sum())
-        rprint(epoch_line(epoch + 1, args.epochs, tot / max(1, n), tot / max(1, n), correct / len(ds)))
+        model.eval()
+        te_loss, te_correct, te_n, te_batches = 0.0, 0, 0, 0
+        with torch.no_grad():
+            for ids, mask, y in test_loader:
+                z = model.forward_logits(feats(ids))
+                te_loss += float(cross_entropy(z, y))
+                te_correct += int((z.argmax(1) == y).sum())
+                te_n += y.numel()
+                te_batches += 1
+        s = all_reduce_sum([tot, n, te_loss, te_batches, te_correct, te_n])
+        rprint(epoch_line(epoch + 1, args.epochs, s[0] / max(1, s[1]), s[2] / max(1, s[3]), s[4] / max(1, s[5])))
     dt = time.time() - t1
     rprint(training_time_line(dt))
-    cli.write_json(args, {"script": "another_neural_net", "preset": "mlp-cpu", "train_seconds": dt})
+    cli.write_json(args, {"script": "another_neural_net", "preset": "mlp-cpu", "train_seconds": dt,
+                          "test_loss": s[2] / max(1, s[3]), "test_accuracy": s[4] / max(1, s[5])})
     return 0
-
 
 if __name__ == "__main__":
     sys.exit(main())

@@ -91,6 +91,20 @@ def load_split_train_test(datadir, valid_size=0.2, batch_size=64, distributed=Fa
     return tr, te
 
 
+def flow_from_directory(directory, target_size=224, batch_size=64, device=None, distributed=False, seed=0):
+    """B8: Keras ``ImageDataGenerator(rescale=1./255).flow_from_directory(directory,
+    target_size=(224,224), batch_size=64, class_mode="categorical", shuffle=True)`` (resnet.py:10-16).
+    Batches are uint8 NCHW (the model's input conversion applies the 1/255 rescale on the device)
+    with integer labels; ``keras_fit`` one-hot encodes them (categorical).  Prints Keras' "Found N
+    images belonging to K classes." line."""
+    from .synthetic import BatchLoader
+    data = ImageFolder(directory, size=target_size)
+    print(f"Found {len(data)} images belonging to {len(data.classes)} classes.")
+    if distributed:
+        return BatchLoader(data, batch_size, ShardedSampler(len(data), shuffle=True, seed=seed), device)
+    return BatchLoader(data, batch_size, device=device, shuffle=True, seed=seed)
+
+
 def get_random_images(dataset, num, distributed=False, device=None):
     indices = list(range(len(dataset)))
     random.shuffle(indices)

@@ -19,10 +19,15 @@ import torch
 
 
 def _hash01(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    # cheap deterministic per-element uniform in [0,1) (float64 LCG-style mixing, device friendly)
-    x = (idx.double() * 0.6180339887498949 + (seed % 1000003) * 0.7548776662466927) % 1.0
-    x = (x * 9301.0 + 49297.0) % 233280.0 / 233280.0
-    return x.float()
+    """Deterministic per-element uniform in [0,1): a 32-bit integer mix (xorshift-multiply) of
+    (seed, index), exact in int64 arithmetic on any device."""
+    m = 0xFFFFFFFF
+    x = (idx.to(torch.int64) * 2654435761 + ((seed * 40503 + 12345) & m)) & m
+    for _ in range(2):
+        x = x ^ (x >> 16)
+        x = (x * 0x45D9F3B) & m
+    x = x ^ (x >> 16)
+    return (x.double() / 4294967296.0).float()
 
 
 class SyntheticImages:
@@ -73,7 +78,7 @@ class SyntheticIMDB:
     def lengths(self, idx):
         # IMDB reviews are long: most are truncated at 128; ~25% shorter (min 8 tokens)
         u = _hash01(self.seed + 11, torch.as_tensor(idx).cpu())
-        L = torch.where(u < 0.75, torch.full_like(u, self.max_len), 8 + (u - 0.0) / 0.75 * (self.max_len - 8))
+        L = torch.where(u < 0.75, torch.full_like(u, self.max_len), 8 + (u - 0.75) / 0.25 * (self.max_len - 8))
         return L.long().clamp(8, self.max_len)
 
     def get_batch(self, idx, device=None):

@@ -7,6 +7,7 @@ Every reference constant becomes a flag whose default is the reference value (SU
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 
@@ -34,8 +35,12 @@ def common_parser(desc):
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--kernels", choices=["hip", "torch"], default="hip",
                     help="torch = PyTorch reference ops (parity runs only)")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="bf16 = HIP kernels (default); fp32 = the reference's precision as an explicit "
+                         "parity mode on the PyTorch reference ops (the HIP kernels are bf16-only)")
     ap.add_argument("--json", default=None, help="append a JSON metrics record to this file")
-    ap.add_argument("--profile", default=None, help="torch.profiler chrome trace path")
+    ap.add_argument("--profile", default=None,
+                    help="torch.profiler chrome trace path (per-rank suffix .rankN under DDP)")
     ap.add_argument("--reference-compat", action="store_true",
                     help="reproduce the reference's printed-value quirks (SURVEY §0.2)")
     ap.add_argument("--verbose", action="store_true", help="per-step prints (reference behaviour)")
@@ -61,10 +66,27 @@ def setup(args):
     from ..parallel import launch
     from ..utils.misc import seed_everything
     _lib.set_backend(args.kernels)
+    _lib.set_precision(getattr(args, "dtype", "bf16"))   # fp32 also selects the reference ops
     use_gpu = torch.cuda.is_available() if args.device == "auto" else args.device == "cuda"
     env = launch.init(args.local_rank, use_gpu=use_gpu)
     seed_everything(args.seed + (0 if args.kernels else 0))
     return env
+
+
+@contextlib.contextmanager
+def run_context(args, env):
+    """Operational wrappers every entry point runs its work under: ``--watchdog S`` (hang
+    detector, kicked by the engine loops; aborts the rank under DDP so the job does not hang) and
+    ``--profile PATH`` (torch.profiler Chrome trace with ROCm kernel activity)."""
+    from ..utils.misc import Watchdog, chrome_trace
+    with contextlib.ExitStack() as stack:
+        if getattr(args, "watchdog", 0) and args.watchdog > 0:
+            stack.enter_context(Watchdog(args.watchdog, abort=bool(getattr(env, "distributed", False))))
+        path = getattr(args, "profile", None)
+        if path and getattr(env, "world_size", 1) > 1:
+            path = f"{path}.rank{env.rank}"
+        stack.enter_context(chrome_trace(path))
+        yield
 
 
 def write_json(args, record):

@@ -20,6 +20,7 @@ import time
 import torch
 
 from ..utils import report as R
+from ..utils.misc import watchdog_kick
 
 
 def _logits(model, x):
@@ -59,14 +60,28 @@ class Batch1Predictor:
         return int(self.static_out.item())
 
 
-def infer_batch1(model, images: torch.Tensor, labels=None, device=None, use_graph=True, print_every_image=False,
-                 printer=R.rprint):
-    """images: [N,3,H,W] (host or device).  Returns (total_seconds, stats dict, predictions)."""
+def infer_batch1(model, images: torch.Tensor | None = None, labels=None, device=None, use_graph=True,
+                 print_every_image=False, printer=R.rprint, fetch=None, example=None):
+    """images: [N,3,H,W] (host or device).  Returns (total_seconds, stats dict, predictions).
+
+    ``fetch``: a callable returning ``(images, labels)``, called INSIDE the timed region -- the
+    reference times ``get_random_images(1000)`` (decode of the 1000 images) together with the
+    per-image loop (pytorch_training_inference_on_image.ipynb:891-905); ``example``
+    is then a [1,3,H,W] tensor of the input shape used to capture the graph beforehand."""
     device = device or next(model.parameters()).device
-    pred = Batch1Predictor(model, images[:1].to(device), use_graph=use_graph)
+    if fetch is None:
+        example = images[:1]
+    pred = Batch1Predictor(model, example.to(device), use_graph=use_graph)
     lat, preds = [], []
     t1 = time.time()
+    t_fetch = 0.0
+    if fetch is not None:
+        images, labels = fetch()
+        if images.dtype == torch.uint8:
+            images = images.float() / 255.0
+        t_fetch = time.time() - t1
     for ii in range(images.shape[0]):
+        watchdog_kick("inference")
         if print_every_image:
             printer(ii + 1)
         ts = time.perf_counter()
@@ -80,6 +95,7 @@ def infer_batch1(model, images: torch.Tensor, labels=None, device=None, use_grap
         lab = labels.tolist() if hasattr(labels, "tolist") else list(labels)
         stats["accuracy"] = sum(int(a == b) for a, b in zip(preds, lab)) / max(1, len(lab))
     stats["images_per_sec"] = images.shape[0] / total
+    stats["fetch_s"] = t_fetch
     stats["graph"] = pred.graph is not None
     return total, stats, preds
 

@@ -34,7 +34,7 @@ from ..parallel.metrics import all_reduce_max, all_reduce_sum
 from ..utils import report as R
 from ..utils.checkpoint import BestCheckpoint
 from ..utils.flat import FlatParams
-from ..utils.misc import StepThrottle, roctx_range
+from ..utils.misc import StepThrottle, roctx_range, watchdog_kick
 from ..utils.timer import PhaseTimer
 
 
@@ -81,6 +81,7 @@ class TrainState:
             self.timer.step()
         if self.throttle is not None:
             self.throttle.tick()
+        watchdog_kick("train_step")
 
     def phase_report(self, printer=None):
         """Summarise the per-phase device times into ``history['phases']`` (and print one line)."""
@@ -98,8 +99,9 @@ def make_state(model, optimizer="sgd", lr=0.1, distributed=False, clip=None, sha
     """Flatten trainable params (bf16 shadows on GPU), build the fused optimizer and DDP."""
     params = [p for p in model.parameters() if p.requires_grad]
     dev = params[0].device
-    if shadow_dtype is None:
-        shadow_dtype = torch.bfloat16 if dev.type == "cuda" else None
+    if shadow_dtype is None:   # bf16 weight shadows feed the bf16 kernels; none in fp32 parity mode
+        from ..ops import _lib
+        shadow_dtype = torch.bfloat16 if _lib.default_compute_dtype(dev) == torch.bfloat16 else None
     flat = FlatParams(params, shadow_dtype=shadow_dtype)
     opt = pcmp_optim.build(optimizer, flat, lr=lr, **opt_kw)
     ddp = DistributedDataParallel(model, flat) if distributed else None
@@ -121,6 +123,7 @@ def evaluate_images(model, loader, reference_compat=False):
     dev = None
     losses, accs = [], []
     for x, y in loader:
+        watchdog_kick("eval")
         z = _logits(model, x)
         logp = torch.log_softmax(z.float(), dim=1)
         losses.append(torch.nn.functional.nll_loss(logp, y))
@@ -260,6 +263,7 @@ def evaluate_text(model, loader):
     model.eval()
     accs = []
     for ids, mask, labels in loader:
+        watchdog_kick("eval")
         z = model.forward_logits(ids, mask)
         accs.append((z.float().argmax(1) == labels).float().mean())
     model.train()
@@ -309,6 +313,7 @@ def keras_evaluate(model, val, timed=True, printer=R.rprint):
     model.eval()
     tot, correct, n = 0.0, 0.0, 0
     for x, y in val:
+        watchdog_kick("eval")
         z = model.forward_logits(x).float()
         tot += float(torch.nn.functional.cross_entropy(z, y, reduction="sum"))
         correct += float((z.argmax(1) == y).sum())

@@ -20,6 +20,7 @@ from dataclasses import dataclass
 import torch
 from torch import nn
 
+from ..ops import _lib
 from ..ops.functions import cross_entropy
 from ..ops.rnn import EmbeddingFn
 from ..ops.transformer import attention, gelu, layer_norm, tanh
@@ -111,7 +112,7 @@ class BertForSequenceClassification(nn.Module):
     def _cdtype(self, device):
         if self.compute_dtype is not None:
             return self.compute_dtype
-        return torch.bfloat16 if device.type == "cuda" else torch.float32
+        return _lib.default_compute_dtype(device)
 
     def forward_logits(self, input_ids, attention_mask=None, token_type_ids=None):
         B, S = input_ids.shape

@@ -16,6 +16,7 @@ import math
 import torch
 from torch import nn
 
+from ..ops import _lib
 from ..ops.rnn import BiLSTMLayerFn, EmbeddingFn, MaskedMeanFn
 from .layers import Dropout, Linear
 
@@ -66,7 +67,7 @@ class BiLSTMClassifier(nn.Module):
     def _cdtype(self, device):
         if self.compute_dtype is not None:
             return self.compute_dtype
-        return torch.bfloat16 if device.type == "cuda" else torch.float32
+        return _lib.default_compute_dtype(device)
 
     def forward_logits(self, input_ids, attention_mask=None):
         """``attention_mask`` is accepted for API parity; the mask is ``input_ids > 0``."""

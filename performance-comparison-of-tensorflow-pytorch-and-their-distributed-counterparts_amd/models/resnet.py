@@ -22,6 +22,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops import _lib
 from ..ops.conv_blocks import ResidualBlockFn, StemFn, stem_s2d_wanted
 from ..ops.kernels import K
 from .layers import Conv2d, ConvBN, GlobalAvgPool, Linear, MLPHead
@@ -122,7 +123,7 @@ class ResNet(nn.Module):
     def _cdtype(self, device):
         if self.compute_dtype is not None:
             return self.compute_dtype
-        return torch.bfloat16 if device.type == "cuda" else torch.float32
+        return _lib.default_compute_dtype(device)
 
     def prepare_input(self, x):
         """NCHW float/uint8 images -> NHWC compute-dtype, channels padded to 8 (on the GPU: the

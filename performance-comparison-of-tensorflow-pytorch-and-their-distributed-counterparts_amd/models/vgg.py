@@ -16,9 +16,10 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops import _lib
+from ..ops.kernels import K
 from .layers import Conv2d, Dropout, Linear, MaxPool2d, MLPHead
 from .resnet import STEM_CIN_PAD
-from ..ops.kernels import K
 
 CFG16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
 
@@ -43,7 +44,7 @@ class VGG(nn.Module):
     def _cdtype(self, device):
         if self.compute_dtype is not None:
             return self.compute_dtype
-        return torch.bfloat16 if device.type == "cuda" else torch.float32
+        return _lib.default_compute_dtype(device)
 
     def prepare_input(self, x):
         dt = self._cdtype(x.device)

@@ -21,6 +21,7 @@ _lock = threading.Lock()
 _loaded = False
 _load_error: str | None = None
 _backend = os.environ.get("PCMP_KERNELS", "hip").lower()
+_compute_dtype: torch.dtype | None = None   # None: bf16 on the GPU, fp32 on the CPU
 
 
 def load(build_if_missing: bool = False) -> bool:
@@ -61,6 +62,28 @@ def set_backend(name: str) -> None:
 
 def backend() -> str:
     return _backend
+
+
+def set_precision(name: str) -> None:
+    """``--dtype``: 'bf16' (default; the HIP kernels, bf16 storage with fp32 accumulation) or
+    'fp32' (the reference's precision).  The HIP kernels are bf16-only, so
+    fp32 is an explicit parity mode: it also selects the PyTorch reference backend, whose ops run
+    in fp32 on the GPU (MIOpen / hipBLASLt underneath).  It exists to compare numerics and
+    accuracy with the reference, not for speed."""
+    global _compute_dtype
+    assert name in ("bf16", "fp32"), name
+    if name == "fp32":
+        _compute_dtype = torch.float32
+        set_backend("torch")
+    else:
+        _compute_dtype = None
+
+
+def default_compute_dtype(device: torch.device) -> torch.dtype:
+    """Activation dtype of a model on ``device`` unless the model was given one explicitly."""
+    if _compute_dtype is not None:
+        return _compute_dtype
+    return torch.bfloat16 if device.type == "cuda" else torch.float32
 
 
 def use_native(t: torch.Tensor) -> bool:

@@ -22,9 +22,9 @@ OP_NAMES = (
     "maxpool_fwd", "maxpool_bwd", "maxpool_bwd_bnr", "gap_fwd", "gap_bwd", "softmax_xent", "dropout", "relu_bwd", "colsum",
     "nchw_to_nhwc", "image_to_s2d",
     "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16", "wt_transpose_multi",
-    "embedding_fwd", "embedding_bwd", "lstm_cell_fwd", "lstm_cell_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
+    "embedding_fwd", "embedding_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
     "masked_mean_fwd", "masked_mean_bwd",
-    "layernorm_fwd", "layernorm_bwd", "gelu_fwd", "gelu_bwd", "bias_act_fwd",
+    "layernorm_fwd", "layernorm_bwd", "gelu_fwd", "gelu_bwd",
     "attention_fwd", "attention_bwd", "tanh_fwd", "tanh_bwd", "add_bf16",
 )
 

@@ -55,21 +55,40 @@ def chrome_trace(path: str | None):
     prof.export_chrome_trace(path)
 
 
+_ACTIVE_WATCHDOG = None
+
+
+def watchdog_kick(phase: str | None = None) -> None:
+    """Progress heartbeat from the training / eval / inference loops (no-op without ``--watchdog``)."""
+    wd = _ACTIVE_WATCHDOG
+    if wd is not None:
+        wd.kick(wd.state["step"] + 1, phase)
+
+
 class Watchdog:
     """Dumps the current step/phase and all Python stacks if no ``kick()`` for ``timeout_s``,
-    then (optionally) aborts the process so a dead rank does not hang the job."""
+    then (optionally) aborts the process so a dead rank does not hang the job.
+
+    The reference's runs that hung were stopped by hand (``KeyboardInterrupt``,
+    Standalone_Inference_Imagenette_trial.ipynb:119-120); ``--watchdog SECONDS`` on every entry
+    point starts one of these (``abort=True`` under DDP: a rank stuck in a collective exits with
+    status 3, and the launcher tears the job down instead of hanging).  The engine loops kick it
+    through :func:`watchdog_kick` once per step / batch / image."""
 
     def __init__(self, timeout_s: float = 600.0, abort: bool = False, stream=sys.stderr):
         self.timeout = timeout_s
         self.abort = abort
         self.stream = stream
         self.last = time.monotonic()
-        self.state = {"step": -1, "phase": "init"}
+        self.state = {"step": 0, "phase": "init"}   # step = kicks so far
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
 
     def start(self):
+        global _ACTIVE_WATCHDOG
+        self.last = time.monotonic()
         self._t.start()
+        _ACTIVE_WATCHDOG = self
         return self
 
     def kick(self, step=None, phase=None):
@@ -80,7 +99,17 @@ class Watchdog:
             self.state["phase"] = phase
 
     def stop(self):
+        global _ACTIVE_WATCHDOG
         self._stop.set()
+        if _ACTIVE_WATCHDOG is self:
+            _ACTIVE_WATCHDOG = None
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+        return False
 
     def _run(self):
         while not self._stop.wait(min(5.0, self.timeout / 4)):

@@ -86,8 +86,9 @@ def main(argv=None):
     total_steps = len(train_loader) * args.epochs
     state.sched = linear_schedule_with_warmup(state.opt, 0, total_steps)
     t0 = time.time()
-    times = train_text_classifier(state, train_loader, val_loader, args.epochs, print_batches=args.print_batches)
-    acc = test_text(model, test_loader)
+    with cli.run_context(args, env):
+        times = train_text_classifier(state, train_loader, val_loader, args.epochs, print_batches=args.print_batches)
+        acc = test_text(model, test_loader)
     cli.write_json(args, {"script": "pytorch_on_language_distr", "model": args.model, "world_size": env.world_size,
                           "epoch_seconds": times, "train_loss": state.history["train_loss"], "test_accuracy": acc,
                           "samples_per_sec": len(train_ds) * args.epochs / max(1e-9, sum(times)),

@@ -32,18 +32,30 @@ def main(argv=None):
     from pcmp.models.keras_resnet import KerasResNet50TL
     from pcmp.parallel.sampler import ShardedSampler
     dev = env.device
-    tr = SyntheticImages(args.train_size, 10, args.image_size, seed=args.seed)
-    va = SyntheticImages(args.val_size, 10, args.image_size, seed=args.seed + 1)
-    train = BatchLoader(tr, args.batch_size, ShardedSampler(len(tr), shuffle=True), dev)
-    val = BatchLoader(va, args.batch_size, ShardedSampler(len(va), shuffle=True), dev)
+    if args.data_dir:
+        # ImageDataGenerator(rescale=1./255).flow_from_directory(<dir>/train|val, batch 64, 224x224,
+        # categorical, shuffle=True) (resnet.py:10-16): uint8 batches, /255 on the device
+        from pcmp.data.imagefolder import flow_from_directory
+        train = flow_from_directory(os.path.join(args.data_dir, "train"), args.image_size, args.batch_size,
+                                    dev, env.distributed)
+        val = flow_from_directory(os.path.join(args.data_dir, "val"), args.image_size, args.batch_size,
+                                  dev, env.distributed)
+        num_classes = len(train.ds.classes)
+    else:
+        tr = SyntheticImages(args.train_size, 10, args.image_size, seed=args.seed)
+        va = SyntheticImages(args.val_size, 10, args.image_size, seed=args.seed + 1)
+        train = BatchLoader(tr, args.batch_size, ShardedSampler(len(tr), shuffle=True), dev)
+        val = BatchLoader(va, args.batch_size, ShardedSampler(len(va), shuffle=True), dev)
+        num_classes = 10
     x0, y0 = next(iter(train))
-    print(len(x0), tuple(x0[0].permute(1, 2, 0).shape), (len(y0), 10))
-    model = KerasResNet50TL(10, image_size=args.image_size).to(dev)
+    print(len(x0), tuple(x0[0].permute(1, 2, 0).shape), (len(y0), num_classes))
+    model = KerasResNet50TL(num_classes, image_size=args.image_size).to(dev)
     state = make_state(model, "sgd", lr=args.lr or 0.001, distributed=env.distributed)
-    hist = keras_fit(state, train, val, args.epochs)
-    loss, acc = keras_evaluate(model, val, timed=True)
+    with cli.run_context(args, env):
+        hist = keras_fit(state, train, val, args.epochs)
+        loss, acc = keras_evaluate(model, val, timed=True)
     cli.write_json(args, {"script": "resnet.py (keras counterpart)", "history": hist, "val_loss": loss,
-                          "val_accuracy": acc, "data": "synthetic"})
+                          "val_accuracy": acc, "data": "real" if args.data_dir else "synthetic"})
     return 0
 
 

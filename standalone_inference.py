@@ -41,6 +41,7 @@ def main(argv=None):
     from pcmp.models import resnet, vgg
     from pcmp.models.keras_resnet import preprocess_input_caffe
     from pcmp.utils import report as R
+    from pcmp.utils.misc import watchdog_kick
 
     dev = env.device
     if args.data_dir:
@@ -51,27 +52,29 @@ def main(argv=None):
         ds = SyntheticImages(args.num_images, 10, args.image_size, seed=args.seed)
         images, _ = ds.get_batch(list(range(args.num_images)), "cpu")
         R.rprint(args.num_images)
-    results = {}
-    for name in args.models.split(","):
-        fam, arch = name.split("-")
-        model = (resnet.ResNet("resnet50", 1000, variant="keras" if fam == "keras" else "torchvision")
-                 if arch == "resnet50" else vgg.vgg16(1000)).to(dev).eval()
-        pre = (lambda x: preprocess_input_caffe(x.permute(0, 2, 3, 1) * 255.0)) if fam == "keras" else (lambda x: x)
-        # single-image sanity prediction (E3)
-        top = predict_topk(model, pre(images[:1]).to(dev), None, 5 if fam == "pt" else 3)
-        R.rprint(R.label_probability_line(top[0][0], round(top[0][1], 2)))
-        predictor = Batch1Predictor(model, pre(images[:1]).to(dev))
-        lat = []
-        t = time.time()
-        for i in range(images.shape[0]):
-            ts = time.perf_counter()
-            idx = predictor(pre(images[i:i + 1]))
-            lat.append(time.perf_counter() - ts)
-            if args.print_labels:
-                R.rprint(idx)
-        total = time.time() - t
-        R.rprint(R.standalone_inference_line(total))
-        results[name] = {"total_s": total, **R.latency_stats(lat)}
+    with cli.run_context(args, env):
+        results = {}
+        for name in args.models.split(","):
+            fam, arch = name.split("-")
+            model = (resnet.ResNet("resnet50", 1000, variant="keras" if fam == "keras" else "torchvision")
+                     if arch == "resnet50" else vgg.vgg16(1000)).to(dev).eval()
+            pre = (lambda x: preprocess_input_caffe(x.permute(0, 2, 3, 1) * 255.0)) if fam == "keras" else (lambda x: x)
+            # single-image sanity prediction (E3)
+            top = predict_topk(model, pre(images[:1]).to(dev), None, 5 if fam == "pt" else 3)
+            R.rprint(R.label_probability_line(top[0][0], round(top[0][1], 2)))
+            predictor = Batch1Predictor(model, pre(images[:1]).to(dev))
+            lat = []
+            t = time.time()
+            for i in range(images.shape[0]):
+                watchdog_kick("inference")
+                ts = time.perf_counter()
+                idx = predictor(pre(images[i:i + 1]))
+                lat.append(time.perf_counter() - ts)
+                if args.print_labels:
+                    R.rprint(idx)
+            total = time.time() - t
+            R.rprint(R.standalone_inference_line(total))
+            results[name] = {"total_s": total, **R.latency_stats(lat)}
     cli.write_json(args, {"script": "standalone_inference", "n_images": int(images.shape[0]), "results": results,
                           "weights": "random-init", "data": "real" if args.data_dir else "synthetic"})
     return 0

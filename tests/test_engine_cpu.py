@@ -182,3 +182,90 @@ def test_train_state_has_throttle():
     st.zero_grad()
     st.backward_step(loss)
     assert st.throttle.in_flight == 0      # CPU: no events
+
+
+def test_synthetic_labels_are_balanced_and_lengths_vary():
+    """The synthetic datasets must carry every class (a degenerate hash once gave every image
+    class 2 and every review label 0 and length 128, which made any accuracy check vacuous)."""
+    from pcmp.data.synthetic import SyntheticImages, SyntheticIMDB
+    y = SyntheticImages(9469, 10, 32, seed=42).labels(torch.arange(9469))
+    counts = torch.bincount(y, minlength=10).float()
+    assert counts.min() > 0.8 * counts.mean() and counts.max() < 1.2 * counts.mean()
+    t = SyntheticIMDB(12500, seed=42)
+    lab = torch.bincount(t.labels(torch.arange(12500)), minlength=2).float()
+    assert abs(lab[0] / lab.sum() - 0.5) < 0.05
+    L = t.lengths(torch.arange(12500))
+    frac_full = (L == 128).float().mean()
+    assert 0.7 < frac_full < 0.8 and int(L.min()) < 20
+    # labels are a pure function of (seed, index): any shard / order sees the same labelled set
+    d = SyntheticImages(100, 10, 32, seed=7)
+    assert torch.equal(d.labels(torch.tensor([5, 17, 3])), d.labels(torch.arange(100))[[5, 17, 3]])
+
+
+def test_mlp_cpu_reports_held_out_metrics():
+    out = _run("another_neural_net.py", "--preset", "mlp-cpu", "--epochs", "2")
+    rec = _last_json(out)
+    assert "test_accuracy" in rec and 0.0 <= rec["test_accuracy"] <= 1.0
+    assert out.count("Epoch ") == 2
+
+
+def test_dtype_fp32_parity_mode_selects_reference_backend():
+    from pcmp.ops import _lib
+    try:
+        _lib.set_precision("fp32")
+        assert _lib.backend() == "torch"
+        assert _lib.default_compute_dtype(torch.device("cuda", 0)) == torch.float32
+        from pcmp.models.resnet import resnet18
+        m = resnet18(num_classes=10)
+        assert m._cdtype(torch.device("cuda", 0)) == torch.float32
+    finally:
+        _lib.set_precision("bf16")
+        _lib.set_backend("hip")
+    assert _lib.default_compute_dtype(torch.device("cuda", 0)) == torch.bfloat16
+    assert _lib.default_compute_dtype(torch.device("cpu")) == torch.float32
+
+
+def test_dtype_flag_on_entrypoint():
+    out = _run("another_neural_net.py", "--preset", "mlp-cpu", "--dtype", "fp32")
+    assert "Training time per epoch is" in out
+
+
+def test_watchdog_fires_and_is_kicked():
+    import io
+    import time as _t
+    from pcmp.utils.misc import Watchdog, watchdog_kick
+    buf = io.StringIO()
+    with Watchdog(0.4, abort=False, stream=buf) as wd:
+        for _ in range(5):
+            watchdog_kick("train_step")
+            _t.sleep(0.05)
+        assert wd.state["step"] == 5 and wd.state["phase"] == "train_step"
+        _t.sleep(1.6)      # no kicks: the watchdog reports the stall with the last step/phase
+    assert "[watchdog] no progress" in buf.getvalue() and "step=5 phase=train_step" in buf.getvalue()
+    watchdog_kick("after")  # no active watchdog: a no-op
+
+
+def test_profile_and_watchdog_flags_on_entrypoint(tmp_path):
+    trace = tmp_path / "trace.json"
+    _run("another_neural_net.py", "--preset", "mlp-cpu", "--watchdog", "120", "--profile", str(trace))
+    assert trace.exists() and trace.stat().st_size > 0
+    json.loads(trace.read_text())
+
+
+def test_keras_flow_from_directory(tmp_path):
+    import numpy as np
+    from PIL import Image
+    for split in ("train", "val"):
+        for c in ("cat", "dog", "eel"):
+            d = tmp_path / split / c
+            d.mkdir(parents=True)
+            for i in range(2):
+                Image.fromarray((np.random.rand(20, 30, 3) * 255).astype(np.uint8)).save(d / f"{i}.JPEG")
+    from pcmp.data.imagefolder import flow_from_directory
+    it = flow_from_directory(str(tmp_path / "train"), 32, 4, None)
+    xs = [x for x, _ in it]
+    assert len(it.ds) == 6 and it.ds.classes == ["cat", "dog", "eel"]
+    assert xs[0].dtype == torch.uint8 and tuple(xs[0].shape[1:]) == (3, 32, 32)
+    out = _run("resnet.py", "--data-dir", str(tmp_path), "--image-size", "32", "--batch-size", "4", "--epochs", "1")
+    assert "Found 6 images belonging to 3 classes." in out and "the inference takes" in out
+    assert _last_json(out)["data"] == "real"
