@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STAGE=${STAGE:-all}
 if [ "$STAGE" = all ] || [ "$STAGE" = tests ]; then
-timeout -k 10 600 python -u -m pytest tests/test_model_parity_gpu.py -x -v -s --timeout 240 --timeout-method thread > gpurun_out/parity.log 2>&1 || { echo "parity tests failed"; tail -60 gpurun_out/parity.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_model_parity_gpu.py -v -s --timeout 240 --timeout-method thread > gpurun_out/parity.log 2>&1 || { echo "parity tests failed"; tail -60 gpurun_out/parity.log; exit 1; }
 grep -E "rel err|median|convergence|TL flow|loss fp32|passed|failed" gpurun_out/parity.log
 fi
 if [ "$STAGE" = all ] || [ "$STAGE" = repro ]; then
