@@ -362,6 +362,217 @@ __global__ void bn_bwd_apply_kernel(const __bf16* __restrict__ dy, const __bf16*
   }
 }
 
+// ---- v2 apply kernels (default): fixed channel group per thread, one wave of the whole tensor ---
+// The grid's thread count T is a multiple of CV = C/8 (CV divides 256), so the 8-channel group
+// i % CV of a thread is the same at every step of its walk: the per-channel coefficients are
+// loaded ONCE into registers (v1 re-read them and did a 64-bit modulo per vector).  Measured
+// (tools/ew_micro.py, profiles/r2_ew_apply_ab.txt, ResNet-50 B=256 shapes, in-process A/B): the
+// best schedule is ONE 16-B vector per operand per thread over a grid that covers the tensor
+// (U = 1, no block cap): 6.0-7.0 TB/s, 8 % less time than v1's 4096-block grid-stride loop and
+// bitwise identical to it; U = 2/4 independent loads per thread or capped grids (2048-16384
+// blocks) were slower, non-temporal stores made no difference.  Full groups of U run without
+// bounds checks (a per-element guard would make hipcc wait vmcnt(0) per load); the tail is one
+// guarded pass.
+static Knob kn_bn_apply_v("bn_apply_v", 2);
+static Knob kn_ew_unroll("ew_unroll", 1);
+static Knob kn_ew_blocks("ew_blocks", 1 << 30);
+static Knob kn_ew_nt("ew_nt", 0);   // 1: non-temporal (streaming) output stores
+
+__device__ __forceinline__ void coef8(const float* p, int cv, float* d) {
+  const f32x4 a0 = reinterpret_cast<const f32x4*>(p)[cv * 2], a1 = reinterpret_cast<const f32x4*>(p)[cv * 2 + 1];
+  d[0] = a0[0]; d[1] = a0[1]; d[2] = a0[2]; d[3] = a0[3];
+  d[4] = a1[0]; d[5] = a1[1]; d[6] = a1[2]; d[7] = a1[3];
+}
+
+// X2: 0 none, 1 plain residual add, 2 second BN branch (x2*sc2+sh2)
+__device__ __forceinline__ void st16(__bf16* p, const u16x8& u, bool nt) {
+  if (nt) __builtin_nontemporal_store(u, reinterpret_cast<u16x8*>(p));
+  else *reinterpret_cast<u16x8*>(p) = u;
+}
+__device__ __forceinline__ void st8f(__bf16* p, const float* v, bool nt) {
+  u16x8 u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+  st16(p, u, nt);
+}
+
+template <int U, int X2, bool RELU, bool MB, bool NT = false>
+__global__ void __launch_bounds__(256) bn_apply_v2_kernel(const __bf16* __restrict__ x, const float* __restrict__ sc,
+                                                          const float* __restrict__ shf, const __bf16* __restrict__ x2,
+                                                          const float* __restrict__ sc2, const float* __restrict__ shf2,
+                                                          __bf16* __restrict__ y, int nvec, int CV,
+                                                          uint8_t* __restrict__ mbits) {
+  const int T = gridDim.x * 256;
+  const int tid = blockIdx.x * 256 + threadIdx.x;
+  const int cv = tid % CV;
+  float a[8], b[8], a2[8], b2[8];
+  coef8(sc, cv, a);
+  coef8(shf, cv, b);
+  if constexpr (X2 == 2) { coef8(sc2, cv, a2); coef8(shf2, cv, b2); }
+  auto body = [&](const u16x8& xv, const u16x8& wv, int i) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = bf2f(xv[e]) * a[e] + b[e];
+      if constexpr (X2 == 1) v[e] += bf2f(wv[e]);
+      if constexpr (X2 == 2) v[e] += bf2f(wv[e]) * a2[e] + b2[e];
+      if constexpr (RELU) v[e] = fmaxf(v[e], 0.f);
+    }
+    u16x8 u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+    st16(y + (size_t)i * 8, u, NT);
+    if constexpr (MB) {
+      unsigned bits = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bits |= ((u[e] & 0x8000u) == 0 && (u[e] & 0x7fffu) != 0) ? (1u << e) : 0u;
+      mbits[i] = (uint8_t)bits;
+    }
+  };
+  int base = tid;
+  for (; base + (U - 1) * T < nvec; base += U * T) {
+    u16x8 xv[U], wv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) xv[k] = *reinterpret_cast<const u16x8*>(x + (size_t)(base + k * T) * 8);
+    if constexpr (X2 != 0) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) wv[k] = *reinterpret_cast<const u16x8*>(x2 + (size_t)(base + k * T) * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) body(xv[k], wv[k], base + k * T);
+  }
+  for (int i = base; i < nvec; i += T) {
+    const u16x8 xv = *reinterpret_cast<const u16x8*>(x + (size_t)i * 8);
+    u16x8 wv{};
+    if constexpr (X2 != 0) wv = *reinterpret_cast<const u16x8*>(x2 + (size_t)i * 8);
+    body(xv, wv, i);
+  }
+}
+
+template <int U, bool MASK, bool TWO, bool G, bool NT = false>
+__global__ void __launch_bounds__(256) bn_bwd_apply_v2_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ ymask,
+                                                              const __bf16* __restrict__ x, const float* __restrict__ coef,
+                                                              __bf16* __restrict__ dx, const __bf16* __restrict__ x2,
+                                                              const float* __restrict__ coef2, __bf16* __restrict__ dx2,
+                                                              __bf16* __restrict__ g_out, int nvec, int CV) {
+  const int T = gridDim.x * 256;
+  const int tid = blockIdx.x * 256 + threadIdx.x;
+  const int cv = tid % CV;
+  const int C = CV * 8;
+  float k1[8], k2[8], k3[8], q1[8], q2[8], q3[8];
+  coef8(coef, cv, k1); coef8(coef + C, cv, k2); coef8(coef + 2 * C, cv, k3);
+  if constexpr (TWO) { coef8(coef2, cv, q1); coef8(coef2 + C, cv, q2); coef8(coef2 + 2 * C, cv, q3); }
+  auto body = [&](const u16x8& gv, const u16x8& mv, const u16x8& xv, const u16x8& x2v, int i) {
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      g[e] = bf2f(gv[e]);
+      if constexpr (MASK) g[e] = bf2f(mv[e]) > 0.f ? g[e] : 0.f;
+    }
+    if constexpr (G) {
+      if constexpr (MASK) st8f(g_out + (size_t)i * 8, g, NT);
+      else st16(g_out + (size_t)i * 8, gv, NT);
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = k1[e] * g[e] + k2[e] * bf2f(xv[e]) + k3[e];
+    st8f(dx + (size_t)i * 8, o, NT);
+    if constexpr (TWO) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = q1[e] * g[e] + q2[e] * bf2f(x2v[e]) + q3[e];
+      st8f(dx2 + (size_t)i * 8, o, NT);
+    }
+  };
+  auto ld = [](const __bf16* p, int i) { return *reinterpret_cast<const u16x8*>(p + (size_t)i * 8); };
+  int base = tid;
+  for (; base + (U - 1) * T < nvec; base += U * T) {
+    u16x8 gv[U], mv[U], xv[U], x2v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) gv[k] = ld(dy, base + k * T);
+    if constexpr (MASK) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) mv[k] = ld(ymask, base + k * T);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) xv[k] = ld(x, base + k * T);
+    if constexpr (TWO) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) x2v[k] = ld(x2, base + k * T);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) body(gv[k], mv[k], xv[k], x2v[k], base + k * T);
+  }
+  for (int i = base; i < nvec; i += T) {
+    u16x8 mv{}, x2v{};
+    if constexpr (MASK) mv = ld(ymask, i);
+    if constexpr (TWO) x2v = ld(x2, i);
+    body(ld(dy, i), mv, ld(x, i), x2v, i);
+  }
+}
+
+// grid for the v2 kernels: a multiple of 8 blocks (so the thread count is a multiple of CV <= 256)
+static int ew2_blocks(int64_t nvec, int U) {
+  const int cap = std::max(8, kn_ew_blocks.get() / 8 * 8);
+  const int need = ceil_div(nvec, 256 * (int64_t)U);
+  return std::max(8, std::min(cap, ceil_div(need, 8) * 8));
+}
+static bool ew2_ok(int CV, int64_t nvec) { return kn_bn_apply_v.get() == 2 && 256 % CV == 0 && nvec < (1ll << 31); }
+
+template <int U>
+static void launch_bn_apply_v2(const __bf16* x, const float* sc, const float* sh, const __bf16* x2, const float* sc2,
+                               const float* sh2, __bf16* y, int64_t nvec, int CV, bool relu, uint8_t* mb,
+                               hipStream_t st) {
+  const int blocks = ew2_blocks(nvec, U);
+  const int x2m = x2 ? (sc2 ? 2 : 1) : 0;
+#define PCMP_BNA(X2, R, M)                                                                                      \
+  do {                                                                                                        \
+    if (kn_ew_nt.get())                                                                                       \
+      hipLaunchKernelGGL((bn_apply_v2_kernel<U, X2, R, M, true>), dim3(blocks), dim3(256), 0, st, x, sc, sh, x2, \
+                         sc2, sh2, y, (int)nvec, CV, mb);                                                     \
+    else                                                                                                      \
+      hipLaunchKernelGGL((bn_apply_v2_kernel<U, X2, R, M, false>), dim3(blocks), dim3(256), 0, st, x, sc, sh, x2, \
+                         sc2, sh2, y, (int)nvec, CV, mb);                                                     \
+  } while (0)
+  if (x2m == 0) {
+    if (relu) { if (mb) PCMP_BNA(0, true, true); else PCMP_BNA(0, true, false); }
+    else { if (mb) PCMP_BNA(0, false, true); else PCMP_BNA(0, false, false); }
+  } else if (x2m == 1) {
+    if (relu) { if (mb) PCMP_BNA(1, true, true); else PCMP_BNA(1, true, false); }
+    else { if (mb) PCMP_BNA(1, false, true); else PCMP_BNA(1, false, false); }
+  } else {
+    if (relu) { if (mb) PCMP_BNA(2, true, true); else PCMP_BNA(2, true, false); }
+    else { if (mb) PCMP_BNA(2, false, true); else PCMP_BNA(2, false, false); }
+  }
+#undef PCMP_BNA
+  PCMP_LAUNCH_CHECK();
+}
+
+template <int U>
+static void launch_bn_bwd_apply_v2(const __bf16* dy, const __bf16* ym, const __bf16* x, const float* coef, __bf16* dx,
+                                   const __bf16* x2, const float* coef2, __bf16* dx2, __bf16* g, int64_t nvec, int CV,
+                                   hipStream_t st) {
+  const int blocks = ew2_blocks(nvec, U);
+#define PCMP_BBA(M, TW, G)                                                                                       \
+  do {                                                                                                         \
+    if (kn_ew_nt.get())                                                                                        \
+      hipLaunchKernelGGL((bn_bwd_apply_v2_kernel<U, M, TW, G, true>), dim3(blocks), dim3(256), 0, st, dy, ym, x, coef, \
+                         dx, x2, coef2, dx2, g, (int)nvec, CV);                                               \
+    else                                                                                                       \
+      hipLaunchKernelGGL((bn_bwd_apply_v2_kernel<U, M, TW, G, false>), dim3(blocks), dim3(256), 0, st, dy, ym, x,  \
+                         coef, dx, x2, coef2, dx2, g, (int)nvec, CV);                                          \
+  } while (0)
+  const bool m = ym != nullptr, tw = x2 != nullptr, gg = g != nullptr;
+  if (m) {
+    if (tw) { if (gg) PCMP_BBA(true, true, true); else PCMP_BBA(true, true, false); }
+    else { if (gg) PCMP_BBA(true, false, true); else PCMP_BBA(true, false, false); }
+  } else {
+    if (tw) { if (gg) PCMP_BBA(false, true, true); else PCMP_BBA(false, true, false); }
+    else { if (gg) PCMP_BBA(false, false, true); else PCMP_BBA(false, false, false); }
+  }
+#undef PCMP_BBA
+  PCMP_LAUNCH_CHECK();
+}
+
 // ------------------------------------------------------------------------------------------------
 static int rows_per_block_for(int M, const RowMap& rm, int target_blocks = 2048) {
   int rpb = std::max(rm.rpp, ceil_div(M, target_blocks));
@@ -471,6 +682,13 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
                 "bn_apply: mbits must be contiguous uint8 with one byte per 8 elements");
     mb = mbits->data_ptr<uint8_t>();
   }
+  if (ew2_ok(C / 8, nvec)) {
+    const int U = kn_ew_unroll.get();
+    auto f = U >= 8 ? &launch_bn_apply_v2<8> : (U == 2 ? &launch_bn_apply_v2<2> : (U == 1 ? &launch_bn_apply_v2<1> : &launch_bn_apply_v2<4>));
+    f(ptr<__bf16>(x), ptr<float>(scale), ptr<float>(shift), x2p, optr<float>(scale2), optr<float>(shift2),
+      ptr<__bf16>(y), nvec, C / 8, relu, mb, cur_stream());
+    return y;
+  }
   hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
                      ptr<float>(scale), ptr<float>(shift), x2p, optr<float>(scale2), optr<float>(shift2),
                      ptr<__bf16>(y), nvec, C / 8, (int)relu, mb);
@@ -545,6 +763,17 @@ std::vector<at::Tensor> bn_bwd_apply(const at::Tensor& dy, const c10::optional<a
   at::Tensor dx2 = two ? at::empty_like(*x2) : at::Tensor();
   at::Tensor g = want_g ? at::empty_like(dy) : at::Tensor();
   const int64_t nvec = x.numel() / 8;
+  if (ew2_ok(C / 8, nvec)) {
+    const int U = kn_ew_unroll.get();
+    auto f = U >= 8 ? &launch_bn_bwd_apply_v2<8> : (U == 2 ? &launch_bn_bwd_apply_v2<2> : (U == 1 ? &launch_bn_bwd_apply_v2<1> : &launch_bn_bwd_apply_v2<4>));
+    f(ptr<__bf16>(dy), optr<__bf16>(ymask), ptr<__bf16>(x), ptr<float>(coef), ptr<__bf16>(dx),
+      two ? ptr<__bf16>(*x2) : nullptr, optr<float>(coef2), two ? ptr<__bf16>(dx2) : nullptr,
+      want_g ? ptr<__bf16>(g) : nullptr, nvec, C / 8, cur_stream());
+    std::vector<at::Tensor> r{dx};
+    if (two) r.push_back(dx2);
+    if (want_g) r.push_back(g);
+    return r;
+  }
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, cur_stream(), ptr<__bf16>(dy),
                      optr<__bf16>(ymask), ptr<__bf16>(x), ptr<float>(coef), ptr<__bf16>(dx),
                      two ? ptr<__bf16>(*x2) : nullptr, optr<float>(coef2), two ? ptr<__bf16>(dx2) : nullptr,

@@ -12,9 +12,21 @@
 #include <hip/hip_bf16.h>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
+#include <atomic>
 #include <cstdint>
 
 namespace pcmp {
+
+// Runtime tuning knob (kernel-variant switches for in-process A/B measurements, cdna_hip_programming
+// §5.4 rule 24): a named integer, registered at static-initialisation time, read with one relaxed
+// atomic load per launch, set from Python with torch.ops.pcmp.set_knob(name, value).  The default
+// is the measured-best variant; nothing in a training step changes a knob.
+struct Knob {
+  const char* name;
+  std::atomic<int> value;
+  Knob(const char* n, int dflt);
+  int get() const { return value.load(std::memory_order_relaxed); }
+};
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

@@ -12,6 +12,10 @@
 //     with zero channel padding to a multiple of 8 (the stem conv's MFMA K granularity)
 #include "common.h"
 
+#include <mutex>
+#include <string>
+#include <vector>
+
 namespace pcmp {
 
 __device__ __forceinline__ void ld8(const __bf16* p, float* v) {
@@ -667,7 +671,38 @@ at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c1
 
 }  // namespace pcmp
 
+namespace pcmp {
+static std::vector<Knob*>& knob_registry() {
+  static std::vector<Knob*> r;
+  return r;
+}
+static std::mutex& knob_mutex() {
+  static std::mutex m;
+  return m;
+}
+Knob::Knob(const char* n, int dflt) : name(n), value(dflt) {
+  std::lock_guard<std::mutex> g(knob_mutex());
+  knob_registry().push_back(this);
+}
+// returns the previous value; unknown names raise
+int64_t set_knob(const std::string& name, int64_t v) {
+  std::lock_guard<std::mutex> g(knob_mutex());
+  for (Knob* k : knob_registry())
+    if (name == k->name) return k->value.exchange((int)v);
+  TORCH_CHECK(false, "set_knob: unknown knob ", name);
+  return 0;
+}
+std::vector<std::string> list_knobs() {
+  std::lock_guard<std::mutex> g(knob_mutex());
+  std::vector<std::string> r;
+  for (Knob* k : knob_registry()) r.push_back(std::string(k->name) + "=" + std::to_string(k->get()));
+  return r;
+}
+}  // namespace pcmp
+
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("set_knob(str name, int value) -> int", &pcmp::set_knob);
+  m.def("list_knobs() -> str[]", &pcmp::list_knobs);
   m.def("maxpool_fwd(Tensor x, int k, int s, int pad, bool want_idx, Tensor? scale=None, Tensor? shift=None) -> Tensor[]",
         &pcmp::maxpool_fwd);
   m.def("maxpool_bwd_bnr(Tensor dy, Tensor idx, Tensor cx, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, "

@@ -797,10 +797,16 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
   const int wr = wid / WN, wc = wid % WN;
 
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int tile_n = lin % p.tiles_n;
-  const int tile_m = lin / p.tiles_n;
+  // split-K (plain GEMMs with too few tiles to fill the chip): consecutive blocks on one XCD take
+  // the splits of one tile; each split writes raw fp32 partials reduced by splitk_epilogue_kernel
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = lin / tiles_mn;
+  const int tl = lin - split * tiles_mn;
+  const int tile_n = tl % p.tiles_n;
+  const int tile_m = tl / p.tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int nk = (p.gk + BK - 1) / BK;
+  const int kbeg = split * p.ksplit;
+  const int nk = (min(p.gk, kbeg + p.ksplit) - kbeg) / BK;
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -859,7 +865,8 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
 
   // uniform tap / channel state of the next K-tile to load (C or K is a multiple of BK)
   const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
-  int kr = 0, ks = 0, kc = 0, k0 = 0;
+  int kc = kbeg % CIN, k0 = kbeg;
+  int ks = (kbeg / CIN) % p.S, kr = (kbeg / CIN) / p.S;
   auto issue_a = [&](int mh, int buf) {
     int tap;
     if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
@@ -957,7 +964,7 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
     if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A0(t+1), B0(t+1)
     lds_barrier();
   }
-  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR>(p, acc, smem, tid, m0, n0, tile_m, 0);
+  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR>(p, acc, smem, tid, m0, n0, tile_m, split);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -982,27 +989,79 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
   }
 }
 
-// split-K forward reduction + fused epilogue: out = act(sum_s ws[s] + bias (+ resid)) as bf16
-__global__ void splitk_epilogue_kernel(const float* __restrict__ ws, __bf16* __restrict__ out,
-                                       const float* __restrict__ bias, const __bf16* __restrict__ resid,
-                                       int64_t n, int gn, int nsplit, int relu) {
-  const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    f32x4 s = reinterpret_cast<const f32x4*>(ws)[i];
-    for (int k = 1; k < nsplit; ++k) s += reinterpret_cast<const f32x4*>(ws + (size_t)k * n)[i];
-    const int c = (int)((i * 4) % gn);
-    u16x4 rv, ov;
-    if (resid) rv = reinterpret_cast<const u16x4*>(resid)[i];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x = s[e] + (bias ? bias[c + e] : 0.f);
-      if (resid) x += bf2f(rv[e]);
-      if (relu) x = fmaxf(x, 0.f);
-      ov[e] = f2bf(x);
+// split-K reduction v2: the split dimension is spread over SL thread lanes of a block as well
+// (COLS = 256/SL float4 columns per block), so a reduction of few columns over many splits (WGRAD
+// of a 64x576 filter over 256 splits: 36 blocks of 256 threads in v1, each walking all 256 slabs
+// serially) runs on SL x more workgroups with SL x shorter dependent chains.  Each lane sums its
+// splits l, l+SL, ... in groups of four ((a+b)+(c+d)); the lanes are combined in lane order through
+// LDS -- a fixed order for a given split count, so results are run-to-run deterministic.
+template <int SL>
+__global__ void __launch_bounds__(256) splitk_reduce2_kernel(const float* __restrict__ ws, float* __restrict__ dst,
+                                                             int n4, int nsplit, int accumulate) {
+  constexpr int COLS = 256 / SL;
+  __shared__ f32x4 sh[SL][COLS];
+  const int c = threadIdx.x % COLS, l = threadIdx.x / COLS;
+  const int col = blockIdx.x * COLS + c;
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (col < n4) {
+    int k = l;
+    for (; k + 3 * SL < nsplit; k += 4 * SL) {
+      const f32x4 a = w4[(size_t)k * n4 + col], b = w4[(size_t)(k + SL) * n4 + col];
+      const f32x4 cc = w4[(size_t)(k + 2 * SL) * n4 + col], d = w4[(size_t)(k + 3 * SL) * n4 + col];
+      s += (a + b) + (cc + d);
     }
-    reinterpret_cast<u16x4*>(out)[i] = ov;
+    for (; k < nsplit; k += SL) s += w4[(size_t)k * n4 + col];
   }
+  if constexpr (SL == 1) {
+    if (col < n4) {
+      if (accumulate) s += reinterpret_cast<f32x4*>(dst)[col];
+      reinterpret_cast<f32x4*>(dst)[col] = s;
+    }
+    return;
+  } else {
+    sh[l][c] = s;
+    __syncthreads();
+    if (l == 0 && col < n4) {
+      f32x4 t = sh[0][c];
+#pragma unroll
+      for (int j = 1; j < SL; ++j) t += sh[j][c];
+      if (accumulate) t += reinterpret_cast<f32x4*>(dst)[col];
+      reinterpret_cast<f32x4*>(dst)[col] = t;
+    }
+  }
+}
+
+// split-K forward reduction + fused epilogue: out = act(sum_s ws[s] + bias (+ resid)) as bf16
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float* __restrict__ ws, __bf16* __restrict__ out,
+                                                              const float* __restrict__ bias,
+                                                              const __bf16* __restrict__ resid, int64_t n, int gn,
+                                                              int nsplit, int relu) {
+  // one float4 column per thread over a grid that covers the output (the layout of the BN apply
+  // kernels, profiles/r2_ew_apply_ab.txt); the split slabs are read four at a time
+  const int64_t n4 = n >> 2;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
+  f32x4 s = w4[i];
+  int k = 1;
+  for (; k + 3 < nsplit; k += 4) {
+    const f32x4 a = w4[(size_t)k * n4 + i], b = w4[(size_t)(k + 1) * n4 + i];
+    const f32x4 c = w4[(size_t)(k + 2) * n4 + i], d = w4[(size_t)(k + 3) * n4 + i];
+    s += (a + b) + (c + d);
+  }
+  for (; k < nsplit; ++k) s += w4[(size_t)k * n4 + i];
+  const int c = (int)((i * 4) % gn);
+  u16x4 rv, ov;
+  if (resid) rv = reinterpret_cast<const u16x4*>(resid)[i];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float x = s[e] + (bias ? bias[c + e] : 0.f);
+    if (resid) x += bf2f(rv[e]);
+    if (relu) x = fmaxf(x, 0.f);
+    ov[e] = f2bf(x);
+  }
+  reinterpret_cast<u16x4*>(out)[i] = ov;
 }
 
 // weight transpose for DGRAD: wt[c][t][k] = w[k][r(t)][s(t)][c]  (bf16), taps t over a
@@ -1103,6 +1162,10 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
+// A/B knobs (torch.ops.pcmp.set_knob; tools/gemm_knob_ab.py)
+static Knob kn_splitk_red("splitk_red_v", 2);   // WGRAD split-K reduction: 1 = v1 column-only grid, 2 = split lanes
+static Knob kn_shortk_bm64("shortk_bm64", 0);   // FWD/DGRAD with gk <= N: 64x128 register-staged tiles (0 = off)
+
 static int igemm8_mode() {
   static const int v = [] {
     const char* e = std::getenv("PCMP_IGEMM8");
@@ -1125,9 +1188,10 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
   TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_dma: partial-stats buffer too small");
-  TORCH_CHECK(p.nsplit == 1 && p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0,
-              "igemm_dma: needs the block-uniform tap walk and no split-K");
-  const int grid = p.tiles_m * p.tiles_n;
+  TORCH_CHECK(p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0 && p.ksplit % BK == 0,
+              "igemm_dma: needs the block-uniform tap walk");
+  TORCH_CHECK(p.nsplit == 1 || (!p.stats && !p.bn_x), "igemm_dma: split-K only with the plain epilogue");
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
   size_t smem = (size_t)2 * (BM + BN) * BK * 2;
   const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
   if (epi_red) {
@@ -1243,8 +1307,9 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
     const char* e = std::getenv("PCMP_BM64_SMALLGRID");
     return e ? std::atoi(e) : 1;
   }();
-  return v && mode != MODE_WGRAD && p.nsplit == 1 && p.gm > 64 && p.gn > 64 &&
-         ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
+  if (!(mode != MODE_WGRAD && p.nsplit == 1 && p.gm > 64 && p.gn > 64)) return false;
+  if (kn_shortk_bm64.get() > 0 && p.gk <= kn_shortk_bm64.get()) return true;
+  return v && ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
 }
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
@@ -1286,6 +1351,116 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
     else launch_cfg<MODE, 128, 128, 2, 2>(p, st);
   }
 }
+
+
+// ------------------------------------------------------------------------------------------------
+// Plain-GEMM planner: a stride-1 1x1 convolution without a BatchNorm epilogue is a plain GEMM
+// (every Linear layer: BERT-base's M = 4096-token projections, the VGG16 classifier, the transfer
+// heads).  Those shapes have too few 128x128 / 256x256 tiles to fill 256 CUs (BERT's N = 768
+// outputs: 48 tiles of 256x256), so the first call of each shape times a small candidate set --
+// the 4-wave LDS-DMA kernel (128x128, 2 blocks/CU) and the 8-wave one (256x256, 1 block/CU), each
+// with 1..6 K-splits whose fp32 partials are reduced by splitk_epilogue_kernel (bias / residual /
+// ReLU fused there) -- and caches the fastest (cudnn.benchmark-style; never while a graph is being
+// captured).  This replaces the round-1 hipBLASLt candidate for these GEMMs.
+static Knob kn_gemm_plan("gemm_plan", 1);   // 0 = default dispatch only, 1 = autotuned plan
+
+struct GemmPlan {
+  int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves)
+  int nsplit;
+};
+
+template <int MODE>
+static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
+  const int ksteps = p.gk / BK;
+  int nsplit = std::max(1, pl.nsplit);
+  const int steps_per = ceil_div(ksteps, nsplit);
+  nsplit = ceil_div(ksteps, steps_per);
+  p.nsplit = nsplit;
+  p.ksplit = steps_per * BK;
+  const __bf16* resid = p.resid;
+  at::Tensor ws;
+  if (nsplit > 1) {
+    ws = at::empty({(int64_t)nsplit, (int64_t)p.gm * p.gn}, fopts);
+    p.out = ws.data_ptr();
+  } else {
+    p.out = out;
+  }
+  if (pl.kind == 1) launch_dma<MODE, 128, 128, 2, 2, NT, 2>(p, st);
+  else if (pl.kind == 2) launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st);
+  else dispatch<MODE>(p, st);
+  if (nsplit > 1) {
+    const int64_t n = (int64_t)p.gm * p.gn;
+    const int blocks = (int)((n / 4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out,
+                       MODE == MODE_FWD ? p.bias : nullptr, resid, n, p.gn, nsplit, p.relu);
+    PCMP_LAUNCH_CHECK();
+  }
+}
+
+template <int MODE>
+static bool plain_gemm_eligible(const IgemmParams& p) {
+  const int cin = MODE == MODE_FWD ? p.C : p.K;
+  return kn_gemm_plan.get() && p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0 && !p.stats && !p.bn_x &&
+         p.gm >= 1024 && p.gk % BK == 0 && cin % BK == 0 && p.gn % 8 == 0 && p.gk / BK >= 4;
+}
+
+static std::mutex g_plan_mu;
+static std::unordered_map<std::string, GemmPlan> g_plan_cache;
+
+// "mode,gm,gn,gk,bias,resid,relu -> kind/nsplit" for every planned shape (reports, tests)
+std::vector<std::string> gemm_plans() {
+  std::lock_guard<std::mutex> g(g_plan_mu);
+  std::vector<std::string> r;
+  for (auto& kv : g_plan_cache)
+    r.push_back(kv.first + " -> " + (kv.second.kind == 2 ? "dma256x256" : kv.second.kind == 1 ? "dma128x128" : "default") +
+                "/split" + std::to_string(kv.second.nsplit));
+  return r;
+}
+
+template <int MODE>
+static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
+  auto& mu = g_plan_mu;
+  auto& cache = g_plan_cache;
+  char key[128];
+  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d", MODE, p.gm, p.gn, p.gk, p.bias != nullptr, p.resid != nullptr,
+           p.relu);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  GemmPlan dflt{0, 1};
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
+  const int ksteps = p.gk / BK;
+  std::vector<GemmPlan> cands{dflt};
+  for (int ns : {1, 2, 3, 4, 6}) {
+    if (ns > 1 && ksteps / ns < 4) continue;
+    cands.push_back({1, ns});
+    if (p.gn >= 256) cands.push_back({2, ns});
+  }
+  hipEvent_t e0, e1;
+  PCMP_HIP_CHECK(hipEventCreate(&e0));
+  PCMP_HIP_CHECK(hipEventCreate(&e1));
+  GemmPlan best = dflt;
+  float best_ms = 1e30f;
+  for (const GemmPlan& c : cands) {
+    run_plan<MODE>(p, c, out, fopts, st);   // warm (workspace allocation)
+    PCMP_HIP_CHECK(hipEventRecord(e0, st));
+    for (int r = 0; r < 3; ++r) run_plan<MODE>(p, c, out, fopts, st);
+    PCMP_HIP_CHECK(hipEventRecord(e1, st));
+    PCMP_HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    PCMP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (ms < best_ms) { best_ms = ms; best = c; }
+  }
+  PCMP_HIP_CHECK(hipEventDestroy(e0));
+  PCMP_HIP_CHECK(hipEventDestroy(e1));
+  std::lock_guard<std::mutex> g(mu);
+  cache.emplace(key, best);
+  return best;
+}
+
 
 static unsigned tensor_bytes(const at::Tensor& t) {
   const int64_t b = t.numel() * t.element_size();
@@ -1348,6 +1523,11 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
     p.stats = ptr<float>(stats);
   }
   auto st = cur_stream();
+  if (plain_gemm_eligible<MODE_FWD>(p)) {
+    const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
+    run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
+    return {y};
+  }
   // Small-M shapes (batch-1 inference: 49..3136 pixels) leave most of the 256 CUs idle; split the
   // reduction so the grid reaches ~256 workgroups, then reduce + epilogue in one pass.
   const int tiles = ceil_div(p.gm, BMsel) * ceil_div(p.gn, BNsel);
@@ -1367,7 +1547,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
     auto ws = at::empty({(int64_t)nsplit, n}, x.options().dtype(at::kFloat));
     p.out = ws.data_ptr();
     dispatch<MODE_FWD>(p, st);
-    const int blocks = (int)std::min<int64_t>(1024, (n / 4 + 255) / 256);
+    const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<__bf16>(y),
                        p.bias, p.resid, n, p.gn, nsplit, (int)relu);
     PCMP_LAUNCH_CHECK();
@@ -1514,6 +1694,11 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(wt);
   if (has_res) p.resid = ptr<__bf16>(*resid);
   p.ksplit = p.gk;
+  if (!bn && plain_gemm_eligible<MODE_DGRAD>(p)) {
+    const GemmPlan pl = plan_gemm<MODE_DGRAD>(p, ptr<__bf16>(dx), fopts, st);
+    run_plan<MODE_DGRAD>(p, pl, ptr<__bf16>(dx), fopts, st);
+    return {dx};
+  }
   at::Tensor part, part2;
   if (bn) {
     set_bn(p);   // before igemm_bm: the kernel choice depends on the epilogue variant
@@ -1598,6 +1783,17 @@ static void wgrad_run(IgemmParams p, int nsplit, float* out, bool accumulate, co
   auto ws = at::empty({(int64_t)nsplit, n}, fopts);
   p.out = ws.data_ptr();
   dispatch<MODE_WGRAD>(p, st);
+  if (kn_splitk_red.get() == 2 && n / 4 < (1ll << 31)) {
+    const int n4 = (int)(n / 4);
+    const int SL = nsplit <= 8 ? 1 : (nsplit <= 32 ? 4 : 16);
+    const int cols = 256 / SL;
+    const dim3 grid(ceil_div(n4, cols));
+    if (SL == 1) hipLaunchKernelGGL(splitk_reduce2_kernel<1>, grid, dim3(256), 0, st, ptr<float>(ws), out, n4, nsplit, (int)accumulate);
+    else if (SL == 4) hipLaunchKernelGGL(splitk_reduce2_kernel<4>, grid, dim3(256), 0, st, ptr<float>(ws), out, n4, nsplit, (int)accumulate);
+    else hipLaunchKernelGGL(splitk_reduce2_kernel<16>, grid, dim3(256), 0, st, ptr<float>(ws), out, n4, nsplit, (int)accumulate);
+    PCMP_LAUNCH_CHECK();
+    return;
+  }
   const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out, n, nsplit,
                      (int)accumulate);
@@ -1701,6 +1897,7 @@ void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor&
 }  // namespace pcmp
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("gemm_plans() -> str[]", &pcmp::gemm_plans);
   m.def("wt_transpose_multi(Tensor src, Tensor(a!) dst, Tensor desc, int blocks) -> ()", &pcmp::wt_transpose_multi);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu, bool want_stats) -> Tensor[]",
         &pcmp::conv_fwd);

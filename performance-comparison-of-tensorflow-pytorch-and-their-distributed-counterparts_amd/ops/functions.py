@@ -12,7 +12,6 @@ import itertools
 
 import torch
 
-from . import autotune
 from .kernels import K
 from .params import compute_weight, compute_weight_t, emit_grad
 
@@ -48,19 +47,10 @@ class LinearFn(torch.autograd.Function):
         w = compute_weight(weight, x.dtype)
         b = bias.detach().float() if bias is not None else None
 
-        def ours():
-            return K.conv_fwd(x.reshape(M, 1, 1, Cin), w.reshape(Nout, 1, 1, Cin), 1, 0, b, None, relu,
-                              False)[0].reshape(M, Nout)
-
-        def blas():   # hipBLASLt: plain GEMM + bias epilogue
-            y = torch.addmm(b.to(x.dtype), x, w.t()) if b is not None else torch.mm(x, w.t())
-            return torch.relu_(y) if relu else y
-
-        if x.is_cuda and x.dtype == torch.bfloat16 and \
-                autotune.pick(("linear_fwd", M, Cin, Nout, b is not None, relu), ours, blas) == "blas":
-            y = blas()
-        else:
-            y = ours()
+        # a plain GEMM on the MFMA kernels: torch.ops.pcmp.conv_fwd plans the kernel / K-split per
+        # shape (csrc/igemm.hip plan_gemm); bias and ReLU are fused into the epilogue
+        y = K.conv_fwd(x.reshape(M, 1, 1, Cin), w.reshape(Nout, 1, 1, Cin), 1, 0, b, None, relu,
+                       False)[0].reshape(M, Nout)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(x, y)
             ctx.weight, ctx.bias, ctx.relu = weight, bias, relu
@@ -84,19 +74,8 @@ class LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             w = compute_weight(weight, dy.dtype)
-
-            def ours():
-                return K.conv_dgrad(dy4, w.reshape(Nout, 1, 1, Cin), 1, 1, 1, 0, None,
-                                    compute_weight_t(weight, dy.dtype)).reshape(M, Cin)
-
-            def blas():   # hipBLASLt: dX = dY W
-                return torch.mm(dy, w)
-
-            if dy.is_cuda and dy.dtype == torch.bfloat16 and \
-                    autotune.pick(("linear_dgrad", M, Nout, Cin), ours, blas) == "blas":
-                dx = blas()
-            else:
-                dx = ours()
+            dx = K.conv_dgrad(dy4, w.reshape(Nout, 1, 1, Cin), 1, 1, 1, 0, None,
+                              compute_weight_t(weight, dy.dtype)).reshape(M, Cin)
         return dx, gw, gb, None
 
 

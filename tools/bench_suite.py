@@ -18,6 +18,7 @@ import pcmp  # noqa: E402,F401
 from pcmp.ops import cross_entropy  # noqa: E402
 
 dev = torch.device("cuda")
+HIP_ONLY = os.environ.get("SUITE_HIP_ONLY") == "1"   # skip the stock-PyTorch comparators (clean profiles)
 
 
 def timeit(fn, warmup=3, iters=10):
@@ -165,6 +166,8 @@ def bert_train():
     m = bert_base().to(dev)
     t = timeit(hip_train_step(m, lambda: m(ids, None, mask, y)[0], "adamw", 2e-5, eps=1e-8, clip=1.0))
     emit(bench="bert_train", impl="hip", samples_s=32 / t, ms=t * 1e3, batch=32)
+    if HIP_ONLY:
+        return
     hf = transformers.BertForSequenceClassification(transformers.BertConfig(num_labels=2)).to(dev)
     o = torch.optim.AdamW(hf.parameters(), lr=2e-5, eps=1e-8, fused=True)
 

@@ -15,6 +15,9 @@ def main():
     ap.add_argument("--steps", type=int, default=0, help="steps profiled (prints ms/step)")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--last", type=float, default=0.5, help="trailing fraction of the trace for the idle-gap count")
+    ap.add_argument("--step-kernel", default="sgd_flat",
+                    help="kernel that ends each training step (per-step table over the trailing steps)")
+    ap.add_argument("--last-steps", type=int, default=3, help="steady-state steps for the per-step table (0 = off)")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True)
     if not files:
@@ -33,6 +36,38 @@ def main():
         msg += f" ({tot / 1e6 / a.steps:.2f} ms/step over {a.steps} steps)"
     print(msg)
     gaps(a.dir, a.last)
+    if a.last_steps:
+        per_step(a.dir, a.step_kernel, a.last_steps, a.top)
+
+
+def per_step(d, step_kernel, nsteps, top):
+    """Per-kernel device time per step over the last ``nsteps`` complete steps (delimited by the
+    step-ending kernel), so first-step autotuning and warm-up do not skew the attribution."""
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        return
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    ends = [i for i, r in enumerate(rows) if step_kernel in r[2]]
+    if len(ends) < nsteps + 1:
+        print(f"per-step table: only {len(ends)} '{step_kernel}' kernels in the trace")
+        return
+    win = rows[ends[-nsteps - 1] + 1: ends[-1] + 1]
+    agg = {}
+    for s_, e_, n in win:
+        k = _short(n) if "igemm" not in n else n.split("(")[0].replace("void ", "")
+        t, c = agg.get(k, (0, 0))
+        agg[k] = (t + e_ - s_, c + 1)
+    span = (win[-1][1] - win[0][0]) / nsteps
+    tot = sum(t for t, _ in agg.values()) / nsteps
+    print(f"per step over the last {nsteps} steps: span {span / 1e3:.1f} us, kernel time {tot / 1e3:.1f} us, "
+          f"{len(win) / nsteps:.0f} kernels")
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
+        print(f"  {t / nsteps / 1e3:9.1f} us/step {100 * t / nsteps / tot:5.1f}%  calls/step={c / nsteps:6.1f}  {k[:100]}")
 
 
 def gaps(d, last):
