@@ -92,6 +92,10 @@ struct IgemmParams {
 constexpr int BK = 64;
 constexpr int NT = 256;
 
+// DGRAD + BN-backward-reduce epilogue: register-ring depth of its resid / x / mask loads (2 = one
+// step ahead, round 1; 4 = three steps ahead).  A/B knob (tools/gemm_knob_ab.py).
+static Knob kn_epi_depth("epi_depth", 4);   // measured: profiles/r2_epilogue_depth_ab.txt
+
 // XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // consecutive logical tiles land on the same XCD so they share its L2.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -153,7 +157,41 @@ enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNR = 2, EPI_BNR2 = 3 };
 
 // FWD/DGRAD epilogue shared by the 4-wave and 8-wave kernels.  acc[j][i] holds the D^T fragment of
 // MFMA column tile j (4 output channels, PAIR-permuted) x row tile i (16 pixels).
-template <int MODE, int BM, int BN, int WM, int WN, int EPI, int NTHR>
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// workgroup barrier for LDS data only: raw s_barrier after an explicit lgkmcnt(0) -- unlike
+// __syncthreads() it does not drain LDS-DMA loads still in flight (cdna_hip_programming.md §5)
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_barrier();
+}
+
+// sum over the 16 lanes of a DPP row (quad xor-1, quad xor-2, half-row mirror, row mirror): every
+// lane of the row ends with the row's sum
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm(1,0,3,2)
+  v += dpp_mov<0x4E>(v);    // quad_perm(2,3,0,1)
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  return v;
+}
+
+// SHRED: column sums reduced across the 16 pixel lanes with DPP instead of an LDS transpose, so
+// the epilogue's LDS scratch is only [6][BN] coefficient rows + [WM][NS][BN] partials (smem must
+// then point at a region that no stage buffer uses: the persistent streaming kernel keeps
+// prefetching the next tile into its stage buffers while this epilogue runs).
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int NTHR, int EPD = 2, bool SHRED = false>
 __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&acc)[BN / WN / 16][BM / WM / 16],
                                                   char* smem, int tid, int m0, int n0, int tile_m, int split) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -219,9 +257,10 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       orows[i] = orow;
     }
     // Stores walk (i outer, v inner: the two 64-B halves of a pixel's 128-B channel run are stored
-    // back to back); the resid / mask / x operand loads of step t+1 are issued before the math of
-    // step t (one-deep software pipeline).
-    unsigned rvA[2][NP], mkA[2][NP], xvA[2][NP], xv2A[2][NP], mbA[2];
+    // back to back); the resid / mask / x operand loads of step t+EPD-1 are issued before the math
+    // of step t (an EPD-slot register ring: EPD-1 steps of HBM loads in flight per thread).
+    constexpr int D = EPD;
+    unsigned rvA[D][NP], mkA[D][NP], xvA[D][NP], xv2A[D][NP], mbA[D];
     auto issue = [&](int t, int b) {
       const int i = t / NV, v = t % NV;
       const int m = m0 + wr * WTM + i * 16 + fr;
@@ -248,7 +287,11 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
         if constexpr (bnr2) ldv(xv2A[b], p.bn_x2);
       }
     };
-    if (has_res || bnr) issue(0, 0);
+    if (has_res || bnr) {
+#pragma unroll
+      for (int d = 0; d < D - 1; ++d)
+        if (d < NV * TM) issue(d, d);
+    }
     // per-channel coefficient tables of the tile's BN columns, staged once in LDS (stage buffers
     // are dead; the column-sum scratch that reuses this space is written after a barrier)
     float* ctab = reinterpret_cast<float*>(smem);
@@ -270,7 +313,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           }
         }
       }
-      __syncthreads();
+      if constexpr (SHRED) lds_sync(); else __syncthreads();
     }
     auto ldt = [&](float* d, int tab, int j0) {
 #pragma unroll
@@ -284,8 +327,8 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       const int m = m0 + wr * WTM + i * 16 + fr;
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
-        const int t = i * NV + v, b = t & 1;
-        if ((has_res || bnr) && t + 1 < NV * TM) issue(t + 1, (t + 1) & 1);
+        const int t = i * NV + v, b = t % D;
+        if ((has_res || bnr) && t + D - 1 < NV * TM) issue(t + D - 1, (t + D - 1) % D);
         const int j0 = v * (VW / 4);
         const int n = n0 + chan(j0);
         if (m >= p.gm || n >= p.gn) continue;
@@ -349,12 +392,26 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       }
     }
     if constexpr (stats || bnr) {
+      float* red;   // [WM][NS][BN] per-wave-row partial column sums
+      if constexpr (SHRED) {
+        red = reinterpret_cast<float*>(smem) + 6 * BN;   // after the coefficient rows
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = row16_sum(sm[k][j][e]);
+            if (fr == 0) *reinterpret_cast<f32x4*>(red + (wr * NS + k) * BN + chan(j)) = v;
+          }
+        lds_sync();
+      } else {
       // Column sums over the tile's pixels: each wave transposes its lanes' partial sums through
       // LDS ([16 pixel rows][NS][WTN], padded rows) and every lane then sums 16 values for its
       // (k, channel) pairs -- ~3 LDS ops per value instead of a 4-step cross-lane reduction.
       constexpr int RS = NS * WTN + 4;
       float* tb = reinterpret_cast<float*>(smem) + wid * 16 * RS;
-      float* red = reinterpret_cast<float*>(smem) + (NTHR / 64) * 16 * RS;   // [WM][NS][BN]
+      red = reinterpret_cast<float*>(smem) + (NTHR / 64) * 16 * RS;   // [WM][NS][BN]
       __syncthreads();   // stage buffers are dead from here on
 #pragma unroll
       for (int k = 0; k < NS; ++k)
@@ -372,6 +429,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
         red[(wr * NS + k) * BN + wc * WTN + ch] = t;
       }
       __syncthreads();
+      }
       float* st = p.stats + (size_t)tile_m * 2 * p.gn;
       float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
       for (int i = tid; i < BN; i += NTHR) {
@@ -396,7 +454,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI>
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2>
 __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -743,7 +801,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       }
     return;
   } else {
-    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT>(p, acc, smem, tid, m0, n0, tile_m, split);
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
   }
 }
 
@@ -765,17 +823,8 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
 constexpr int NT8 = 512;
 constexpr int BM8 = 256;
 
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
-template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI>
+template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI, int EPD = 2>
 __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams p) {
   constexpr int NW = NTHR / 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -964,7 +1013,169 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
     if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A0(t+1), B0(t+1)
     lds_barrier();
   }
-  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR>(p, acc, smem, tid, m0, n0, tile_m, split);
+  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Persistent streaming kernel for the memory-bound FWD / DGRAD GEMMs (short reductions with
+// write-heavy epilogues: the 1x1 convolutions of ResNet-50 whose outputs and BN operands are
+// 100-400 MB).  The one-tile-per-block kernels expose a full HBM round trip per tile (operand load
+// -> MFMA -> epilogue loads -> stores) at 2-3 resident blocks per CU (tools/dgrad_probe.py: the
+// layer-1 1x1 DGRAD ran at 3.6 TB/s).  Here each block loops over tiles t, t + grid, ... and, as
+// soon as a tile's last K-step has been read from LDS, issues the LDS-DMA loads of the NEXT tile's
+// first two K-steps, which then land while the current tile's epilogue runs.  The epilogue's LDS
+// scratch (BN coefficients + DPP-reduced column partials, SHRED) sits after the two stage buffers,
+// so it never aliases the prefetch.  4 waves (2x2), BK = 64, 2 blocks per CU.
+// K-loop per tile: stage kt lives in buffer kt & 1; s_waitcnt vmcnt counts retire exactly the
+// stage about to be read (NA + NB DMA instructions per stage per wave), then a barrier.
+template <int MODE, int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(NT, 2) igemm_stream_kernel(const IgemmParams p) {
+  constexpr int NW = NT / 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NA = BM / 8 / NW;   // DMA instructions (8 rows each) per wave per A stage
+  constexpr int NB = BN / 8 / NW;
+  constexpr int PER = NA + NB;      // per wave per stage
+  static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
+  static_assert(WM * WN == NW && NA >= 1 && NB >= 1, "tiling");
+  static_assert(WTN % 32 == 0, "PAIR channel permutation works on 32-row groups");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* scratch = smem + 2 * STAGE;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int nk = p.gk / BK;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
+  const int gch = (lane & 7) ^ (lane >> 3);   // source chunk of this lane (XOR-swizzled image)
+
+  // per-tile loader state (rows of this wave's DMA instructions)
+  int a_off[NA], a_y[NA], a_x[NA], b_off[NB];
+  int kr = 0, ks = 0, kc = 0, k0 = 0;      // tap / channel walk of the next stage to issue
+  int ld_tile = -1, ld_k = 0;             // (tile, K-step) of the next stage to issue
+  auto setup = [&](int t) {
+    const int tile_n = t % p.tiles_n, tile_m = t / p.tiles_n;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = m0 + (wid * NA + i) * 8 + (lane >> 3);
+      const bool v = m < p.gm;
+      const int mm = v ? m : 0;
+      if constexpr (MODE == MODE_FWD) {
+        const int n = fdiv(mm, p.fd_PQ);
+        const int rem = mm - n * p.P * p.Q;
+        const int pp = fdiv(rem, p.fd_Q);
+        const int qq = rem - pp * p.Q;
+        const int yv = pp * p.stride - p.pad;
+        a_y[i] = v ? yv : -(1 << 28);
+        a_x[i] = qq * p.stride - p.pad;
+        a_off[i] = ((n * p.H + yv) * p.W + a_x[i]) * p.C + gch * 8;
+      } else {
+        const int n = fdiv(mm, p.fd_HW);
+        const int rem = mm - n * p.dH * p.dW;
+        const int hh = fdiv(rem, p.fd_W);
+        const int ww = rem - hh * p.dW;
+        const int yv = hh + p.offy;
+        a_y[i] = v ? yv : -(1 << 28);
+        a_x[i] = ww + p.offx;
+        a_off[i] = ((n * p.P + yv) * p.Q + a_x[i]) * p.K + gch * 8;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = n0 + chan_perm<true>((wid * NB + i) * 8 + (lane >> 3));
+      b_off[i] = n < p.gn ? n * p.gk + gch * 8 : -1;
+    }
+    kr = ks = kc = k0 = 0;
+    ld_tile = t;
+    ld_k = 0;
+  };
+  auto issue = [&](int buf) {   // DMA the stage (ld_tile, ld_k) into buffer buf, advance the walk
+    char* sA = smem + buf * STAGE;
+    char* sB = sA + A_BYTES;
+    int tap;
+    if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
+    else tap = -(kr * p.Q + ks) * p.K + kc;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      bool ok;
+      if constexpr (MODE == MODE_FWD)
+        ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
+      else
+        ok = (unsigned)(a_y[i] - kr) < (unsigned)p.P && (unsigned)(a_x[i] - ks) < (unsigned)p.Q;
+      const unsigned voff = ok ? (unsigned)(a_off[i] + tap) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(sA + (wid * NA + i) * 1024),
+                                               16, voff, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const unsigned voff = b_off[i] >= 0 ? (unsigned)(b_off[i] + k0) * 2u : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(sB + (wid * NB + i) * 1024),
+                                               16, voff, 0, 0, 0);
+    }
+    k0 += BK;
+    kc += BK;
+    if (kc >= CIN) {
+      kc = 0;
+      if (++ks == p.S) { ks = 0; ++kr; }
+    }
+    ++ld_k;
+  };
+
+  f32x4 acc[TN][TM];
+  int t = blockIdx.x;
+  if (t < tiles) {
+    setup(t);
+    issue(0);
+    if (nk > 1) issue(1);
+  }
+  for (; t < tiles; t += gridDim.x) {
+    const int tile_n = t % p.tiles_n, tile_m = t / p.tiles_n;
+    const int m0 = tile_m * BM, n0 = tile_n * BN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      // retire stage kt: the stage issued after it (kt + 1), if any, may stay in flight
+      if (kt + 1 < nk) wait_vm<PER>(); else wait_vm<0>();
+      lds_barrier();
+      const char* sA = smem + buf * STAGE;
+      const char* sB = sA + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8 fa[TM], fb[TN];
+        const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 16 + (lane & 15), chunk));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_barrier();   // every wave is done reading buffer buf
+      if (kt + 2 < nk) issue(buf);                  // stage kt + 2 of this tile
+    }
+    // next tile's first stages land while this tile's epilogue runs
+    const int tn = t + gridDim.x;
+    if (tn < tiles) {
+      setup(tn);
+      issue(0);
+      if (nk > 1) issue(1);
+    }
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, 2, true>(p, acc, scratch, tid, m0, n0, tile_m, 0);
+  }
+  wait_vm<0>();
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1148,10 +1359,16 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
   } else if constexpr (MODE == MODE_DGRAD) {
+    const bool deep = kn_epi_depth.get() >= 4;
+#define PCMP_IGEMM_LAUNCH_D(U, E) \
+  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, U, E, 4>), dim3(grid), dim3(NT), smem, st, p)
     if (epi == EPI_BNR) {
-      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR); else PCMP_IGEMM_LAUNCH(false, EPI_BNR);
+      if (deep) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR); }
+      else if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR); else PCMP_IGEMM_LAUNCH(false, EPI_BNR);
     } else if (epi == EPI_BNR2) {
-      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH(false, EPI_BNR2);
+      if (deep) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR2); }
+      else if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH(false, EPI_BNR2);
+#undef PCMP_IGEMM_LAUNCH_D
     } else {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
@@ -1203,11 +1420,15 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
 #define PCMP_DMA_LAUNCH(E)                                                                              \
   do {                                                                                                \
-    auto kfn = &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E>;                                \
+    constexpr bool can_deep = (E == EPI_BNR || E == EPI_BNR2) && NTHR == 256;                                        \
+    auto kfn = (can_deep && kn_epi_depth.get() >= 4) ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4> \
+                                                     : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>; \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
-      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
+      for (auto f : {&igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>,                       \
+                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>})                      \
+        PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f),                          \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
       attr_set = true;                                                                                \
     }                                                                                                 \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(NTHR), smem, st, p);                                     \
@@ -1255,6 +1476,61 @@ static int use_dma4(int mode, const IgemmParams& p) {
     return v == 1 ? 2 : (v == 2 ? 3 : 0);
   }
   return 1;
+}
+
+// persistent streaming kernel (FWD/DGRAD, short reductions): grid = min(tiles, kn_stream_grid)
+// Measured (tools/gemm_knob_ab.py, profiles/r2_stream_kernel_ab.txt): the streaming kernel wins only
+// on the wide short-K DGRAD + BN-backward GEMMs (layer-1 256->64 351 -> 343 us, layer-2 512->128
+// 209 -> 203, layer-3 1024->256 130 -> 122) and loses on the FWD + statistics ones (layer-1 64->256
+// 153 -> 185 us), so by default it runs DGRAD with >= 256 output channels and <= 4 K-steps.
+static Knob kn_stream_maxk("stream_maxk", 4);     // use it for gk/BK <= N K-steps (0 = off)
+static Knob kn_stream_fwd("stream_fwd", 0);       // 1: also for FWD
+static Knob kn_stream_grid("stream_grid", 512);   // resident blocks (2 per CU)
+
+template <int MODE, int BM, int BN, int WM, int WN>
+static void launch_stream(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_stream: partial-stats buffer too small");
+  TORCH_CHECK(p.nsplit == 1 && p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0,
+              "igemm_stream: needs the block-uniform tap walk and no split-K");
+  const int tiles = p.tiles_m * p.tiles_n;
+  const int grid = std::max(1, std::min(tiles, kn_stream_grid.get()));
+  const size_t smem = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
+  int epi = EPI_PLAIN;
+  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
+  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
+#define PCMP_STREAM_LAUNCH(E)                                                                          \
+  do {                                                                                                 \
+    auto kfn = &igemm_stream_kernel<MODE, BM, BN, WM, WN, E>;                                          \
+    static bool attr_set = false;                                                                      \
+    if (!attr_set) {                                                                                   \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                           \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));     \
+      attr_set = true;                                                                                 \
+    }                                                                                                  \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p);                                        \
+  } while (0)
+  if constexpr (MODE == MODE_FWD) {
+    if (epi == EPI_STATS) PCMP_STREAM_LAUNCH(EPI_STATS); else PCMP_STREAM_LAUNCH(EPI_PLAIN);
+  } else {
+    if (epi == EPI_BNR) PCMP_STREAM_LAUNCH(EPI_BNR);
+    else if (epi == EPI_BNR2) PCMP_STREAM_LAUNCH(EPI_BNR2);
+    else PCMP_STREAM_LAUNCH(EPI_PLAIN);
+  }
+#undef PCMP_STREAM_LAUNCH
+  PCMP_LAUNCH_CHECK();
+}
+
+// 0: not used; 1: 128x128; 2: 128x64 (narrow outputs)
+static int use_stream(int mode, const IgemmParams& p) {
+  const int mk = kn_stream_maxk.get();
+  if (mk <= 0 || mode == MODE_WGRAD || p.nsplit != 1) return 0;
+  if (mode == MODE_FWD && !kn_stream_fwd.get()) return 0;
+  const int cin = mode == MODE_FWD ? p.C : p.K;
+  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK > mk || p.gm < 4096) return 0;
+  if (mode == MODE_DGRAD && !kn_stream_fwd.get() && p.gn < 256) return 0;
+  return p.gn <= 64 ? 2 : 1;
 }
 
 // 8-wave LDS-DMA kernel eligibility: FWD/DGRAD with the block-uniform tap walk (source channels a
@@ -1314,6 +1590,7 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
 static int igemm_bm(int mode, const IgemmParams& p) {
+  if (use_stream(mode, p)) return 128;
   if (use_igemm8(mode, p)) return BM8;
   if (use_bm64_smallgrid(mode, p)) return 64;
   if (use_dma4(mode, p) == 3) return 256;
@@ -1323,6 +1600,11 @@ static int igemm_bm(int mode, const IgemmParams& p) {
 template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE != MODE_WGRAD) {
+    switch (use_stream(MODE, p)) {
+      case 1: launch_stream<MODE, 128, 128, 2, 2>(p, st); return;
+      case 2: launch_stream<MODE, 128, 64, 2, 2>(p, st); return;
+      default: break;
+    }
     if (use_igemm8(MODE, p) == 256) { launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st); return; }
   }
   if constexpr (MODE == MODE_WGRAD) {
