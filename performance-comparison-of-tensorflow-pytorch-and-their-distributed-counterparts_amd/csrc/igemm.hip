@@ -1647,13 +1647,23 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
 static Knob kn_gemm_plan("gemm_plan", 1);   // 0 = default dispatch only, 1 = autotuned plan
 
 struct GemmPlan {
-  int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves)
+  int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves),
+                // 3 = register-staged 64x64, 4 = register-staged 32x64 (small-M inference convs)
   int nsplit;
 };
+static const char* plan_kind_name(int k) {
+  switch (k) {
+    case 1: return "dma128x128";
+    case 2: return "dma256x256";
+    case 3: return "reg64x64";
+    case 4: return "reg32x64";
+    default: return "default";
+  }
+}
 
 template <int MODE>
 static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
-  const int ksteps = p.gk / BK;
+  const int ksteps = ceil_div(p.gk, BK);
   int nsplit = std::max(1, pl.nsplit);
   const int steps_per = ceil_div(ksteps, nsplit);
   nsplit = ceil_div(ksteps, steps_per);
@@ -1669,6 +1679,8 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   }
   if (pl.kind == 1) launch_dma<MODE, 128, 128, 2, 2, NT, 2>(p, st);
   else if (pl.kind == 2) launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st);
+  else if (pl.kind == 3) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
+  else if (pl.kind == 4) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
   else dispatch<MODE>(p, st);
   if (nsplit > 1) {
     const int64_t n = (int64_t)p.gm * p.gn;
@@ -1694,32 +1706,47 @@ std::vector<std::string> gemm_plans() {
   std::lock_guard<std::mutex> g(g_plan_mu);
   std::vector<std::string> r;
   for (auto& kv : g_plan_cache)
-    r.push_back(kv.first + " -> " + (kv.second.kind == 2 ? "dma256x256" : kv.second.kind == 1 ? "dma128x128" : "default") +
-                "/split" + std::to_string(kv.second.nsplit));
+    r.push_back(kv.first + " -> " + plan_kind_name(kv.second.kind) + "/split" + std::to_string(kv.second.nsplit));
   return r;
 }
 
+// small_m: an inference-sized convolution (few output tiles, long reduction): the candidates are
+// the register-staged kernels at 128/64/32-row tiles with 1..32 K-splits (the split partials are
+// reduced by splitk_epilogue_kernel together with bias / residual / ReLU), plus the round-1
+// heuristic (default tile, heur_split splits) so the plan is never a regression by construction.
 template <int MODE>
-static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
+static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOptions& fopts, hipStream_t st,
+                          bool small_m = false, int heur_split = 1) {
   auto& mu = g_plan_mu;
   auto& cache = g_plan_cache;
-  char key[128];
-  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d", MODE, p.gm, p.gn, p.gk, p.bias != nullptr, p.resid != nullptr,
-           p.relu);
+  char key[192];
+  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d|%d,%d,%d,%d,%d,%d,%d,%d,%d", MODE, p.gm, p.gn, p.gk,
+           p.bias != nullptr, p.resid != nullptr, p.relu, p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad);
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
   }
-  GemmPlan dflt{0, 1};
+  GemmPlan dflt{0, small_m ? heur_split : 1};
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
-  const int ksteps = p.gk / BK;
+  const int ksteps = ceil_div(p.gk, BK);
   std::vector<GemmPlan> cands{dflt};
-  for (int ns : {1, 2, 3, 4, 6}) {
-    if (ns > 1 && ksteps / ns < 4) continue;
-    cands.push_back({1, ns});
-    if (p.gn >= 256) cands.push_back({2, ns});
+  if (small_m) {
+    for (int ns : {1, 2, 4, 8, 12, 16, 24, 32}) {
+      if (ns > 1 && ksteps / ns < 2) continue;
+      for (int kind : {0, 3, 4}) {
+        if (kind == 0 && ns == heur_split) continue;
+        if (kind == 4 && p.gm > 256) continue;
+        cands.push_back({kind, ns});
+      }
+    }
+  } else {
+    for (int ns : {1, 2, 3, 4, 6}) {
+      if (ns > 1 && ksteps / ns < 4) continue;
+      cands.push_back({1, ns});
+      if (p.gn >= 256) cands.push_back({2, ns});
+    }
   }
   hipEvent_t e0, e1;
   PCMP_HIP_CHECK(hipEventCreate(&e0));
@@ -1820,6 +1847,11 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   static const int split_mink = [] { const char* e = getenv("PCMP_FWD_SPLIT_MINK"); return e ? std::max(1, atoi(e)) : 4; }();
   if (!want_stats && tiles < 128 && ksteps >= 8)
     nsplit = std::max(1, std::min({ceil_div(split_target, tiles), ksteps / split_mink, 32}));
+  if (!want_stats && tiles < 128 && ksteps >= 8 && kn_gemm_plan.get()) {
+    const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st, true, nsplit);
+    run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
+    return {y};
+  }
   if (nsplit > 1) {
     const int steps_per = ceil_div(ksteps, nsplit);
     nsplit = ceil_div(ksteps, steps_per);

@@ -414,3 +414,29 @@ def test_splitk_fwd_repeated(gpu):
             close(y, yr)
             # bitwise reproducible (fixed split order)
             assert torch.equal(y, _ops().conv_fwd(x, w, 1, p, bias, res, relu, False)[0])
+
+
+def test_planned_inference_convs_match_reference(gpu):
+    """The autotuned small-M FWD plan (kernel tile x K-split, csrc/igemm.hip plan_gemm) on ResNet-50
+    batch-1 shapes (incl. stride 2) matches the reference and the unplanned round-1 path."""
+    torch.manual_seed(1)
+    ops = _ops()
+    shapes = [(56, 64, 64, 3, 1), (28, 128, 128, 3, 1), (56, 128, 128, 3, 2), (14, 1024, 256, 1, 1),
+              (14, 256, 1024, 1, 1), (7, 512, 512, 3, 1), (14, 1024, 2048, 1, 2)]
+    for (H, C, K, R, s) in shapes:
+        p = R // 2
+        x = rnd(1, H, H, C, dev=gpu)
+        w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+        bias = torch.randn(K, device=gpu)
+        yr = ref.conv_fwd(x, w, s, p, bias, None, True, False)[0]
+        ops.set_knob("gemm_plan", 0)
+        try:
+            y0 = ops.conv_fwd(x, w, s, p, bias, None, True, False)[0]
+        finally:
+            ops.set_knob("gemm_plan", 1)
+        y1 = ops.conv_fwd(x, w, s, p, bias, None, True, False)[0]
+        close(y0, yr)
+        close(y1, yr)
+        assert torch.equal(y1, ops.conv_fwd(x, w, s, p, bias, None, True, False)[0])   # cached plan, fixed order
+    plans = ops.gemm_plans()
+    assert any("|1," in k for k in plans), plans   # batch-1 geometry keys were planned
