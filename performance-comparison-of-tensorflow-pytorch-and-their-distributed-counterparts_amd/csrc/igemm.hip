@@ -1179,6 +1179,132 @@ __global__ void __launch_bounds__(NT, 2) igemm_stream_kernel(const IgemmParams p
 }
 
 // ------------------------------------------------------------------------------------------------
+// Skinny FWD kernel for batch-1 inference (M = output pixels <= a few hundred: ResNet-50 layer 3/4
+// and the classifier at batch 1).  Those GEMMs are latency-bound: a block has only a few K-steps
+// of tiny MFMA work, so what matters is how many operand loads are in flight, not data reuse.  No
+// LDS and no barriers: every lane loads its MFMA fragments straight from global memory into
+// registers (16-B buffer loads, hardware zero-fill for padding / tails) in fragment layout, and a
+// ring of PF K32-steps of loads stays in flight (the register-staged kernels keep one K-step).
+// Block = 4 waves, tile 64 pixels x 64 output channels; wave w owns channels 16w..16w+15 for all 64
+// pixels (4 MFMA fragments); D^T = W * X^T so each lane ends with 4 consecutive channels of one
+// pixel.  The split index is blockIdx.y-major; splits > 1 write fp32 partials for
+// splitk_epilogue_kernel, one split writes bf16 act(acc + bias (+ resid)).
+// Requires C % 32 == 0 (a K32 step never straddles a filter tap).
+template <int PF>
+__global__ void __launch_bounds__(NT, 2) skinny_fwd_kernel(const IgemmParams p) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = blockIdx.x / tiles_mn;
+  const int tl = blockIdx.x - split * tiles_mn;
+  const int tile_n = tl % p.tiles_n, tile_m = tl / p.tiles_n;
+  const int m0 = tile_m * 64, n0 = tile_n * 64 + wid * 16;
+  const int kbeg = split * p.ksplit;
+  const int kend = min(p.gk, kbeg + p.ksplit);
+  const int nsteps = (kend - kbeg) / 32;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+  // per-fragment pixel geometry (pixel m0 + 16i + fr)
+  int a_base[4], a_y[4], a_x[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + 16 * i + fr;
+    const bool v = m < p.gm;
+    const int mm = v ? m : 0;
+    const int n = fdiv(mm, p.fd_PQ);
+    const int rem = mm - n * p.P * p.Q;
+    const int pp = fdiv(rem, p.fd_Q);
+    const int qq = rem - pp * p.Q;
+    a_y[i] = v ? pp * p.stride - p.pad : -(1 << 28);
+    a_x[i] = qq * p.stride - p.pad;
+    a_base[i] = ((n * p.H + a_y[i]) * p.W + a_x[i]) * p.C + fq * 8;
+  }
+  const int nrow = n0 + fr;
+  const int b_base = nrow < p.gn ? nrow * p.gk + fq * 8 : -1;
+  // tap walk of the next K32 step to issue
+  int kc = kbeg % p.C, ks = (kbeg / p.C) % p.S, kr = (kbeg / p.C) / p.S, kk = kbeg;
+  uint4 ra[PF][4], rb[PF];
+  auto issue = [&](int slot) {
+    const int tap = (kr * p.W + ks) * p.C + kc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
+      ra[slot][i] = bload16(rsA, ok ? (unsigned)(a_base[i] + tap) * 2u : kOOB);
+    }
+    rb[slot] = bload16(rsB, b_base >= 0 ? (unsigned)(b_base + kk) * 2u : kOOB);
+    kk += 32;
+    kc += 32;
+    if (kc >= p.C) {
+      kc = 0;
+      if (++ks == p.S) { ks = 0; ++kr; }
+    }
+  };
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nsteps) issue(u);
+  for (int s0 = 0; s0 < nsteps; s0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      if (s0 + u >= nsteps) break;
+      const bf16x8 fb = __builtin_bit_cast(bf16x8, rb[u]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, __builtin_bit_cast(bf16x8, ra[u][i]), acc[i], 0, 0, 0);
+      if (s0 + u + PF < nsteps) issue(u);
+    }
+  }
+  // epilogue: lane holds channels n0 + 4 fq .. +3 of pixels m0 + 16 i + fr
+  const int n = n0 + 4 * fq;
+  if (n >= p.gn) return;
+  if (p.nsplit > 1) {
+    float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + 16 * i + fr;
+      if (m < p.gm) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[i];
+    }
+    return;
+  }
+  __bf16* out = reinterpret_cast<__bf16*>(p.out);
+  float bias[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[e] = p.bias[n + e];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + 16 * i + fr;
+    if (m >= p.gm) continue;
+    const size_t o = (size_t)m * p.gn + n;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = acc[i][e] + bias[e];
+    if (p.resid) {
+      const uint2 r = *reinterpret_cast<const uint2*>(p.resid + o);
+      v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
+      v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    *reinterpret_cast<uint2*>(out + o) = uint2{f2bf2(v[0], v[1]), f2bf2(v[2], v[3])};
+  }
+}
+
+static void launch_skinny(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, 64);
+  p.tiles_n = ceil_div(p.gn, 64);
+  TORCH_CHECK(p.C % 32 == 0 && p.ksplit % 32 == 0 && p.gn % 4 == 0, "skinny_fwd: C, ksplit multiples of 32");
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  hipLaunchKernelGGL(skinny_fwd_kernel<8>, dim3(grid), dim3(NT), 0, st, p);
+  PCMP_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------------
 // split-K reduction: dst[i] (+)= sum_s ws[s][i]   (fp32, float4)
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ dst,
                                      int64_t n, int nsplit, int accumulate) {
@@ -1645,10 +1771,11 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
 // ReLU fused there) -- and caches the fastest (cudnn.benchmark-style; never while a graph is being
 // captured).  This replaces the round-1 hipBLASLt candidate for these GEMMs.
 static Knob kn_gemm_plan("gemm_plan", 1);   // 0 = default dispatch only, 1 = autotuned plan
+static Knob kn_plan_force("plan_force", -1); // tests: >= 0 restricts the candidates to that kind (uncached)
 
 struct GemmPlan {
   int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves),
-                // 3 = register-staged 64x64, 4 = register-staged 32x64 (small-M inference convs)
+                // 3 = register-staged 64x64, 4 = register-staged 32x64, 5 = DMA 128x64 (small-M inference convs)
   int nsplit;
 };
 static const char* plan_kind_name(int k) {
@@ -1657,18 +1784,21 @@ static const char* plan_kind_name(int k) {
     case 2: return "dma256x256";
     case 3: return "reg64x64";
     case 4: return "reg32x64";
+    case 5: return "dma128x64";
+    case 6: return "skinny64x64";
     default: return "default";
   }
 }
 
 template <int MODE>
 static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
-  const int ksteps = ceil_div(p.gk, BK);
+  const int kq = pl.kind == 6 ? 32 : BK;   // K granularity of the kernel
+  const int ksteps = ceil_div(p.gk, kq);
   int nsplit = std::max(1, pl.nsplit);
   const int steps_per = ceil_div(ksteps, nsplit);
   nsplit = ceil_div(ksteps, steps_per);
   p.nsplit = nsplit;
-  p.ksplit = steps_per * BK;
+  p.ksplit = steps_per * kq;
   const __bf16* resid = p.resid;
   at::Tensor ws;
   if (nsplit > 1) {
@@ -1681,7 +1811,11 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   else if (pl.kind == 2) launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st);
   else if (pl.kind == 3) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
   else if (pl.kind == 4) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
-  else dispatch<MODE>(p, st);
+  else if (pl.kind == 5) launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st);
+  else if (pl.kind == 6) {
+    if constexpr (MODE == MODE_FWD) launch_skinny(p, st);
+    else TORCH_CHECK(false, "skinny kernel is FWD only");
+  } else dispatch<MODE>(p, st);
   if (nsplit > 1) {
     const int64_t n = (int64_t)p.gm * p.gn;
     const int blocks = (int)((n / 4 + 255) / 256);
@@ -1700,6 +1834,7 @@ static bool plain_gemm_eligible(const IgemmParams& p) {
 
 static std::mutex g_plan_mu;
 static std::unordered_map<std::string, GemmPlan> g_plan_cache;
+static std::vector<std::string>* g_plan_log = nullptr;   // candidate timings (plan_candidates op)
 
 // "mode,gm,gn,gk,bias,resid,relu -> kind/nsplit" for every planned shape (reports, tests)
 std::vector<std::string> gemm_plans() {
@@ -1722,7 +1857,8 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
   char key[192];
   snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d|%d,%d,%d,%d,%d,%d,%d,%d,%d", MODE, p.gm, p.gn, p.gk,
            p.bias != nullptr, p.resid != nullptr, p.relu, p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad);
-  {
+  const int force = kn_plan_force.get();
+  if (force < 0) {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
@@ -1733,13 +1869,23 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
   const int ksteps = ceil_div(p.gk, BK);
   std::vector<GemmPlan> cands{dflt};
   if (small_m) {
+    // the LDS-DMA kernels keep 2-3 half-tiles of operands in flight (the register-staged ones one
+    // K-step), which matters when a block's few K-steps are latency-bound; they need the
+    // block-uniform tap walk
+    const int cin = MODE == MODE_FWD ? p.C : p.K;
+    const bool dma_ok = p.gk % BK == 0 && cin % BK == 0;
     for (int ns : {1, 2, 4, 8, 12, 16, 24, 32}) {
       if (ns > 1 && ksteps / ns < 2) continue;
-      for (int kind : {0, 3, 4}) {
+      for (int kind : {0, 3, 4, 1, 5}) {
         if (kind == 0 && ns == heur_split) continue;
         if (kind == 4 && p.gm > 256) continue;
+        if ((kind == 1 || kind == 5) && (!dma_ok || ceil_div(ksteps, ns) < 2)) continue;
+        if (kind == 5 && p.gn > 1024) continue;
         cands.push_back({kind, ns});
       }
+      if (MODE == MODE_FWD && p.C % 32 == 0 && p.gk % 32 == 0 && p.gn % 4 == 0 && p.gm <= 1024 &&
+          p.gk / 32 / ns >= 2)
+        cands.push_back({6, ns});
     }
   } else {
     for (int ns : {1, 2, 3, 4, 6}) {
@@ -1748,10 +1894,16 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
       if (p.gn >= 256) cands.push_back({2, ns});
     }
   }
+  if (force >= 0) {
+    std::vector<GemmPlan> f;
+    for (const GemmPlan& c : cands)
+      if (c.kind == force) f.push_back(c);
+    if (!f.empty()) cands = f;
+  }
   hipEvent_t e0, e1;
   PCMP_HIP_CHECK(hipEventCreate(&e0));
   PCMP_HIP_CHECK(hipEventCreate(&e1));
-  GemmPlan best = dflt;
+  GemmPlan best = cands[0];
   float best_ms = 1e30f;
   for (const GemmPlan& c : cands) {
     run_plan<MODE>(p, c, out, fopts, st);   // warm (workspace allocation)
@@ -1762,14 +1914,42 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
     float ms = 0.f;
     PCMP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
     if (ms < best_ms) { best_ms = ms; best = c; }
+    if (g_plan_log) g_plan_log->push_back(std::string(plan_kind_name(c.kind)) + "/split" + std::to_string(c.nsplit) +
+                                          " " + std::to_string(ms / 3 * 1000.f) + "us");
   }
   PCMP_HIP_CHECK(hipEventDestroy(e0));
   PCMP_HIP_CHECK(hipEventDestroy(e1));
+  if (force >= 0) return best;
   std::lock_guard<std::mutex> g(mu);
   cache.emplace(key, best);
   return best;
 }
 
+
+static unsigned tensor_bytes(const at::Tensor& t);
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias,
+                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats);
+
+// Timings of every planner candidate for one conv_fwd call (reports / kernel tuning): runs the
+// planner uncached with its log enabled.
+std::vector<std::string> plan_candidates(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                         const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
+                                         bool relu) {
+  std::vector<std::string> log;
+  const int old = kn_plan_force.value.exchange(99);   // 99: no such kind -> every candidate, uncached
+  g_plan_log = &log;
+  try {
+    conv_fwd(x, w, stride, pad, bias, resid, relu, false);
+  } catch (...) {
+    g_plan_log = nullptr;
+    kn_plan_force.value.store(old);
+    throw;
+  }
+  g_plan_log = nullptr;
+  kn_plan_force.value.store(old);
+  return log;
+}
 
 static unsigned tensor_bytes(const at::Tensor& t) {
   const int64_t b = t.numel() * t.element_size();
@@ -2212,6 +2392,8 @@ void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor&
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("gemm_plans() -> str[]", &pcmp::gemm_plans);
+  m.def("plan_candidates(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu) -> str[]",
+        &pcmp::plan_candidates);
   m.def("wt_transpose_multi(Tensor src, Tensor(a!) dst, Tensor desc, int blocks) -> ()", &pcmp::wt_transpose_multi);
   m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu, bool want_stats) -> Tensor[]",
         &pcmp::conv_fwd);

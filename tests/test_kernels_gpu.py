@@ -440,3 +440,28 @@ def test_planned_inference_convs_match_reference(gpu):
         assert torch.equal(y1, ops.conv_fwd(x, w, s, p, bias, None, True, False)[0])   # cached plan, fixed order
     plans = ops.gemm_plans()
     assert any("|1," in k for k in plans), plans   # batch-1 geometry keys were planned
+
+
+@pytest.mark.parametrize("kind", [3, 4, 6])
+def test_small_m_plan_kinds_match_reference(gpu, kind):
+    """Each small-M candidate kernel (register 64x64 / 32x64, skinny register-direct) forced through
+    the planner, with and without K-splits (the planner times 1..32 splits), vs the fp32 reference;
+    bias + residual + ReLU epilogues, batch-1 layer-3/4 shapes incl. stride 2 and the classifier."""
+    torch.manual_seed(2)
+    ops = _ops()
+    ops.set_knob("plan_force", kind)
+    try:
+        for (H, C, K, R, s, use_res) in [(14, 256, 256, 3, 1, False), (14, 256, 256, 3, 2, False),
+                                         (7, 2048, 512, 1, 1, False), (7, 512, 2048, 1, 1, True),
+                                         (1, 2048, 1000, 1, 1, False), (14, 1024, 256, 1, 1, False)]:
+            p = R // 2
+            x = rnd(1, H, H, C, dev=gpu)
+            w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+            bias = torch.randn(K, device=gpu)
+            Ho = (H + 2 * p - R) // s + 1
+            res = rnd(1, Ho, Ho, K, dev=gpu) if use_res else None
+            y = ops.conv_fwd(x, w, s, p, bias, res, True, False)[0]
+            yr = ref.conv_fwd(x, w, s, p, bias, res, True, False)[0]
+            close(y, yr)
+    finally:
+        ops.set_knob("plan_force", -1)

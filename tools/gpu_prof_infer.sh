@@ -2,7 +2,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_inf -o run -- python tools/prof_infer.py 200 > gpurun_out/prof_inf.log 2>&1 || { tail -20 gpurun_out/prof_inf.log; exit 1; }
 grep p50 gpurun_out/prof_inf.log
-python tools/prof_summary.py gpurun_out/prof_inf --top 30 > gpurun_out/prof_inf_summary.txt
+python tools/prof_summary.py gpurun_out/prof_inf --top 30 --last-steps 0 > gpurun_out/prof_inf_summary.txt
 cat gpurun_out/prof_inf_summary.txt
 python - <<'PY'
 import csv, glob
