@@ -87,6 +87,15 @@ struct IgemmParams {
   // instead of bn_mask -- 1/16 of the bytes of the bf16 tensor
   const uint8_t* bn_mbits;
   int stats_cap;   // BM-row tiles the stats / stats2 buffers hold (host-side bounds check)
+  // in-kernel group reduction of the per-tile statistics rows (grp > 0): the last-arriving block of
+  // every group of grp consecutive row tiles (same column tile) sums the group's rows in fixed order
+  // into grp_red[g][2][gn] (fp64; grp_red2 for stats2), so the BN finalize reads <= 64 rows and
+  // needs no separate partial-reduction launch.  grp_cnt: per-(group, column tile) arrival counters,
+  // zero on entry, reset to zero by the last arriver.
+  int grp;
+  int* grp_cnt;
+  double* grp_red;
+  double* grp_red2;
 };
 
 constexpr int BK = 64;
@@ -450,20 +459,59 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           }
         }
       }
+      if (p.grp > 0) {
+        // Publish this tile's rows (plain stores -> every wave drains -> one agent-scope release ->
+        // ticket); the group's last arriver acquires and sums the group's rows in row order
+        // (cdna_hip_programming.md Guideline 16, split-K seam recipe).  Bitwise deterministic: the
+        // summation order does not depend on which block arrives last.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(smem);   // the epilogue scratch is dead here
+        const int tile_n = n0 / BN;
+        const int g = tile_m / p.grp;
+        int* cnt = p.grp_cnt + g * p.tiles_n + tile_n;
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const int members = min(p.grp, p.tiles_m - g * p.grp);
+          const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *flag = (t == members - 1) ? 1 : 0;
+        }
+        __syncthreads();
+        if (*flag) {
+          if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          __syncthreads();
+          const int r0 = g * p.grp, r1 = min(p.tiles_m, r0 + p.grp);
+          constexpr int NO = bnr2 ? 4 : 2;   // (buffer, sum index) pairs
+          for (int i = tid; i < NO * BN; i += NTHR) {
+            const int k = i / BN, c = n0 + (i - k * BN);
+            if (c >= p.gn) continue;
+            const float* src = (k < 2 ? p.stats : p.stats2) + (size_t)(k & 1) * p.gn + c;
+            double acc = 0.0;
+            for (int r = r0; r < r1; ++r) acc += (double)src[(size_t)r * 2 * p.gn];
+            double* dst = (k < 2 ? p.grp_red : p.grp_red2) + (size_t)g * 2 * p.gn + (size_t)(k & 1) * p.gn + c;
+            *dst = acc;
+          }
+          if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2>
-__global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT>
+__global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int NVA = BM * BK / 8 / NT;  // 16-B vectors per thread per stage
-  constexpr int NVB = BN * BK / 8 / NT;
+  constexpr int NVA = BM * BK / 8 / NTHR;  // 16-B vectors per thread per stage
+  constexpr int NVB = BN * BK / 8 / NTHR;
   static_assert(NVA >= 1 && NVB >= 1, "tile too small");
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == NTHR / 64, "one wave tile per wave");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -516,7 +564,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
   if constexpr (MODE != MODE_WGRAD) {
 #pragma unroll
     for (int i = 0; i < NVA; ++i) {
-      const int m = m0 + lrow + 32 * i;
+      const int m = m0 + lrow + (NTHR / 8) * i;
       const bool v = m < p.gm;
       const int mm = v ? m : 0;
       if constexpr (MODE == MODE_FWD) {
@@ -541,7 +589,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
     }
 #pragma unroll
     for (int i = 0; i < NVB; ++i) {
-      const int n = n0 + chan_perm<PAIR>(lrow + 32 * i);
+      const int n = n0 + chan_perm<PAIR>(lrow + (NTHR / 8) * i);
       b_off[i] = n < p.gn ? n * p.gk : -1;
     }
     if constexpr (UNIF) {
@@ -586,12 +634,12 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
     wb_coloff = ((wb_r - p.pad) * p.W + (wb_s - p.pad)) * p.C + wb_c;
 #pragma unroll
     for (int i = 0; i < NVA; ++i) {
-      const int row = (tid + NT * i) / CPR_A;
+      const int row = (tid + NTHR * i) / CPR_A;
       wa_off[i] = (kbeg + row) * p.K + m0 + wa_col;
     }
 #pragma unroll
     for (int i = 0; i < NVB; ++i) {
-      const int row = (tid + NT * i) / CPR_B;
+      const int row = (tid + NTHR * i) / CPR_B;
       const int m = min(kbeg + row, p.gk);   // rows past gk are masked; keep the decomposition in range
       const int n = fdiv(m, p.fd_PQ);
       const int rem = m - n * p.P * p.Q;
@@ -661,7 +709,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       const bool co_ok = m0 + wa_col < p.gm;
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
-        const int row = (tid + NT * i) / CPR_A;
+        const int row = (tid + NTHR * i) / CPR_A;
         const bool ok = co_ok && k0 + row < kend;
         ra[i] = bload16(rsA, ok ? (unsigned)wa_off[i] * 2u : kOOB);
         wa_off[i] += BK * p.K;
@@ -669,7 +717,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       // B': rows = m, cols = j=(r,s,c): im2col gather of x
 #pragma unroll
       for (int i = 0; i < NVB; ++i) {
-        const int row = (tid + NT * i) / CPR_B;
+        const int row = (tid + NTHR * i) / CPR_B;
         const int yy = wb_ps[i] - p.pad + wb_r;
         const int xx = wb_qs[i] - p.pad + wb_s;
         const bool ok = wb_ok && k0 + row < kend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
@@ -694,19 +742,19 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
     if constexpr (MODE != MODE_WGRAD) {
 #pragma unroll
       for (int i = 0; i < NVA; ++i)
-        *reinterpret_cast<uint4*>(sA + rr_off(lrow + 32 * i, lchunk)) = ra[i];
+        *reinterpret_cast<uint4*>(sA + rr_off(lrow + (NTHR / 8) * i, lchunk)) = ra[i];
 #pragma unroll
       for (int i = 0; i < NVB; ++i)
-        *reinterpret_cast<uint4*>(sB + rr_off(lrow + 32 * i, lchunk)) = rb[i];
+        *reinterpret_cast<uint4*>(sB + rr_off(lrow + (NTHR / 8) * i, lchunk)) = rb[i];
     } else {
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
-        const int v = tid + NT * i;
+        const int v = tid + NTHR * i;
         *reinterpret_cast<uint4*>(sA + tr_off<BM>(v / CPR_A, wa_col)) = ra[i];
       }
 #pragma unroll
       for (int i = 0; i < NVB; ++i) {
-        const int v = tid + NT * i;
+        const int v = tid + NTHR * i;
         *reinterpret_cast<uint4*>(sB + tr_off<BN>(v / CPR_B, wb_col)) = rb[i];
       }
     }
@@ -801,7 +849,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_kernel(const IgemmParams p) {
       }
     return;
   } else {
-    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
   }
 }
 
@@ -1509,6 +1557,35 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
 static Knob kn_splitk_red("splitk_red_v", 2);   // WGRAD split-K reduction: 1 = v1 column-only grid, 2 = split lanes
 static Knob kn_shortk_bm64("shortk_bm64", 0);   // FWD/DGRAD with gk <= N: 64x128 register-staged tiles (0 = off)
 
+// 8-wave (512-thread) register-staged WGRAD with 256x256 tiles (2x4 waves of 128x64): half the
+// operand bytes per MFMA of the 4-wave 128x128 tile.  Measured (profiles/r2_wgrad8_ab.txt): layer-3
+// 3x3 (256 filters x 2304 columns) 95 -> 86 us, layer-4 3x3 unchanged, the 1x1 filters 12-19 %
+// slower (short per-block reductions after the split), so it runs the 3x3 filters with 256 output
+// channels.  Knob wgrad8: 0 off, 1 that policy, 2 every filter with >= 256 x 256 (A/B).
+static Knob kn_wgrad8("wgrad8", 1);
+static bool use_wgrad8(const IgemmParams& p) {
+  const int k = kn_wgrad8.get();
+  if (!k || p.gm < 256 || p.gn < 256) return false;
+  return k == 2 || (p.R * p.S > 1 && p.gm <= 256);
+}
+
+static void launch_wgrad8(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, 256);
+  p.tiles_n = ceil_div(p.gn, 256);
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
+  const size_t smem = (size_t)(nk > 1 ? 2 : 1) * (256 + 256) * BK * 2;
+  auto kfn = &igemm_kernel<MODE_WGRAD, 256, 256, 2, 4, false, EPI_PLAIN, 2, 512>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(512), smem, st, p);
+  PCMP_LAUNCH_CHECK();
+}
+
 static int igemm8_mode() {
   static const int v = [] {
     const char* e = std::getenv("PCMP_IGEMM8");
@@ -1694,6 +1771,7 @@ static int wgrad_wide(const IgemmParams& p) {
 }
 
 static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
+  if (use_wgrad8(p)) { BM = 256; BN = 256; return; }
   const int w = wgrad_wide(p);
   if (w == 1) { BM = 64; BN = 256; return; }
   if (w == 2) { BM = 256; BN = 64; return; }
@@ -1734,6 +1812,7 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
     if (use_igemm8(MODE, p) == 256) { launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st); return; }
   }
   if constexpr (MODE == MODE_WGRAD) {
+    if (use_wgrad8(p)) { launch_wgrad8(p, st); return; }
     const int w = wgrad_wide(p);
     if (w == 1) { launch_cfg<MODE, 64, 256, 1, 4>(p, st); return; }
     if (w == 2) { launch_cfg<MODE, 256, 64, 4, 1>(p, st); return; }
@@ -1926,6 +2005,64 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
 }
 
 
+// ------------------------------------------------------------------------------------------------
+// In-kernel BN-statistics group reduction (IgemmParams::grp): arrival counters come from a
+// per-device ring over one persistent zero-initialised int32 buffer (the last arriver of each group
+// resets its counter, so a slot is zero again once the kernel that used it has finished; the ring
+// holds 2^20 slots, a ResNet-50 step uses ~6,000, and the host runs at most a couple of steps
+// ahead).  Knob bn_group: 0 = off (per-tile rows + partials_reduce launch, round 1; the default).
+// Measured (profiles/r2_bn_group_ab.txt): correct and bitwise reproducible, but ResNet-50 fell from
+// 11,750 to 6,720 img/s -- each last arriver walks up to 98 rows per (channel, sum) at one dependent
+// L2 round trip per row, which lengthens every statistics-producing conv by far more than the
+// ~5 us partials_reduce launch it removes (the round-1 single-launch finalize failed the same way).
+static Knob kn_bn_group("bn_group", 0);
+constexpr int kCounterSlots = 1 << 20;
+
+static int* counter_slots(int n, int device) {
+  static std::mutex mu;
+  static std::unordered_map<int, std::pair<int*, int>> bufs;   // device -> (buffer, cursor)
+  std::lock_guard<std::mutex> g(mu);
+  auto it = bufs.find(device);
+  if (it == bufs.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* buf = nullptr;
+    PCMP_HIP_CHECK(hipMalloc(&buf, sizeof(int) * kCounterSlots));
+    PCMP_HIP_CHECK(hipMemset(buf, 0, sizeof(int) * kCounterSlots));
+    PCMP_HIP_CHECK(hipDeviceSynchronize());
+    it = bufs.emplace(device, std::make_pair(buf, 0)).first;
+  }
+  auto& e = it->second;
+  if (n > kCounterSlots) return nullptr;
+  if (e.second + n > kCounterSlots) e.second = 0;
+  int* r = e.first + e.second;
+  e.second += n;
+  return r;
+}
+
+// group size for T row tiles: <= 64 reduced rows, >= 16 tiles per group
+static int bn_group_size(int T) { return std::max(16, ceil_div(T, 64)); }
+
+// set up the group reduction for a single-launch statistics producer; returns the reduced [G][2][gn]
+// fp64 tensor(s) (undefined when grouping is off or not worth it)
+static void setup_bn_group(IgemmParams& p, int T, const at::Tensor& like, at::Tensor& red, at::Tensor* red2) {
+  if (!kn_bn_group.get() || T <= 64) return;
+  const int grp = bn_group_size(T);
+  const int G = ceil_div(T, grp);
+  const int tiles_n_max = ceil_div(p.gn, 64);   // every kernel's column tile is >= 64 wide
+  int* cnt = counter_slots(G * tiles_n_max, like.get_device());
+  if (!cnt) return;
+  auto dopts = like.options().dtype(at::kDouble);
+  red = at::empty({G, 2, (int64_t)p.gn}, dopts);
+  p.grp = grp;
+  p.grp_cnt = cnt;
+  p.grp_red = red.data_ptr<double>();
+  if (red2) {
+    *red2 = at::empty({G, 2, (int64_t)p.gn}, dopts);
+    p.grp_red2 = red2->data_ptr<double>();
+  }
+}
+
 static unsigned tensor_bytes(const at::Tensor& t);
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  const c10::optional<at::Tensor>& bias,
@@ -1973,6 +2110,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr; p.bn_msc = nullptr; p.bn_msh = nullptr;
   p.bn_mbits = nullptr;
   p.stats_cap = 0;
+  p.grp = 0; p.grp_cnt = nullptr; p.grp_red = nullptr; p.grp_red2 = nullptr;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
 }
 
@@ -2005,11 +2143,12 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   p.ksplit = p.gk; p.nsplit = 1;
   const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
   const int BNsel = p.gn <= 64 ? 64 : 128;
-  at::Tensor stats;
+  at::Tensor stats, stats_red;
   if (want_stats) {
     p.stats_cap = ceil_div(p.gm, igemm_bm(MODE_FWD, p));
     stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
     p.stats = ptr<float>(stats);
+    setup_bn_group(p, p.stats_cap, x, stats_red, nullptr);
   }
   auto st = cur_stream();
   if (plain_gemm_eligible<MODE_FWD>(p)) {
@@ -2048,7 +2187,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
     return {y};
   }
   dispatch<MODE_FWD>(p, st);
-  if (want_stats) return {y, stats};
+  if (want_stats) return {y, stats_red.defined() ? stats_red : stats};
   return {y};
 }
 
@@ -2193,7 +2332,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     run_plan<MODE_DGRAD>(p, pl, ptr<__bf16>(dx), fopts, st);
     return {dx};
   }
-  at::Tensor part, part2;
+  at::Tensor part, part2, red, red2;
   if (bn) {
     set_bn(p);   // before igemm_bm: the kernel choice depends on the epilogue variant
     const int T = ceil_div(p.gm, igemm_bm(MODE_DGRAD, p));
@@ -2201,9 +2340,14 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     p.stats_cap = T;
     p.stats = ptr<float>(part);
     if (two) { part2 = at::empty({T, 2, C}, fopts); p.stats2 = ptr<float>(part2); }
+    setup_bn_group(p, T, dy, red, two ? &red2 : nullptr);
   }
   dispatch<MODE_DGRAD>(p, st);
   if (!bn) return {dx};
+  if (red.defined()) {
+    if (two) return {dx, red, red2};
+    return {dx, red};
+  }
   if (two) return {dx, part, part2};
   return {dx, part};
 }
@@ -2317,7 +2461,8 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   static std::mutex mu;
   static std::unordered_map<std::string, int> cache;
   char key[160];
-  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad);
+  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
+           (int)use_wgrad8(p));
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);

@@ -42,7 +42,18 @@ def load(build_if_missing: bool = False) -> bool:
             _load_error = None
         except Exception as e:  # pragma: no cover - depends on the environment
             _load_error = f"failed to load {LIB_PATH}: {e}"
+        if _loaded:
+            _apply_env_knobs()
         return _loaded
+
+
+def _apply_env_knobs() -> None:
+    """``PCMP_KNOBS="name=value,..."``: kernel-variant knobs (torch.ops.pcmp.set_knob) for whole-
+    program A/B runs; the defaults are the measured-best variants."""
+    spec = os.environ.get("PCMP_KNOBS", "")
+    for item in filter(None, (t.strip() for t in spec.split(","))):
+        name, _, val = item.partition("=")
+        torch.ops.pcmp.set_knob(name.strip(), int(val))
 
 
 def available() -> bool:

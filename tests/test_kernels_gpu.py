@@ -465,3 +465,37 @@ def test_small_m_plan_kinds_match_reference(gpu, kind):
             close(y, yr)
     finally:
         ops.set_knob("plan_force", -1)
+
+
+@pytest.mark.parametrize("mode", ["fwd", "dgrad_bnr", "dgrad_bnr2"])
+def test_bn_group_reduction_in_kernel(gpu, mode):
+    """The last-arriving block of each row-tile group sums the group's BN-statistics rows in fixed
+    order (fp64 [G,2,C] out, no partials_reduce launch): equal to the per-tile rows' sum, bitwise
+    reproducible, and identical in the finalize result."""
+    torch.manual_seed(3)
+    ops = _ops()
+    N, H, C, K = 32, 56, 64, 256   # 100,352 rows -> 784 tiles of 128 -> 49 groups of 16
+    x = rnd(N, H, H, C, dev=gpu)
+    w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
+    dy = rnd(N, H, H, K, dev=gpu)
+    xb = rnd(N, H, H, C, dev=gpu)
+
+    def run(group):
+        ops.set_knob("bn_group", group)
+        try:
+            if mode == "fwd":
+                return ops.conv_fwd(x, w, 1, 0, None, None, False, True)[1:]
+            mean = torch.zeros(C, device=gpu)
+            istd = torch.ones(C, device=gpu)
+            two = mode == "dgrad_bnr2"
+            out = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, None, None, xb, mean, istd,
+                                     x if two else None, mean if two else None, istd if two else None, None, None)
+            return out[1:]
+        finally:
+            ops.set_knob("bn_group", 0)
+
+    a, b, c = run(1), run(1), run(0)   # (knob default is 0; the path stays tested)
+    for pa, pb, pc in zip(a, b, c):
+        assert pa.dtype == torch.float64 and pa.shape[0] <= 64 and pc.dtype == torch.float32
+        assert torch.equal(pa, pb)
+        torch.testing.assert_close(pa.sum(0), pc.double().sum(0), rtol=1e-5, atol=1e-3)
