@@ -242,6 +242,18 @@ def _side_branch_ok(t, L) -> bool:
             os.environ.get("PCMP_DOWN_STREAM", "1") != "0")
 
 
+# Output pixels (N*P*Q) up to which an eval-mode downsample conv is forked onto the side stream.
+# Off: in the captured batch-1 graph the parallel branch costs ~93 us of fork/join per image
+# (p50 0.479 -> 0.572 ms, profiles/r2_infer_fork_ab.txt, tools/infer_fork_ab.py).
+EVAL_FORK_MAX_ROWS = 0
+
+
+def _eval_fork_ok(x, L) -> bool:
+    P = (x.shape[1] + 2 * L.pad - L.R) // L.stride + 1
+    Q = (x.shape[2] + 2 * L.pad - L.S) // L.stride + 1
+    return _side_branch_ok(x, L) and x.shape[0] * P * Q <= EVAL_FORK_MAX_ROWS
+
+
 class ResidualBlockFn(torch.autograd.Function):
     """out = relu( BN_L(conv_L(...relu(BN_1(conv_1(x)))...)) + shortcut(x) )."""
 
@@ -250,10 +262,18 @@ class ResidualBlockFn(torch.autograd.Function):
         dtype = x.dtype
         main, down = blk.main_layers(), blk.down_layer()
         if not blk.training:
+            # small inference batches: the downsample conv's few workgroups run next to the main
+            # branch on the side stream (kept as a parallel branch when the forward is graph-captured)
+            efork = None
+            if down is not None and _eval_fork_ok(x, down):
+                efork = _params.fork_side(lambda: _conv_bn_eval(x, down, dtype, False), (x,))
             h = x
             for L in main[:-1]:
                 h = _conv_bn_eval(h, L, dtype, True)
-            r = _conv_bn_eval(x, down, dtype, False) if down is not None else x
+            if efork is not None:
+                r = _params.join_side(*efork)
+            else:
+                r = _conv_bn_eval(x, down, dtype, False) if down is not None else x
             return _conv_bn_eval(h, main[-1], dtype, True, r)
 
         _params.WEIGHT_GEN[0] += 1      # running statistics move in training mode
