@@ -106,6 +106,142 @@ __global__ void partials_reduce_kernel(const float* __restrict__ part, int T, in
   if (g == 0 && col < L) red[(size_t)blockIdx.y * L + col] = s + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
 }
 
+// per-channel finalize math, shared by the two-launch and the fused (last-arriver) paths
+struct FinFwd {
+  double count;
+  const float* gamma; const float* beta;
+  float* rmean; float* rvar;
+  float momentum, eps;
+  float* mean_out; float* invstd_out; float* scale_out; float* shift_out;
+};
+__device__ __forceinline__ void bn_finalize_channel(int c, double s1, double s2, const FinFwd& a) {
+  const double mean = s1 / a.count;
+  double var = s2 / a.count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+  a.mean_out[c] = (float)mean;
+  a.invstd_out[c] = invstd;
+  const float gm = a.gamma ? a.gamma[c] : 1.f, bt = a.beta ? a.beta[c] : 0.f;
+  a.scale_out[c] = gm * invstd;
+  a.shift_out[c] = bt - (float)mean * gm * invstd;
+  if (a.rmean) {
+    const double unbiased = a.count > 1 ? var * a.count / (a.count - 1) : var;
+    a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * (float)mean;
+    a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * (float)unbiased;
+  }
+}
+
+struct FinBwd {
+  double count;
+  const float* gamma; const float* mean; const float* invstd;
+  float* dgamma_out; float* dbeta_out;
+  int accumulate;
+  float* coef;
+  int C;
+};
+__device__ __forceinline__ void bn_bwd_finalize_channel(int c, double sg, double sgx, const FinBwd& a) {
+  const float dbeta = (float)sg, dgamma = (float)sgx;
+  if (a.dgamma_out) a.dgamma_out[c] = a.accumulate ? a.dgamma_out[c] + dgamma : dgamma;
+  if (a.dbeta_out) a.dbeta_out[c] = a.accumulate ? a.dbeta_out[c] + dbeta : dbeta;
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  const float is = a.invstd[c], mu = a.mean[c];
+  const float k1 = gm * is;
+  const float k2 = -(float)(gm * (double)is * is * sgx / a.count);
+  const float k3 = -(float)(gm * (double)is * sg / a.count) - k2 * mu;
+  a.coef[c] = k1;
+  a.coef[a.C + c] = k2;
+  a.coef[2 * a.C + c] = k3;
+}
+
+// ---- fused stage-1 reduction + finalize (one launch instead of two) --------------------------
+typedef __attribute__((address_space(1))) unsigned long long gu64;   // global (not flat) shared words
+typedef __attribute__((address_space(1))) int gi32;
+// grid (ceil(C/32), G), 256 threads = 64 columns (sum 0 and sum 1 of 32 channels) x 4 row lanes.
+// Stage 1 is partials_reduce_kernel's arithmetic column for column (same rows, same order); each
+// block publishes its fp64 row of `red` with write-through (sc1) 8-byte agent-scope atomic stores,
+// drains them, and takes a ticket on its channel group's counter with a relaxed agent-scope
+// fetch_add -- no release fence, so no L2 write-back (cdna_hip_programming.md Guideline 16, R1
+// form; an agent release per block, i.e. buffer_wbl2, cost 3.6% of the ResNet-50 step).  The last of
+// the G blocks reads the rows with sc1 (agent-scope atomic) loads, which bypass its L1, and runs
+// the finalize over the G rows in bn_finalize_kernel's order (lane g sums rows g, g+4, ...; lanes
+// added 0..3), so the result is bitwise that of the two-launch path, whichever block arrives last.
+// It resets the counter to zero for the next use of the slot.
+template <bool BWD, typename FA>
+__global__ __launch_bounds__(256) void partials_reduce_finalize_kernel(const float* __restrict__ part, int T, int C,
+                                                                      int rpb, double* __restrict__ red,
+                                                                      int* __restrict__ cnt, FA fa) {
+  __shared__ double sh[4][64];
+  __shared__ double shf[2][4][32];
+  __shared__ int flag;
+  const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int cb = blockIdx.x * 32;
+  const int cj = cb + (j & 31);
+  const int L = 2 * C;
+  const int col = (j < 32) ? cj : C + cj;
+  const bool ok = cj < C;
+  const int r0 = blockIdx.y * rpb, r1 = min(T, r0 + rpb);
+  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ok) {
+    int r = r0 + g;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + 4 * u) * L + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s8[u] += v[u];
+    }
+    for (; r < r1; r += 4) s8[0] += part[(size_t)r * L + col];
+  }
+  const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
+  sh[g][j] = s;
+  __syncthreads();
+  gu64* redg = (gu64*)red;
+  if (g == 0 && ok)
+    __hip_atomic_store(redg + (size_t)blockIdx.y * L + col,
+                       (unsigned long long)__double_as_longlong(s + sh[1][j] + sh[2][j] + sh[3][j]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+  __syncthreads();
+  gi32* my = (gi32*)cnt + blockIdx.x;
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(my, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = (t == (int)gridDim.y - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the ticket
+  const int G = gridDim.y;
+  const int q = threadIdx.x & 31, lane = (threadIdx.x >> 5) & 3;
+  const int c = cb + q;
+  if (threadIdx.x < 128) {
+    // all (<= 16 + 16) loads in flight first, then the ordered sums (G <= 64 by construction)
+    double va[16], vb[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int t = lane + 4 * k;
+      const bool in = c < C && t < G;
+      va[k] = in ? __longlong_as_double((long long)__hip_atomic_load(redg + (size_t)t * L + c, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
+      vb[k] = in ? __longlong_as_double((long long)__hip_atomic_load(redg + (size_t)t * L + C + c, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
+    }
+    double a = 0, b = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (lane + 4 * k < G) { a += va[k]; b += vb[k]; }
+    shf[0][lane][q] = a;
+    shf[1][lane][q] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x < 32 && c < C) {
+    double a = shf[0][0][q], b = shf[1][0][q];
+    for (int k = 1; k < 4; ++k) { a += shf[0][k][q]; b += shf[1][k][q]; }
+    if constexpr (BWD) bn_bwd_finalize_channel(c, a, b, fa);
+    else bn_finalize_channel(c, a, b, fa);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(my, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- finalize: partials [T][2][C] -> mean, invstd, scale, shift; running stats update --------
 // block = 256 threads handles 64 channels (4 row-groups of partials).
 template <typename PT>
@@ -140,20 +276,8 @@ __global__ void bn_finalize_kernel(const PT* __restrict__ part, int T, int C, do
   __syncthreads();
   if (g == 0 && c < C) {
     for (int k = 1; k < 4; ++k) { s1 += sh[0][k][threadIdx.x]; s2 += sh[1][k][threadIdx.x]; }
-    const double mean = s1 / count;
-    double var = s2 / count - mean * mean;
-    if (var < 0) var = 0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-    mean_out[c] = (float)mean;
-    invstd_out[c] = invstd;
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    scale_out[c] = gm * invstd;
-    shift_out[c] = bt - (float)mean * gm * invstd;
-    if (rmean) {
-      const double unbiased = count > 1 ? var * count / (count - 1) : var;
-      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
-      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
-    }
+    bn_finalize_channel(c, s1, s2, FinFwd{count, gamma, beta, rmean, rvar, momentum, eps, mean_out, invstd_out,
+                                          scale_out, shift_out});
   }
 }
 
@@ -310,17 +434,7 @@ __global__ void bn_bwd_finalize_kernel(const PT* __restrict__ part, int T, int C
   __syncthreads();
   if (g == 0 && c < C) {
     for (int k = 1; k < 4; ++k) { sg += sh[0][k][threadIdx.x]; sgx += sh[1][k][threadIdx.x]; }
-    const float dbeta = (float)sg, dgamma = (float)sgx;
-    if (dgamma_out) dgamma_out[c] = accumulate ? dgamma_out[c] + dgamma : dgamma;
-    if (dbeta_out) dbeta_out[c] = accumulate ? dbeta_out[c] + dbeta : dbeta;
-    const float gm = gamma ? gamma[c] : 1.f;
-    const float is = invstd[c], mu = mean[c];
-    const float k1 = gm * is;
-    const float k2 = -(float)(gm * (double)is * is * sgx / count);
-    const float k3 = -(float)(gm * (double)is * sg / count) - k2 * mu;
-    coef[c] = k1;
-    coef[C + c] = k2;
-    coef[2 * C + c] = k3;
+    bn_bwd_finalize_channel(c, sg, sgx, FinBwd{count, gamma, mean, invstd, dgamma_out, dbeta_out, accumulate, coef, C});
   }
 }
 
@@ -616,6 +730,28 @@ static at::Tensor reduce_partials(const at::Tensor& part, int& T_out) {
   return red;
 }
 
+int* counter_slots(int n, int device);   // igemm.hip: zeroed ticket counters, reset by their last user
+static Knob kn_bn_fused_fin("bn_fused_fin", 0);   // 1: one-launch partials reduction + finalize (neutral: off)
+
+// The fused path for T > 64 partial rows: returns false (caller takes the two-launch path) when
+// disabled or when no counters can be had (first use inside a graph capture).
+template <bool BWD, typename FA>
+static bool fused_finalize(const at::Tensor& part, const FA& fa) {
+  const int T = part.size(0), C = part.size(2);
+  if (T <= 64 || !kn_bn_fused_fin.get()) return false;
+  const int rpb = std::max(16, ceil_div(T, 64));
+  const int G = ceil_div(T, rpb);   // <= 64: the reducer holds 16 rows per lane in registers
+  TORCH_CHECK(G <= 64, "fused_finalize: too many row groups");
+  const int nb = ceil_div(C, 32);
+  int* cnt = counter_slots(nb, part.get_device());
+  if (!cnt) return false;
+  auto red = at::empty({G, 2 * (int64_t)C}, part.options().dtype(at::kDouble));
+  hipLaunchKernelGGL((partials_reduce_finalize_kernel<BWD, FA>), dim3(nb, G), dim3(256), 0, cur_stream(),
+                     ptr<float>(part), T, C, rpb, ptr<double>(red), cnt, fa);
+  PCMP_LAUNCH_CHECK();
+  return true;
+}
+
 // partials -> (mean, invstd, scale, shift) ; updates running stats in place when given.
 std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const c10::optional<at::Tensor>& gamma,
                                     const c10::optional<at::Tensor>& beta,
@@ -634,6 +770,11 @@ std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const
     return {out[0], out[1], out[2], out[3]};
   }
   PCMP_CHECK_F32(part);
+  TORCH_CHECK(part.is_contiguous(), "bn_finalize: contiguous partials");
+  if (fused_finalize<false>(part, FinFwd{(double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
+                                         optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
+                                         ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C}))
+    return {out[0], out[1], out[2], out[3]};
   int T2;
   at::Tensor red = reduce_partials(part, T2);
   if (red.defined())
@@ -737,6 +878,10 @@ at::Tensor bn_bwd_finalize(const at::Tensor& part, int64_t count, const c10::opt
     return coef;
   }
   PCMP_CHECK_F32(part);
+  TORCH_CHECK(part.is_contiguous(), "bn_bwd_finalize: contiguous partials");
+  if (fused_finalize<true>(part, FinBwd{(double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
+                                        optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef), C}))
+    return coef;
   int T2;
   at::Tensor red = reduce_partials(part, T2);
   if (red.defined())

@@ -2018,7 +2018,7 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
 static Knob kn_bn_group("bn_group", 0);
 constexpr int kCounterSlots = 1 << 20;
 
-static int* counter_slots(int n, int device) {
+int* counter_slots(int n, int device) {
   static std::mutex mu;
   static std::unordered_map<int, std::pair<int*, int>> bufs;   // device -> (buffer, cursor)
   std::lock_guard<std::mutex> g(mu);
@@ -2161,8 +2161,9 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   const int tiles = ceil_div(p.gm, BMsel) * ceil_div(p.gn, BNsel);
   const int ksteps = ceil_div(p.gk, BK);
   int nsplit = 1;
-  // PCMP_FWD_SPLIT_TARGET / PCMP_FWD_SPLIT_MINK: grid target and minimum K-steps per split (A/B knobs)
-  static const int split_target = [] { const char* e = getenv("PCMP_FWD_SPLIT_TARGET"); return e ? atoi(e) : 256; }();
+  // PCMP_FWD_SPLIT_TARGET / PCMP_FWD_SPLIT_MINK: grid target and minimum K-steps per split (A/B-only knobs of
+  // the round-1 heuristic; numerics at high split counts are covered by the plan_force small-M tests)
+  static const int split_target = [] { const char* e = getenv("PCMP_FWD_SPLIT_TARGET"); return e ? std::max(1, atoi(e)) : 256; }();
   static const int split_mink = [] { const char* e = getenv("PCMP_FWD_SPLIT_MINK"); return e ? std::max(1, atoi(e)) : 4; }();
   if (!want_stats && tiles < 128 && ksteps >= 8)
     nsplit = std::max(1, std::min({ceil_div(split_target, tiles), ksteps / split_mink, 32}));

@@ -192,6 +192,41 @@ def test_bn_forward_backward(gpu, C):
     close(gg, ggr)
 
 
+@pytest.mark.parametrize("T,C", [(65, 64), (6272, 64), (300, 72), (1568, 2048)])
+def test_bn_fused_finalize_bitwise(gpu, T, C):
+    """One-launch partials reduction + finalize (last-arriver ticket) == the two-launch path, bitwise,
+    for the forward (mean/invstd/scale/shift/running stats) and backward (dgamma/dbeta/coef)
+    finalize; both against an fp64 torch reduction.  Repeated calls reuse the ticket counters."""
+    ops = _ops()
+    g = torch.Generator(device=gpu).manual_seed(T + C)
+    part = torch.randn(T, 2, C, device=gpu, generator=g)
+    part[:, 1] = part[:, 1].abs() * 4 + 2          # sum of squares: positive, var > 0
+    gam = torch.rand(C, device=gpu, generator=g) + 0.5
+    bet = torch.randn(C, device=gpu, generator=g)
+    mean, invstd = torch.randn(C, device=gpu, generator=g), torch.rand(C, device=gpu, generator=g) + 0.5
+    count = T * 16
+    outs = {}
+    for v in (0, 1, 1, 1):
+        ops.set_knob("bn_fused_fin", v)
+        rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+        fwd = ops.bn_finalize(part, count, gam, bet, rm, rv, 0.1, 1e-5)
+        dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), 0.25, device=gpu)
+        coef = ops.bn_bwd_finalize(part, count, gam, mean, invstd, dg, db, True)
+        outs.setdefault(v, []).append([t.clone() for t in (*fwd, rm, rv, dg, db, coef)])
+    ops.set_knob("bn_fused_fin", 1)
+    base = outs[0][0]
+    for rep in outs[1]:
+        for a, b in zip(base, rep):
+            assert torch.equal(a, b)
+    s = part.double().sum(0)
+    m = s[0] / count
+    var = (s[1] / count - m * m).clamp_min(0)
+    close(base[0], m.float(), 1e-6, 1e-6)
+    close(base[1], (1.0 / torch.sqrt(var + 1e-5)).float(), 1e-5, 1e-6)
+    close(base[7], (0.25 + s[0]).float(), 1e-6, 1e-4)    # dbeta accumulated
+    close(base[6], (0.5 + s[1]).float(), 1e-6, 1e-4)     # dgamma accumulated
+
+
 def test_maxpool_gap(gpu):
     x = rnd(2, 17, 17, 64, dev=gpu)
     y, idx = _ops().maxpool_fwd(x, 3, 2, 1, True)
