@@ -12,6 +12,7 @@
 //     with zero channel padding to a multiple of 8 (the stem conv's MFMA K granularity)
 #include "common.h"
 
+#include <climits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -669,6 +670,150 @@ at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c1
   return y;
 }
 
+// ---- row-wise top-k / argmax: one wave per row ----------------------------------------------
+// Replaces torch.argmax / torch.topk on logits (batch-1 prediction, top-1/top-5 accuracy).  Each
+// lane keeps its own sorted top-KM of the columns it strides over (lane, lane+64, ...), then k
+// rounds of a 64-lane butterfly pick the best head and its lane pops it.  Order: larger value
+// first, ties to the smaller column (torch.argmax's first-occurrence rule); NaN ranks above every
+// number, as in torch.
+__device__ __forceinline__ bool topk_better(float a, int ia, float b, int ib) {
+  const bool na = a != a, nb = b != b;
+  if (na != nb) return na;
+  if (na) return ia < ib;
+  return a > b || (a == b && ia < ib);
+}
+__device__ __forceinline__ float load_f(const float* p) { return *p; }
+__device__ __forceinline__ float load_f(const __bf16* p) { return (float)*p; }
+
+template <typename T, int KM>
+__global__ __launch_bounds__(256) void topk_rows_kernel(const T* __restrict__ x, int B, int C, int64_t ld, int k,
+                                                        float* __restrict__ vals, int64_t* __restrict__ idx) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const T* xr = x + (size_t)row * ld;
+  float v[KM];
+  int ix[KM];
+#pragma unroll
+  for (int q = 0; q < KM; ++q) { v[q] = -INFINITY; ix[q] = INT_MAX; }
+  for (int j = lane; j < C; j += 64) {
+    float cv = load_f(xr + j);
+    int ci = j;
+#pragma unroll
+    for (int q = 0; q < KM; ++q)
+      if (topk_better(cv, ci, v[q], ix[q])) {
+        const float tv = v[q]; const int ti = ix[q];
+        v[q] = cv; ix[q] = ci; cv = tv; ci = ti;
+      }
+  }
+  for (int r = 0; r < k; ++r) {
+    float bv = v[0];
+    int bi = ix[0];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float ov = __shfl_xor(bv, off);
+      const int oi = __shfl_xor(bi, off);
+      if (topk_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) {
+      if (vals) vals[(size_t)row * k + r] = bv;
+      idx[(size_t)row * k + r] = bi;
+    }
+    if (ix[0] == bi) {   // the winning lane pops its head
+#pragma unroll
+      for (int q = 0; q + 1 < KM; ++q) { v[q] = v[q + 1]; ix[q] = ix[q + 1]; }
+      v[KM - 1] = -INFINITY; ix[KM - 1] = INT_MAX;
+    }
+  }
+}
+
+std::vector<at::Tensor> topk_rows(const at::Tensor& x, int64_t k, bool want_values) {
+  PCMP_CHECK_CUDA(x);
+  TORCH_CHECK(x.dim() == 2 && x.numel() > 0 && x.stride(1) == 1, "topk_rows: non-empty [B, C] rows with unit column stride");
+  const int C = x.size(1);
+  const int B = x.size(0);
+  const int64_t ld = x.stride(0);
+  TORCH_CHECK(k >= 1 && k <= 8 && k <= C, "topk_rows: 1 <= k <= min(8, C)");
+  auto idx = at::empty({B, k}, x.options().dtype(at::kLong));
+  at::Tensor vals = want_values ? at::empty({B, k}, x.options().dtype(at::kFloat)) : at::Tensor();
+  float* vp = want_values ? ptr<float>(vals) : nullptr;
+  const dim3 grid(ceil_div(B, 4)), block(256);
+  const int kk = (int)k;
+  if (x.scalar_type() == at::kFloat) {
+    const float* xp = x.data_ptr<float>();
+    if (k == 1) hipLaunchKernelGGL((topk_rows_kernel<float, 1>), grid, block, 0, cur_stream(), xp, B, C, ld, 1, vp, ptr<int64_t>(idx));
+    else hipLaunchKernelGGL((topk_rows_kernel<float, 8>), grid, block, 0, cur_stream(), xp, B, C, ld, kk, vp, ptr<int64_t>(idx));
+  } else {
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16, "topk_rows: f32 or bf16 input");
+    const __bf16* xp = reinterpret_cast<const __bf16*>(x.data_ptr());
+    if (k == 1) hipLaunchKernelGGL((topk_rows_kernel<__bf16, 1>), grid, block, 0, cur_stream(), xp, B, C, ld, 1, vp, ptr<int64_t>(idx));
+    else hipLaunchKernelGGL((topk_rows_kernel<__bf16, 8>), grid, block, 0, cur_stream(), xp, B, C, ld, kk, vp, ptr<int64_t>(idx));
+  }
+  PCMP_LAUNCH_CHECK();
+  if (want_values) return {vals, idx};
+  return {idx};
+}
+
+// ---- synthetic image batch (data/synthetic.py SyntheticImages on the GPU) ----------------------
+// x[b,c,i,j] = clamp(0.5*color[y_b,c] + 0.25*(sin(fy*t_i)*cos(fx*t_j) + 1)*0.5 + noise*u, 0, 1),
+// t = linspace(0, 2*pi, S), u a counter-based uniform (splitmix64 of (seed, element index)): one
+// launch instead of ~10 torch ops, four contiguous pixels per thread (16-B stores).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void synth_images_kernel(const int64_t* __restrict__ labels,
+                                                           const float* __restrict__ color,
+                                                           const float* __restrict__ freq, int B, int C, int S,
+                                                           uint64_t seed, float noise, float* __restrict__ out) {
+  const int S4 = S / 4;
+  const int64_t total = (int64_t)B * C * S * S4;
+  const float step = 6.283185307179586f / (float)(S - 1);
+  const uint64_t key = splitmix64(seed);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int j4 = t % S4;
+    int64_t r = t / S4;
+    const int i = r % S; r /= S;
+    const int c = r % C;
+    const int b = r / C;
+    const int y = (int)labels[b];
+    const float fy = freq[2 * y], fx = freq[2 * y + 1];
+    const float base = 0.5f * color[y * C + c];
+    const float sy = sinf(fy * (i * step));
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = 4 * j4 + e;
+      const uint64_t h = splitmix64(key ^ (uint64_t)(4 * t + e));
+      const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+      const float val = base + 0.25f * (sy * cosf(fx * (j * step)) + 1.f) * 0.5f + noise * u;
+      o[e] = fminf(fmaxf(val, 0.f), 1.f);
+    }
+    *reinterpret_cast<float4*>(out + 4 * t) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+at::Tensor synth_images(const at::Tensor& labels, const at::Tensor& color, const at::Tensor& freq, int64_t S,
+                        int64_t seed, double noise) {
+  PCMP_CHECK_CUDA(labels); PCMP_CHECK_CONTIG(labels); PCMP_CHECK_F32(color); PCMP_CHECK_F32(freq);
+  PCMP_CHECK_CONTIG(color); PCMP_CHECK_CONTIG(freq);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.dim() == 1, "synth_images: int64 labels [B]");
+  TORCH_CHECK(color.dim() == 2 && freq.dim() == 2 && freq.size(1) == 2 && freq.size(0) == color.size(0),
+              "synth_images: color [K,C], freq [K,2]");
+  TORCH_CHECK(S >= 4 && S % 4 == 0, "synth_images: image size must be a multiple of 4");
+  const int B = labels.size(0), C = color.size(1);
+  auto out = at::empty({B, C, S, S}, color.options());
+  if (B == 0) return out;
+  const int64_t total = (int64_t)B * C * S * (S / 4);
+  const int grid = (int)std::min<int64_t>(ceil_div(total, (int64_t)256), 8192);
+  hipLaunchKernelGGL(synth_images_kernel, dim3(grid), dim3(256), 0, cur_stream(), ptr<int64_t>(labels),
+                     ptr<float>(color), ptr<float>(freq), B, C, (int)S, (uint64_t)seed, (float)noise, ptr<float>(out));
+  PCMP_LAUNCH_CHECK();
+  return out;
+}
+
 }  // namespace pcmp
 
 namespace pcmp {
@@ -719,4 +864,6 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()", &pcmp::colsum);
   m.def("nchw_to_nhwc(Tensor x, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor", &pcmp::nchw_to_nhwc);
   m.def("image_to_s2d(Tensor x, int pad, float scale, Tensor? mean, Tensor? stdv, bool nhwc) -> Tensor", &pcmp::image_to_s2d);
+  m.def("topk_rows(Tensor x, int k, bool want_values) -> Tensor[]", &pcmp::topk_rows);
+  m.def("synth_images(Tensor labels, Tensor color, Tensor freq, int S, int seed, float noise) -> Tensor", &pcmp::synth_images);
 }

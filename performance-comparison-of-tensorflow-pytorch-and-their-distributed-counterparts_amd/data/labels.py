@@ -14,6 +14,7 @@ import re
 
 import torch
 
+from ..ops.kernels import topk_rows
 from .imagefolder import IMAGENETTE_LABELS
 
 _ENTRY = re.compile(r"""^\s*\{?\s*(\d+)\s*:\s*(['"])(.*?)\2\s*,?\s*\}?\s*$""")
@@ -53,7 +54,7 @@ def decode_topk(logits_or_probs: torch.Tensor, labels: list[str] | None = None, 
     """Per sample, the k best (class id, label, probability) triples (Keras decode_predictions)."""
     x = logits_or_probs.float()
     p = torch.softmax(x, dim=-1) if from_logits else x
-    val, idx = p.topk(k, dim=-1)
+    val, idx = topk_rows(p, k)
     out = []
     for vi, ii in zip(val.tolist(), idx.tolist()):
         out.append([(c, labels[c] if labels is not None and c < len(labels) else str(c), v) for c, v in zip(ii, vi)])

@@ -9,7 +9,8 @@ No network in this environment: Imagenette2 and the IMDB CSV (its zip is a missi
   * ``SyntheticIMDB``: int64 token ids ``[128]`` (vocab 30522, [CLS]=101 ... [SEP]=102, post
     padding 0), a review-length distribution, 2 classes with class-dependent token statistics.
 Labels, lengths and class signatures are pure functions of (seed, index), so any sharding or
-shuffling sees the same labelled dataset on every rank; the additive noise is drawn per batch.  Batches are generated directly on the target device (no host->device copy).
+shuffling sees the same labelled dataset on every rank; the additive noise is drawn per batch.  Batches are generated directly on the target device (no host->device copy); on the GPU
+one fused kernel (synth_images) writes the batch.
 """
 from __future__ import annotations
 
@@ -47,15 +48,28 @@ class SyntheticImages:
     def labels(self, idx: torch.Tensor) -> torch.Tensor:
         return (torch.floor(_hash01(self.seed + 7, idx.cpu()) * self.num_classes).long() % self.num_classes)
 
+    def _native_ok(self, dev) -> bool:
+        from ..ops import _lib
+        return dev.type == "cuda" and self.size % 4 == 0 and _lib.use_native(torch.empty(0, device=dev))
+
     def get_batch(self, idx, device=None):
         dev = torch.device(device) if device is not None else self.device
         idx = torch.as_tensor(idx, dtype=torch.long)
         y = self.labels(idx)
         B, S, C = idx.numel(), self.size, self.channels
+        seed = int(self.seed * 1000003 + int(idx[0]) * 7919 + B) % (2 ** 62)
+        if self._native_ok(dev):
+            # one fused launch (csrc/elementwise.hip synth_images_kernel): same formula, counter-based noise
+            from ..ops.kernels import K
+            if getattr(self, "_dev_tabs", (None,))[0] != dev:
+                self._dev_tabs = (dev, self.color.view(self.num_classes, C).contiguous().to(dev),
+                                  self.freq.contiguous().to(dev))
+            yd = y.to(dev, non_blocking=True)
+            return K.synth_images(yd, self._dev_tabs[1], self._dev_tabs[2], S, seed, float(self.noise)), yd
         lin = torch.linspace(0, 2 * math.pi, S, device=dev)
         fy, fx = self.freq[y, 0].to(dev), self.freq[y, 1].to(dev)
         pat = torch.sin(fy.view(B, 1, 1) * lin.view(1, S, 1)) * torch.cos(fx.view(B, 1, 1) * lin.view(1, 1, S))
-        g = torch.Generator(device=dev).manual_seed(int(self.seed * 1000003 + int(idx[0]) * 7919 + B) % (2 ** 62))
+        g = torch.Generator(device=dev).manual_seed(seed)
         noise = torch.rand(B, C, S, S, device=dev, generator=g)
         x = 0.5 * self.color[y].to(dev) + 0.25 * (pat.unsqueeze(1) + 1.0) * 0.5 + self.noise * noise
         return x.clamp_(0.0, 1.0), y.to(dev)

@@ -19,6 +19,7 @@ import time
 
 import torch
 
+from ..ops.kernels import argmax_rows
 from ..utils import report as R
 from ..utils.misc import watchdog_kick
 
@@ -36,18 +37,18 @@ class Batch1Predictor:
         self.use_graph = use_graph and self.device.type == "cuda"
         with torch.no_grad():
             for _ in range(warmup):
-                self.static_out = _logits(model, self.static_in).argmax(1)
+                self.static_out = argmax_rows(_logits(model, self.static_in))
             if self.use_graph:
                 torch.cuda.synchronize()
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
                     for _ in range(2):
-                        self.static_out = _logits(model, self.static_in).argmax(1)
+                        self.static_out = argmax_rows(_logits(model, self.static_in))
                 torch.cuda.current_stream().wait_stream(s)
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph):
-                    self.static_out = _logits(model, self.static_in).argmax(1)
+                    self.static_out = argmax_rows(_logits(model, self.static_in))
                 torch.cuda.synchronize()
 
     @torch.no_grad()
@@ -56,7 +57,7 @@ class Batch1Predictor:
         if self.graph is not None:
             self.graph.replay()
         else:
-            self.static_out = _logits(self.model, self.static_in).argmax(1)
+            self.static_out = argmax_rows(_logits(self.model, self.static_in))
         return int(self.static_out.item())
 
 

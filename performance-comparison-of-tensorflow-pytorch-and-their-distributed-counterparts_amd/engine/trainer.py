@@ -29,6 +29,7 @@ import torch
 
 from .. import optim as pcmp_optim
 from ..ops.functions import cross_entropy
+from ..ops.kernels import argmax_rows
 from ..parallel.ddp import DistributedDataParallel
 from ..parallel.metrics import all_reduce_max, all_reduce_sum
 from ..utils import report as R
@@ -127,7 +128,7 @@ def evaluate_images(model, loader, reference_compat=False):
         z = _logits(model, x)
         logp = torch.log_softmax(z.float(), dim=1)
         losses.append(torch.nn.functional.nll_loss(logp, y))
-        accs.append((logp.argmax(1) == y).float().mean())
+        accs.append((argmax_rows(logp) == y).float().mean())
         nb += 1
     if nb:
         loss_sum = float(torch.stack(losses).sum())
@@ -265,7 +266,7 @@ def evaluate_text(model, loader):
     for ids, mask, labels in loader:
         watchdog_kick("eval")
         z = model.forward_logits(ids, mask)
-        accs.append((z.float().argmax(1) == labels).float().mean())
+        accs.append((argmax_rows(z) == labels).float().mean())
     model.train()
     s = all_reduce_sum([float(torch.stack(accs).sum()) if accs else 0.0, len(accs)])
     return s[0] / max(1.0, s[1])
@@ -295,7 +296,7 @@ def keras_fit(state: TrainState, train, val=None, epochs=5, printer=R.rprint):
             loss = categorical_crossentropy(z, onehot)
             state.backward_step(loss)
             tot += float(loss) * y.numel()
-            correct += float((z.argmax(1) == y).sum())
+            correct += float((argmax_rows(z) == y).sum())
             n += y.numel()
         rec = {"epoch": e + 1, "loss": tot / max(1, n), "accuracy": correct / max(1, n), "time_s": time.time() - t0}
         if val is not None:
@@ -316,7 +317,7 @@ def keras_evaluate(model, val, timed=True, printer=R.rprint):
         watchdog_kick("eval")
         z = model.forward_logits(x).float()
         tot += float(torch.nn.functional.cross_entropy(z, y, reduction="sum"))
-        correct += float((z.argmax(1) == y).sum())
+        correct += float((argmax_rows(z) == y).sum())
         n += y.numel()
     model.train()
     if timed:

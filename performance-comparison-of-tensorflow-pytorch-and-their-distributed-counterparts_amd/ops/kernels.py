@@ -26,6 +26,7 @@ OP_NAMES = (
     "masked_mean_fwd", "masked_mean_bwd",
     "layernorm_fwd", "layernorm_bwd", "gelu_fwd", "gelu_bwd",
     "attention_fwd", "attention_bwd", "tanh_fwd", "tanh_bwd", "add_bf16",
+    "topk_rows", "synth_images",
 )
 
 
@@ -56,3 +57,18 @@ class _Dispatch:
 
 
 K = _Dispatch()
+
+
+def argmax_rows(z: torch.Tensor) -> torch.Tensor:
+    """``z.argmax(1)`` of [B, C] scores (native wave-per-row kernel on the GPU)."""
+    if z.dim() == 2 and z.stride(1) == 1 and z.dtype in (torch.float32, torch.bfloat16):
+        return K.topk_rows(z, 1, False)[0].view(-1)
+    return z.argmax(1)
+
+
+def topk_rows(z: torch.Tensor, k: int):
+    """(values fp32, indices) of the k largest scores per row (k <= 8 native; torch otherwise)."""
+    if z.dim() == 2 and z.stride(1) == 1 and k <= 8 and z.dtype in (torch.float32, torch.bfloat16):
+        return tuple(K.topk_rows(z, k, True))
+    v, i = z.float().topk(k, dim=-1)
+    return v, i

@@ -563,3 +563,43 @@ def attention_bwd(dctx, qkv, ctx, lse, ids, B, S, H, p_drop, seed, offset):
     dK = dS.transpose(-1, -2) @ q * 0.125
     out = torch.stack([dQ, dK, dV], 2)  # [B,H,3,S,d]
     return out.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * D).to(qkv.dtype)
+
+
+def topk_rows(x, k, want_values):
+    """Row-wise top-k of the last dim: larger first, ties to the smaller index, NaN above numbers
+    (csrc/elementwise.hip topk_rows_kernel)."""
+    xf = x.float().reshape(-1, x.shape[-1])
+    v, i = torch.sort(xf, dim=-1, descending=True, stable=True)
+    v, i = v[:, :k].contiguous(), i[:, :k].contiguous()
+    return [v, i] if want_values else [i]
+
+
+_SM_GOLD, _SM_M1, _SM_M2 = 0x9E3779B97F4A7C15, 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+
+
+def _splitmix64(z):
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(_SM_GOLD)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(_SM_M1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(_SM_M2)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_images(labels, color, freq, S, seed, noise):
+    """data/synthetic.py image formula with the counter-based noise of synth_images_kernel."""
+    import math
+
+    import numpy as np
+    B, C = labels.numel(), color.shape[1]
+    y = labels.long().cpu()
+    step = np.float32(2 * math.pi) / np.float32(S - 1)
+    t = torch.arange(S, dtype=torch.float32) * float(step)
+    fy, fx = freq[y, 0].float().cpu(), freq[y, 1].float().cpu()
+    pat = torch.sin(fy.view(B, 1, 1) * t.view(1, S, 1)) * torch.cos(fx.view(B, 1, 1) * t.view(1, 1, S))
+    key = _splitmix64(np.array([seed & (2 ** 64 - 1)], dtype=np.uint64))[0]
+    n = np.arange(B * C * S * S, dtype=np.uint64)
+    u = (_splitmix64(key ^ n) >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    u = torch.from_numpy(u).view(B, C, S, S)
+    x = 0.5 * color[y].float().cpu().view(B, C, 1, 1) + 0.25 * (pat.unsqueeze(1) + 1.0) * 0.5 + noise * u
+    return x.clamp_(0.0, 1.0).to(labels.device)

@@ -9,6 +9,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..ops.kernels import argmax_rows
+
 
 def _device():
     if dist.is_initialized() and dist.get_backend() == "nccl":
@@ -48,7 +50,7 @@ class MetricAccumulator:
         n = labels.numel() if labels is not None else 1
         self.loss_sum += loss.detach().double() * n
         if logits is not None and labels is not None:
-            self.correct += (logits.detach().argmax(1) == labels).sum().double()
+            self.correct += (argmax_rows(logits.detach()) == labels).sum().double()
         self.count += n
         self.steps += 1
 

@@ -534,3 +534,41 @@ def test_bn_group_reduction_in_kernel(gpu, mode):
         assert pa.dtype == torch.float64 and pa.shape[0] <= 64 and pc.dtype == torch.float32
         assert torch.equal(pa, pb)
         torch.testing.assert_close(pa.sum(0), pc.double().sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,k", [(1, 1000, 1), (256, 1000, 1), (64, 10, 5), (37, 1000, 8), (5, 3, 3)])
+def test_topk_rows_vs_stable_sort(gpu, dtype, B, C, k):
+    g = torch.Generator(device=gpu).manual_seed(B * 7 + C + k)
+    x = torch.randn(B, C + 8, device=gpu, generator=g).to(dtype)[:, :C]   # row stride C+8 (padded logits)
+    x[0, C // 2] = x[0].max() if B > 1 else x[0, C // 2]                   # a tie: the smaller index wins
+    v, i = _ops().topk_rows(x, k, True)
+    vr, ir = ref.topk_rows(x, k, True)
+    assert torch.equal(i.cpu(), ir.cpu())
+    assert torch.equal(v.cpu(), vr.cpu())
+    (i1,) = _ops().topk_rows(x, 1, False)
+    assert torch.equal(i1.view(-1).cpu(), x.float().argmax(1).cpu())
+
+
+def test_topk_rows_nan_ranks_first(gpu):
+    x = torch.randn(2, 100, device=gpu)
+    x[1, 17] = float("nan")
+    (i,) = _ops().topk_rows(x, 1, False)
+    assert i.view(-1).tolist() == [int(x[0].argmax()), 17]
+
+
+def test_synth_images_vs_reference(gpu):
+    from pcmp.data.synthetic import SyntheticImages
+    ds = SyntheticImages(n=100, image_size=32, seed=3, device=gpu)
+    lab = torch.tensor([0, 4, 9, 4], device=gpu)
+    col = ds.color.view(10, 3).contiguous().to(gpu)
+    fr = ds.freq.contiguous().to(gpu)
+    out = _ops().synth_images(lab, col, fr, 32, 12345, 0.15)
+    outr = ref.synth_images(lab, col, fr, 32, 12345, 0.15)
+    close(out, outr, 0, 1e-5)
+    x, y = ds.get_batch(list(range(8)))
+    assert x.shape == (8, 3, 32, 32) and x.dtype == torch.float32 and x.is_cuda
+    assert 0.0 <= float(x.min()) and float(x.max()) <= 1.0
+    assert torch.equal(y.cpu(), ds.labels(torch.arange(8)))
+    x2, _ = ds.get_batch(list(range(8)))
+    assert torch.equal(x, x2)          # deterministic per (seed, index window)
