@@ -49,8 +49,11 @@ class SyntheticImages:
         return (torch.floor(_hash01(self.seed + 7, idx.cpu()) * self.num_classes).long() % self.num_classes)
 
     def _native_ok(self, dev) -> bool:
+        import os
+
         from ..ops import _lib
-        return dev.type == "cuda" and self.size % 4 == 0 and _lib.use_native(torch.empty(0, device=dev))
+        return (dev.type == "cuda" and self.size % 4 == 0 and os.environ.get("PCMP_SYNTH_NATIVE", "1") != "0"
+                and _lib.use_native(torch.empty(0, device=dev)))
 
     def get_batch(self, idx, device=None):
         dev = torch.device(device) if device is not None else self.device

@@ -225,12 +225,14 @@ def test_transfer_learning_flow_reaches_reference_accuracy(gpu):
     from pcmp.models.layers import MLPHead
     from pcmp.models.resnet import resnet50
     res, B = 96, 64
-    ds = SyntheticImages(12800, 10, res, seed=42, device=gpu)
-    # "pretraining": 160 SGD steps over images 2560.. (never seen by the TL split below)
+    ds = SyntheticImages(28160, 10, res, seed=42, device=gpu)
+    # "pretraining": 400 SGD steps over images 2560.. (never seen by the TL split below).  160 steps
+    # left the frozen features on the edge: test accuracy 0.65-1.0 depending on which autotuned
+    # kernel plans (and so which rounding) earlier tests had cached.
     torch.manual_seed(0)
     m = resnet50(num_classes=10).to(gpu).train()
     pre = make_state(m, "sgd", lr=0.05, momentum=0.9, weight_decay=5e-5)
-    for i in range(160):
+    for i in range(400):
         pre.opt.set_lr(0.05 * min(1.0, (i + 1) / 30))
         x, y = ds.get_batch(list(range(2560 + i * B, 2560 + (i + 1) * B)))
         pre.zero_grad()
