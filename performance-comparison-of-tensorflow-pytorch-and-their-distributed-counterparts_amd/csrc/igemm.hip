@@ -1227,6 +1227,245 @@ __global__ void __launch_bounds__(NT, 2) igemm_stream_kernel(const IgemmParams p
 }
 
 // ------------------------------------------------------------------------------------------------
+// Halo-tiled direct convolution for stride-1 convs with narrow channels: the ResNet layer-1 3x3
+// (64 -> 64 channels at 56x56: FWD and DGRAD) and the space-to-depth stem (16 -> 64 channels,
+// 4x4 taps at 112x112).  The implicit GEMM above re-reads every input pixel once per filter tap
+// (9x / 16x L2->LDS traffic for a 64-wide output tile); here a tile is TR whole output rows of one
+// image (BM = 224 pixels) and the block DMAs the (TR+R-1) x (Wo+S-1) input halo into LDS ONCE,
+// zero-filled at the borders through the buffer range check.  Every tap's B fragment is read from
+// the halo in place: within a filter row r the (s, c) pairs of the KRSC reduction order are
+// contiguous in the halo row, so the K32 chunk of reduction index k starts at halo pixel
+// (ty + r, tx + s) channel c -- one ds_read_b128 per lane per pixel fragment, no im2col image.
+// The 64 output channels' weights (K = R*S*C <= 576) live in REGISTERS for the whole persistent
+// kernel (each wave: 32 channels x K), so the only LDS reads are pixel fragments: 7 reads per 14
+// MFMAs.  LDS layout: [halo row][16-B channel chunk][column], each (row, chunk) run of HWp >= HWd+15
+// slots (HWp % 16 == 0) shifted by skew(row) = (row * Wo) % 16, so the bank quad of (row, col) is
+// (linear output pixel + tap offset) % 16: the 16 pixels of a fragment -- row wraps included -- and
+// both k-groups of every ds_read_b128 lane group land on 16 distinct quads (an XOR swizzle of a
+// pixel-major image left 40 % of the LDS cycles as bank conflicts: profiles/r2_halo_pmc.txt).
+// One block per CU walks a contiguous range of tiles (neighbouring tiles share halo rows
+// in the XCD's L2); the next tile's halo DMA overlaps this tile's MFMAs and epilogue.  The
+// accumulators have igemm_kernel's D^T/PAIR layout, so the shared epilogue (BatchNorm statistics,
+// fused BN-backward reduction, residual, ReLU) is reused unchanged.
+// DGRAD runs as the forward correlation of dy with the tap-mirrored transposed weight
+// (pad' = R-1-pad); FLIP reads wt[c][R-1-r][S-1-s][k] while loading the weight registers.
+struct HaloGeom {
+  const __bf16* src;      // [N][Hs][Ws][CS]
+  const __bf16* wsrc;     // [64][R][S][CS]
+  unsigned src_bytes;
+  int Hs, Ws, Ho, Wo, padT, padL, TR, HWd, HWp, HR, tiles, tiles_img, lds_bytes, ninstr;
+  FastDiv fd_HWp, fd_Wo, fd_timg;
+};
+constexpr int HALO_BM = 224;
+
+
+template <int MODE, int EPI, int CS, int RS, bool FLIP, int WO, bool OVL>
+__global__ void __launch_bounds__(NT, 1) halo_conv_kernel(const IgemmParams p, const HaloGeom g) {
+  constexpr int BM = HALO_BM, BN = 64, WM = 2, WN = 2;
+  constexpr int WTM = BM / WM, TM = WTM / 16, TN = BN / WN / 16;
+  constexpr int KC = RS * RS * CS / 32;   // K32 chunks
+  constexpr int NCH = CS / 8;              // 16-B channel chunks per pixel
+  constexpr int TR = BM / WO, HWd = WO + RS - 1, HWp = (HWd + 30) / 16 * 16, HR = TR + RS - 1;
+  constexpr int NINSTR = (HR * NCH * HWp * 16 + 1023) / 1024;
+  static_assert(TM == 7 && TN == 2 && (RS * CS) % 32 == 0 && BM % WO == 0, "halo tiling");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  constexpr int LDS_BYTES = NINSTR * 1024;
+  // OVL (FWD without residual / ReLU / bias): the finished tile goes to LDS as bf16 (ytile, 16-B
+  // chunks XOR-swizzled by pixel) and its global stores are spread over the NEXT tile's MFMA steps,
+  // so at one wave per SIMD the output traffic hides under the matrix work instead of following it
+  constexpr int YT_BYTES = OVL ? BM * BN * 2 : 0;
+  constexpr int NYS = BM * BN * 2 / 16 / NT;   // 16-B output chunks per thread per tile (7)
+  char* ytile = smem + 2 * LDS_BYTES;
+  char* scratch = ytile + YT_BYTES;
+  __bf16* yout = reinterpret_cast<__bf16*>(p.out);
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(g.src, g.src_bytes);
+
+  // this wave's 32 output channels x the whole reduction, as MFMA A fragments (PAIR channel order)
+  bf16x8 wreg[KC][TN];
+#pragma unroll
+  for (int kt = 0; kt < KC; ++kt)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = chan_perm<true>(wc * 32 + j * 16 + (lane & 15));
+      const int k = kt * 32 + 8 * (lane >> 4);
+      const int r = k / (RS * CS), sx = (k / CS) % RS, c = k % CS;
+      const int rr = FLIP ? RS - 1 - r : r, ss = FLIP ? RS - 1 - sx : sx;
+      wreg[kt][j] = *reinterpret_cast<const bf16x8*>(g.wsrc + ((size_t)(n * RS + rr) * RS + ss) * CS + c);
+    }
+  // Per lane, fragment and filter row r: the byte address of its K32 chunk 0.  Within a filter row
+  // the chunk's offset from there is lane-uniform and compile-time (folded into ds_read_b128's
+  // immediate): CS=64: chunk (kt%2)*4 -> +4*HWp slots, tap column s -> +s; CS=16: tap pair s0 -> +s0.
+  // The lane's k-group g picks chunk g (CS=64), or pixel +g/2 and chunk g%2 (CS=16).
+  const int kg = lane >> 4;
+  int base[TM][RS];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int pp = wr * WTM + i * 16 + (lane & 15);
+    const int ty = pp / WO, tx = pp % WO;
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+      const int hr = ty + r;
+      const int chunk = CS == 64 ? kg : (kg & 1);
+      const int col = tx + (CS == 64 ? 0 : (kg >> 1)) + ((hr * WO) & 15);
+      base[i][r] = ((hr * NCH + chunk) * HWp + col) * 16;
+    }
+  }
+  // Halo staging: 16-B global loads in PIXEL-major order (8 lanes per 128-B line: full-line,
+  // coalesced reads; out-of-image pixels read as zero through the buffer range check), written to
+  // the chunk-major LDS image by ds_write_b128 after the MFMAs of the tile before.  (LDS-DMA must
+  // write LDS in lane order, so it could only fill the chunk-major image by gathering 16 B from 64
+  // different lines per instruction: ~5 us per tile, slower than the MFMAs.)
+  // one wave-instruction = PPI consecutive pixels x all NCH chunks = 1 KB of contiguous global
+  // memory; lane -> (pixel lane % PPI, chunk lane / PPI), so the 8 lanes of each ds_write_b128 lane
+  // group store one chunk of 8 consecutive pixels: 8 consecutive slots, no bank conflict
+  constexpr int NPIX = HR * HWd, NSLOT = NPIX * NCH, PPI = 64 / NCH;
+  constexpr int NLD = (NSLOT + NT - 1) / NT;
+  uint4 stg[NLD];
+  auto load_halo = [&](int t) {
+    const int n_img = fdiv(t, g.fd_timg);
+    const int y0 = (t - n_img * g.tiles_img) * TR - g.padT;
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int pix = (l * NT + wid * 64) / NCH + lane % PPI, c = lane / PPI;
+      const int hr = pix / HWd, hc = pix % HWd;
+      const int y = y0 + hr, x = hc - g.padL;
+      const bool ok = pix < NPIX && (unsigned)y < (unsigned)g.Hs && (unsigned)x < (unsigned)g.Ws;
+      stg[l] = bload16(rs, ok ? (unsigned)((((n_img * g.Hs + y) * g.Ws + x) * CS + c * 8) * 2) : kOOB);
+    }
+  };
+  auto store_halo = [&](char* dst) {
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+      const int pix = (l * NT + wid * 64) / NCH + lane % PPI, c = lane / PPI;
+      if (NSLOT % NT == 0 || pix < NPIX) {
+        const int hr = pix / HWd, hc = pix % HWd;
+        *reinterpret_cast<uint4*>(dst + ((hr * NCH + c) * HWp + hc + ((hr * WO) & 15)) * 16) = stg[l];
+      }
+    }
+  };
+  const int per = (g.tiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(g.tiles, t0 + per);
+  if (t0 < t1) {
+    load_halo(t0);
+    store_halo(smem);
+  }
+  auto ystore = [&](int tp, int l) {   // chunk l of this thread: ytile -> global (tile tp)
+    const int q = l * NT + tid, pix = q >> 3, c = q & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(ytile + pix * 128 + ((c ^ (pix & 7)) << 4));
+    *reinterpret_cast<uint4*>(yout + (size_t)tp * BM * BN + (size_t)q * 8) = v;
+  };
+  for (int t = t0, it = 0; t < t1; ++t, ++it) {
+    char* cur = smem + (it & 1) * LDS_BYTES;
+    lds_sync();   // the halo of this tile is in LDS; every wave is done reading the other buffer
+    const bool more = t + 1 < t1;
+    if (more) load_halo(t + 1);   // in flight during this tile's MFMAs
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // software pipeline one K32 chunk deep: chunk kt+1's fragment reads are issued before chunk
+    // kt's MFMAs; the scheduling barrier keeps the compiler from hoisting every chunk's reads to
+    // the top of the unrolled loop (126 live fragments -> spills)
+    bf16x8 fa[2][TM];
+    auto load_frags = [&](int kt, bf16x8 (&f)[TM]) {
+      const int r = kt * 32 / (RS * CS);
+      int off;   // lane-uniform slot offset inside filter row r
+      if constexpr (CS == 64) off = ((kt % 2) * 4) * HWp + (kt / 2) % RS;
+      else off = (kt % (RS / 2)) * 2;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        f[i] = *reinterpret_cast<const bf16x8*>(cur + base[i][r] + off * 16);
+    };
+    // chunk order: with FLIP the taps run mirrored, so the implicit-GEMM DGRAD's accumulation order
+    // (its taps ascending) is kept and the two kernels agree bitwise
+    constexpr int CH = CS / 32 > 0 ? CS / 32 : 1;
+    auto chunk = [&](int u) {
+      if constexpr (!FLIP || CS < 32) return u;
+      const int kr = u / (RS * CH), ks = (u / CH) % RS, cc = u % CH;
+      return ((RS - 1 - kr) * RS + (RS - 1 - ks)) * CH + cc;
+    };
+    load_frags(chunk(0), fa[0]);
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      if (u + 1 < KC) load_frags(chunk(u + 1), fa[(u + 1) & 1]);
+      const int kt = chunk(u);
+      if constexpr (OVL)
+        if (u < NYS && it > 0) ystore(t - 1, u);   // the previous tile's output, one chunk per step
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[kt][j], fa[u & 1][i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (OVL) {
+      lds_sync();   // every wave has read the previous tile out of ytile
+      if (more) store_halo(smem + ((it + 1) & 1) * LDS_BYTES);
+      // bf16 rounding (the value stored) + per-channel sums of the rounded values, as the shared
+      // epilogue does; 8 channels per lane and pixel fragment -> one 16-B LDS store
+      const int fr = lane & 15, fq = lane >> 4;
+      float sm[2][TN][4];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pl = wr * WTM + i * 16 + fr;
+        unsigned ov[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = q >> 1, e0 = (q & 1) * 2;
+          const unsigned u = f2bf2(acc[j][i][e0], acc[j][i][e0 + 1]);
+          if constexpr (EPI == EPI_STATS) {
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+            sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
+          }
+          ov[q] = u;
+        }
+        const int c = wc * 4 + fq;   // 16-B chunk: channels wc*32 + fq*8 .. +7 (PAIR order)
+        *reinterpret_cast<uint4*>(ytile + pl * 128 + ((c ^ (pl & 7)) << 4)) = *reinterpret_cast<const uint4*>(ov);
+      }
+      if constexpr (EPI == EPI_STATS) {
+        float* red = reinterpret_cast<float*>(scratch);   // [WM][2][BN]
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = row16_sum(sm[k][j][e]);
+            if (fr == 0) *reinterpret_cast<f32x4*>(red + (wr * 2 + k) * BN + wc * 32 + fq * 8 + j * 4) = v;
+          }
+        lds_sync();
+        if (tid < BN) {
+          float* st = p.stats + (size_t)t * 2 * BN;
+          st[tid] = red[0 * BN + tid] + red[2 * BN + tid];
+          st[BN + tid] = red[1 * BN + tid] + red[3 * BN + tid];
+        }
+      }
+    } else {
+      if (more) store_halo(smem + ((it + 1) & 1) * LDS_BYTES);
+      igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, 2, true>(p, acc, scratch, tid, t * BM, 0, t, 0);
+    }
+  }
+  if constexpr (OVL) {
+    if (t0 < t1) {
+      lds_sync();
+#pragma unroll
+      for (int l = 0; l < NYS; ++l) ystore(t1 - 1, l);
+    }
+  }
+  wait_vm<0>();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Skinny FWD kernel for batch-1 inference (M = output pixels <= a few hundred: ResNet-50 layer 3/4
 // and the classifier at batch 1).  Those GEMMs are latency-bound: a block has only a few K-steps
 // of tiny MFMA work, so what matters is how many operand loads are in flight, not data reuse.  No
@@ -1725,6 +1964,97 @@ static void launch_stream(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
+// halo-tiled direct conv for the layer-1 3x3 / stem shapes: bit 0 FWD, bit 1 DGRAD.  DGRAD is off:
+// its BN-backward epilogue loads stall the one wave per SIMD (profiles/r2_halo_conv.txt)
+static Knob kn_halo("halo", 1);
+static Knob kn_halo_ovl("halo_ovl", 1);   // output stores overlapped with the next tile's MFMAs
+
+// Eligibility + geometry of halo_conv_kernel: stride 1, square filter, 64 output channels and
+// (C, R) = (64, 3) [layer-1 3x3, FWD and DGRAD] or (16, 4) [space-to-depth stem, FWD]; the output
+// width divides 224 (a tile = whole rows) and the grid has at least one tile per CU.
+static bool halo_geom(int mode, const IgemmParams& p, HaloGeom& g) {
+  const int hk = kn_halo.get();
+  if (!(hk & (mode == MODE_FWD ? 1 : 2)) || mode == MODE_WGRAD || p.nsplit != 1 || p.stride != 1 || p.R != p.S || p.gn != 64 ||
+      p.grp != 0 || p.sub)
+    return false;
+  int CS, pad;
+  if (mode == MODE_FWD) {
+    CS = p.C; g.Hs = p.H; g.Ws = p.W; g.Ho = p.P; g.Wo = p.Q; pad = p.pad;
+    if (p.bias) return false;
+  } else {
+    CS = p.K; g.Hs = p.P; g.Ws = p.Q; g.Ho = p.H; g.Wo = p.W; pad = p.R - 1 - p.pad;
+    if (p.bn_x2 || pad < 0) return false;
+  }
+  // compiled geometries: layer-1 3x3 at 56 wide, the space-to-depth stem at 112 wide
+  if (!((CS == 64 && p.R == 3 && g.Wo == 56) || (CS == 16 && p.R == 4 && g.Wo == 112 && mode == MODE_FWD)))
+    return false;
+  g.TR = HALO_BM / g.Wo;
+  if (g.Ho % g.TR != 0 || g.Ho != g.Hs + 2 * pad - p.R + 1 || g.Wo != g.Ws + 2 * pad - p.S + 1) return false;
+  g.tiles_img = g.Ho / g.TR;
+  g.tiles = p.N * g.tiles_img;
+  if (g.tiles < 256 || (int64_t)g.tiles * HALO_BM != (int64_t)p.gm) return false;
+  g.padT = pad; g.padL = pad;
+  g.HWd = g.Wo + p.S - 1;
+  g.HWp = (g.HWd + 15 + 15) / 16 * 16;    // room for the 0..15-slot row skew, multiple of 16
+  g.HR = g.TR + p.R - 1;
+  g.ninstr = ceil_div(g.HR * (CS / 8) * g.HWp * 16, 1024);
+  g.lds_bytes = g.ninstr * 1024;
+  if (2 * g.lds_bytes + HALO_BM * 64 * 2 + 768 * (int)sizeof(float) > 160 * 1024) return false;
+  g.src = p.a; g.src_bytes = p.a_bytes; g.wsrc = p.b;
+  g.fd_HWp = make_fastdiv(g.HWp);
+  g.fd_Wo = make_fastdiv(g.Wo);
+  g.fd_timg = make_fastdiv(g.tiles_img);
+  return true;
+}
+static bool use_halo(int mode, const IgemmParams& p) {
+  HaloGeom g;
+  return halo_geom(mode, p, g);
+}
+
+template <int MODE>
+static void launch_halo(IgemmParams& p, hipStream_t st) {
+  HaloGeom g;
+  TORCH_CHECK(halo_geom(MODE, p, g), "halo_conv: shape not eligible");
+  p.tiles_m = g.tiles;
+  p.tiles_n = 1;
+  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "halo_conv: partial-stats buffer too small");
+  const int grid = std::min(g.tiles, 256);
+  size_t smem = (size_t)2 * g.lds_bytes + 768 * sizeof(float);
+  const int CS = MODE == MODE_FWD ? p.C : p.K;
+#define PCMP_HALO_LAUNCH(E, C_, R_, FL, WO_, OV)                                                       \
+  do {                                                                                                 \
+    auto kfn = &halo_conv_kernel<MODE, E, C_, R_, FL, WO_, OV>;                                        \
+    static bool attr_set = false;                                                                      \
+    if (!attr_set) {                                                                                   \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                           \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));     \
+      attr_set = true;                                                                                 \
+    }                                                                                                  \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p, g);                                     \
+  } while (0)
+  if constexpr (MODE == MODE_FWD) {
+    const bool ovl = !p.resid && !p.relu && !p.bias && kn_halo_ovl.get();
+    if (ovl) smem += (size_t)HALO_BM * 64 * 2;
+    if (CS == 64) {
+      if (ovl) {
+        if (p.stats) PCMP_HALO_LAUNCH(EPI_STATS, 64, 3, false, 56, true); else PCMP_HALO_LAUNCH(EPI_PLAIN, 64, 3, false, 56, true);
+      } else {
+        if (p.stats) PCMP_HALO_LAUNCH(EPI_STATS, 64, 3, false, 56, false); else PCMP_HALO_LAUNCH(EPI_PLAIN, 64, 3, false, 56, false);
+      }
+    } else {
+      if (ovl) {
+        if (p.stats) PCMP_HALO_LAUNCH(EPI_STATS, 16, 4, false, 112, true); else PCMP_HALO_LAUNCH(EPI_PLAIN, 16, 4, false, 112, true);
+      } else {
+        if (p.stats) PCMP_HALO_LAUNCH(EPI_STATS, 16, 4, false, 112, false); else PCMP_HALO_LAUNCH(EPI_PLAIN, 16, 4, false, 112, false);
+      }
+    }
+  } else if constexpr (MODE == MODE_DGRAD) {
+    if (p.bn_x) PCMP_HALO_LAUNCH(EPI_BNR, 64, 3, true, 56, false); else PCMP_HALO_LAUNCH(EPI_PLAIN, 64, 3, true, 56, false);
+  }
+#undef PCMP_HALO_LAUNCH
+  PCMP_LAUNCH_CHECK();
+}
+
 // 0: not used; 1: 128x128; 2: 128x64 (narrow outputs)
 static int use_stream(int mode, const IgemmParams& p) {
   const int mk = kn_stream_maxk.get();
@@ -1794,6 +2124,7 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
 static int igemm_bm(int mode, const IgemmParams& p) {
+  if (use_halo(mode, p)) return HALO_BM;
   if (use_stream(mode, p)) return 128;
   if (use_igemm8(mode, p)) return BM8;
   if (use_bm64_smallgrid(mode, p)) return 64;
@@ -1804,6 +2135,7 @@ static int igemm_bm(int mode, const IgemmParams& p) {
 template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE != MODE_WGRAD) {
+    if (use_halo(MODE, p)) { launch_halo<MODE>(p, st); return; }
     switch (use_stream(MODE, p)) {
       case 1: launch_stream<MODE, 128, 128, 2, 2>(p, st); return;
       case 2: launch_stream<MODE, 128, 64, 2, 2>(p, st); return;

@@ -572,3 +572,62 @@ def test_synth_images_vs_reference(gpu):
     assert torch.equal(y.cpu(), ds.labels(torch.arange(8)))
     x2, _ = ds.get_batch(list(range(8)))
     assert torch.equal(x, x2)          # deterministic per (seed, index window)
+
+
+def _with_knob(name, value, fn):
+    old = _ops().set_knob(name, value)
+    try:
+        return fn()
+    finally:
+        _ops().set_knob(name, old)
+
+
+@pytest.mark.parametrize("case", ["l1_3x3", "stem_s2d"])
+@pytest.mark.parametrize("epi", ["stats", "plain", "resid_relu"])
+def test_halo_conv_fwd_matches_igemm_and_reference(gpu, case, epi):
+    """halo_conv_kernel (stride-1 narrow-channel direct conv) == the implicit-GEMM kernel bitwise
+    (same K32 chunks in the same order), and close to the fp32 reference; BN statistics partials
+    (per 224-pixel tile instead of per 128) sum to the same column totals."""
+    if case == "l1_3x3":
+        N, H, C, R, pad = 20, 56, 64, 3, 1      # 20 * 56/4 = 280 tiles >= 256
+    else:
+        N, H, C, R, pad = 5, 115, 16, 4, 0      # space-to-depth stem: 115 -> 112, 5 * 56 = 280 tiles
+    x = rnd(N, H, H, C, dev=gpu)
+    w = rnd(64, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+    stats = epi == "stats"   # stats / plain: the overlapped-output variant; resid_relu: shared epilogue
+    res = rnd(N, H + 2 * pad - R + 1, H + 2 * pad - R + 1, 64, dev=gpu) if epi == "resid_relu" else None
+    run = lambda: _ops().conv_fwd(x, w, 1, pad, None, res, epi == "resid_relu", stats)
+    got = _with_knob("halo", 1, run)
+    base = _with_knob("halo", 0, run)
+    assert torch.equal(got[0], base[0])
+    yr = ref.conv_fwd(x, w, 1, pad, None, res, epi == "resid_relu", stats)
+    close(got[0], yr[0])
+    if stats:
+        assert got[1].shape[0] == N * (H + 2 * pad - R + 1) ** 2 // 224   # one partial row per halo tile
+        close(got[1].sum(0), base[1].sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("bnr", [True, False])
+def test_halo_conv_dgrad_matches_igemm(gpu, bnr):
+    """Layer-1 3x3 DGRAD on the halo kernel (tap-mirrored transposed weights, pad' = R-1-pad) ==
+    the implicit-GEMM DGRAD bitwise, with and without the fused BN-backward reduction."""
+    N, H, C = 20, 56, 64
+    dy = rnd(N, H, H, C, dev=gpu)
+    w = rnd(C, 3, 3, C, dev=gpu, scale=(2.0 / (9 * C)) ** 0.5)
+    x = rnd(N, H, H, C, dev=gpu)
+    mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    sc, sh = torch.randn(C, device=gpu), torch.randn(C, device=gpu) * 0.5
+    if bnr:
+        run = lambda: _ops().conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, x, mean, invstd, None, None, None, sc, sh)
+    else:
+        run = lambda: [_ops().conv_dgrad(dy, w, H, H, 1, 1, None)]
+    got = _with_knob("halo", 3, run)
+    base = _with_knob("halo", 0, run)
+    assert torch.equal(got[0], base[0])
+    if bnr:
+        assert got[1].shape[0] == N * H * H // 224
+        close(got[1].sum(0), base[1].sum(0), rtol=1e-4, atol=1e-2)
+        outr = ref.conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, x, mean, invstd, None, None, None, sc, sh)
+        close(got[0], outr[0])
+    else:
+        close(got[0], ref.conv_dgrad(dy, w, H, H, 1, 1, None))

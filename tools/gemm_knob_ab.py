@@ -18,6 +18,7 @@ from pcmp.ops import _lib  # noqa: E402
 
 # name, N, H, W, Cin, Cout, R, stride, pad
 SHAPES = [
+    ("stem_s2d_4x4_16to64", 256, 115, 115, 16, 64, 4, 1, 0),
     ("l1_1x1_64to256", 256, 56, 56, 64, 256, 1, 1, 0),
     ("l1_1x1_256to64", 256, 56, 56, 256, 64, 1, 1, 0),
     ("l1_3x3_64", 256, 56, 56, 64, 64, 3, 1, 1),
