@@ -1351,6 +1351,21 @@ __global__ void __launch_bounds__(NT, 1) halo_conv_kernel(const IgemmParams p, c
     load_halo(t0);
     store_halo(smem);
   }
+  // DGRAD OVL (BN-backward reduction with the ReLU mask recomputed from x): per lane the 8 channels
+  // wc*32 + fq*8.. of its fragments; their (istd, -mean*istd, mask scale, mask shift) are staged
+  // in LDS once, and the tile's x values (7 x 16 B per lane) are loaded right after its MFMAs
+  constexpr bool DBNR = OVL && MODE == MODE_DGRAD;
+  float* ctab = reinterpret_cast<float*>(scratch) + 4 * BN;   // [4][BN] after the [2][2][BN] sums
+  if constexpr (DBNR) {
+    if (tid < BN) {
+      const float is = p.bn_istd[tid];
+      ctab[tid] = is;
+      ctab[BN + tid] = -p.bn_mean[tid] * is;
+      ctab[2 * BN + tid] = p.bn_msc[tid];
+      ctab[3 * BN + tid] = p.bn_msh[tid];
+    }
+  }
+  uint4 xv[DBNR ? TM : 1];
   auto ystore = [&](int tp, int l) {   // chunk l of this thread: ytile -> global (tile tp)
     const int q = l * NT + tid, pix = q >> 3, c = q & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(ytile + pix * 128 + ((c ^ (pix & 7)) << 4));
@@ -1401,6 +1416,13 @@ __global__ void __launch_bounds__(NT, 1) halo_conv_kernel(const IgemmParams p, c
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[kt][j], fa[u & 1][i], acc[j][i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (DBNR) {   // (after the MFMAs: prefetched under them it spills the weight registers)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pl = wr * WTM + i * 16 + (lane & 15);
+        xv[i] = *reinterpret_cast<const uint4*>(p.bn_x + ((size_t)t * BM + pl) * BN + wc * 32 + (lane >> 4) * 8);
+      }
+    }
     if constexpr (OVL) {
       lds_sync();   // every wave has read the previous tile out of ytile
       if (more) store_halo(smem + ((it + 1) & 1) * LDS_BYTES);
@@ -1414,6 +1436,19 @@ __global__ void __launch_bounds__(NT, 1) halo_conv_kernel(const IgemmParams p, c
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int e = 0; e < 4; ++e) sm[k][j][e] = 0.f;
+      float ka[DBNR ? 8 : 1], kb[DBNR ? 8 : 1], ms[DBNR ? 8 : 1], mh[DBNR ? 8 : 1];
+      if constexpr (DBNR) {   // this lane's 8 channels, once per tile
+        const int ch = wc * 32 + fq * 8;
+#pragma unroll
+        for (int e = 0; e < 8; e += 4) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(ctab + ch + e);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(ctab + BN + ch + e);
+          const f32x4 c = *reinterpret_cast<const f32x4*>(ctab + 2 * BN + ch + e);
+          const f32x4 d = *reinterpret_cast<const f32x4*>(ctab + 3 * BN + ch + e);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { ka[e + k] = a[k]; kb[e + k] = b[k]; ms[e + k] = c[k]; mh[e + k] = d[k]; }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int pl = wr * WTM + i * 16 + fr;
@@ -1421,8 +1456,18 @@ __global__ void __launch_bounds__(NT, 1) halo_conv_kernel(const IgemmParams p, c
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int j = q >> 1, e0 = (q & 1) * 2;
-          const unsigned u = f2bf2(acc[j][i][e0], acc[j][i][e0 + 1]);
-          if constexpr (EPI == EPI_STATS) {
+          unsigned u = f2bf2(acc[j][i][e0], acc[j][i][e0 + 1]);
+          if constexpr (DBNR) {   // g = round(dgrad) where relu(x*msc+msh) > 0; sums of g, g*xhat
+            const int ce = 2 * q;
+            const unsigned xw = (&xv[i].x)[q];
+            const float xa = __uint_as_float(xw << 16), xb = __uint_as_float(xw & 0xffff0000u);
+            const float z0 = fmaf(xa, ms[ce], mh[ce]), z1 = fmaf(xb, ms[ce + 1], mh[ce + 1]);
+            u &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
+            const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+            sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
+            sm[1][j][e0] += r0 * fmaf(xa, ka[ce], kb[ce]);
+            sm[1][j][e0 + 1] += r1 * fmaf(xb, ka[ce + 1], kb[ce + 1]);
+          } else if constexpr (EPI == EPI_STATS) {
             const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
             sm[0][j][e0] += r0; sm[0][j][e0 + 1] += r1;
             sm[1][j][e0] += r0 * r0; sm[1][j][e0 + 1] += r1 * r1;
@@ -1432,7 +1477,7 @@ __global__ void __launch_bounds__(NT, 1) halo_conv_kernel(const IgemmParams p, c
         const int c = wc * 4 + fq;   // 16-B chunk: channels wc*32 + fq*8 .. +7 (PAIR order)
         *reinterpret_cast<uint4*>(ytile + pl * 128 + ((c ^ (pl & 7)) << 4)) = *reinterpret_cast<const uint4*>(ov);
       }
-      if constexpr (EPI == EPI_STATS) {
+      if constexpr (EPI == EPI_STATS || DBNR) {
         float* red = reinterpret_cast<float*>(scratch);   // [WM][2][BN]
 #pragma unroll
         for (int k = 0; k < 2; ++k)
@@ -1964,17 +2009,23 @@ static void launch_stream(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
-// halo-tiled direct conv for the layer-1 3x3 / stem shapes: bit 0 FWD, bit 1 DGRAD.  DGRAD is off:
-// its BN-backward epilogue loads stall the one wave per SIMD (profiles/r2_halo_conv.txt)
+// halo-tiled direct conv for the layer-1 3x3 / stem shapes: bit 0 FWD, bit 1 every DGRAD variant,
+// bit 2 the overlapped BN-backward DGRAD.  DGRAD is off by default: its BN-backward epilogue loads
+// stall the one wave per SIMD (profiles/r2_halo_conv.txt)
 static Knob kn_halo("halo", 1);
 static Knob kn_halo_ovl("halo_ovl", 1);   // output stores overlapped with the next tile's MFMAs
+
+static bool halo_dgrad_ovl(const IgemmParams& p) {
+  return kn_halo_ovl.get() && p.bn_x && !p.bn_x2 && !p.resid && !p.relu && !p.bn_mask && !p.bn_mbits && p.bn_msc &&
+         p.bn_msh;
+}
 
 // Eligibility + geometry of halo_conv_kernel: stride 1, square filter, 64 output channels and
 // (C, R) = (64, 3) [layer-1 3x3, FWD and DGRAD] or (16, 4) [space-to-depth stem, FWD]; the output
 // width divides 224 (a tile = whole rows) and the grid has at least one tile per CU.
 static bool halo_geom(int mode, const IgemmParams& p, HaloGeom& g) {
   const int hk = kn_halo.get();
-  if (!(hk & (mode == MODE_FWD ? 1 : 2)) || mode == MODE_WGRAD || p.nsplit != 1 || p.stride != 1 || p.R != p.S || p.gn != 64 ||
+  if ((mode == MODE_FWD && !(hk & 1)) || (mode == MODE_DGRAD && !(hk & 6)) || mode == MODE_WGRAD || p.nsplit != 1 || p.stride != 1 || p.R != p.S || p.gn != 64 ||
       p.grp != 0 || p.sub)
     return false;
   int CS, pad;
@@ -1984,6 +2035,9 @@ static bool halo_geom(int mode, const IgemmParams& p, HaloGeom& g) {
   } else {
     CS = p.K; g.Hs = p.P; g.Ws = p.Q; g.Ho = p.H; g.Wo = p.W; pad = p.R - 1 - p.pad;
     if (p.bn_x2 || pad < 0) return false;
+    // bit 1 enables every DGRAD variant, bit 2 only the overlapped BN-backward form (mask
+    // recomputed from x, no residual)
+    if (!(hk & 2) && !((hk & 4) && halo_dgrad_ovl(p))) return false;
   }
   // compiled geometries: layer-1 3x3 at 56 wide, the space-to-depth stem at 112 wide
   if (!((CS == 64 && p.R == 3 && g.Wo == 56) || (CS == 16 && p.R == 4 && g.Wo == 112 && mode == MODE_FWD)))
@@ -2049,7 +2103,14 @@ static void launch_halo(IgemmParams& p, hipStream_t st) {
       }
     }
   } else if constexpr (MODE == MODE_DGRAD) {
-    if (p.bn_x) PCMP_HALO_LAUNCH(EPI_BNR, 64, 3, true, 56, false); else PCMP_HALO_LAUNCH(EPI_PLAIN, 64, 3, true, 56, false);
+    if (halo_dgrad_ovl(p)) {
+      smem += (size_t)HALO_BM * 64 * 2;
+      PCMP_HALO_LAUNCH(EPI_BNR, 64, 3, true, 56, true);
+    } else if (p.bn_x) {
+      PCMP_HALO_LAUNCH(EPI_BNR, 64, 3, true, 56, false);
+    } else {
+      PCMP_HALO_LAUNCH(EPI_PLAIN, 64, 3, true, 56, false);
+    }
   }
 #undef PCMP_HALO_LAUNCH
   PCMP_LAUNCH_CHECK();

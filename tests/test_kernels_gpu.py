@@ -621,9 +621,19 @@ def test_halo_conv_dgrad_matches_igemm(gpu, bnr):
         run = lambda: _ops().conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, x, mean, invstd, None, None, None, sc, sh)
     else:
         run = lambda: [_ops().conv_dgrad(dy, w, H, H, 1, 1, None)]
-    got = _with_knob("halo", 3, run)
     base = _with_knob("halo", 0, run)
-    assert torch.equal(got[0], base[0])
+    # halo=4: only the overlapped BN-backward form (mask from x, no residual); halo=3 with and
+    # without the overlapped output path: every DGRAD variant
+    for knobs in ({"halo": 4}, {"halo": 3}, {"halo": 3, "halo_ovl": 0}):
+        olds = {k: _ops().set_knob(k, v) for k, v in knobs.items()}
+        try:
+            got = run()
+        finally:
+            for k, v in olds.items():
+                _ops().set_knob(k, v)
+        assert torch.equal(got[0], base[0]), knobs
+        if bnr:
+            close(got[1].sum(0), base[1].sum(0), rtol=1e-4, atol=1e-2)
     if bnr:
         assert got[1].shape[0] == N * H * H // 224
         close(got[1].sum(0), base[1].sum(0), rtol=1e-4, atol=1e-2)

@@ -74,6 +74,13 @@ def build_cases(modes, only):
                 return ops.conv_dgrad_bnr(dy, w, H, W, s, p, res.clone() if s == 2 else res, None, xb, mean, istd,
                                           None, None, None, None, None, None, bits)
             cases.append((f"dgrad_bnr {name}", flops, byts, dg))
+            if s == 1 and R == 3:
+                # intermediate-layer form (the model's conv2 DGRAD): mask recomputed from x, no residual
+                msc, msh = torch.rand(C, device=dev, generator=g) + 0.5, torch.randn(C, device=dev, generator=g) * 0.1
+
+                def dgm(dy=dy, w=w, H=H, W=W, p=p, xb=xb, mean=mean, istd=istd, msc=msc, msh=msh):
+                    return ops.conv_dgrad_bnr(dy, w, H, W, 1, p, None, None, xb, mean, istd, None, None, None, msc, msh)
+                cases.append((f"dgrad_bnr_mfx {name}", flops, (dy.numel() + 2 * xb.numel()) * 2, dgm))
         if "wgrad" in modes:
             out = torch.zeros(K, R, R, C, device=dev)
             byts = (x.numel() + dy.numel()) * 2 + out.numel() * 4
