@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2 re-entry verification: full GPU test suite, smoke, flagship bench, per-layer profile.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
+timeout -k 10 300 python tools/layer_profile.py --model resnet50 --batch 256 --top 60 > gpurun_out/layer_profile.txt 2>&1 || { echo "layer profile failed"; tail -20 gpurun_out/layer_profile.txt; exit 1; }
+head -30 gpurun_out/layer_profile.txt
