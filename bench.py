@@ -39,14 +39,14 @@ import os
 import sys
 import time
 
-# before the HIP runtime initialises: one hardware queue per stream (compute, WGRAD side, DDP comm,
-# RCCL) instead of HIP's default 4 shared round-robin (see pcmp/__init__.py)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# before the HIP runtime initialises: importing pcmp raises GPU_MAX_HW_QUEUES to >= 8, one hardware
+# queue per stream (compute, WGRAD side, DDP comm, RCCL) instead of the pool's exported 4 shared
+# round-robin (pcmp/__init__.py)
+import pcmp  # noqa: E402,F401
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 STOCK_TORCH_IMG_PER_SEC = {"resnet50": 6540.0, "resnet18": 16850.0}  # BASELINE.md self-baseline, 1 GPU, B=256
 

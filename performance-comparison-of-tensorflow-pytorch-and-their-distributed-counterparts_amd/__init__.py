@@ -3,14 +3,36 @@
 Process-level HIP runtime settings are applied here, at import, because the HIP runtime reads them
 once when it initialises (the first device query), before any pcmp or torch.cuda call:
 
-* ``GPU_MAX_HW_QUEUES`` (default 8 here, HIP's own default is 4): every HIP stream is bound to a
-  hardware queue when it is created, round-robin over this many.  A pcmp training process uses
-  the compute stream, the WGRAD/downsample side stream, the DDP comm stream and RCCL's streams;
-  with 4 queues the side stream landed on the compute stream's queue once the RCCL streams
-  existed, which serialises WGRAD behind DGRAD and RCCL's ring kernels behind backward (measured:
-  ResNet-50 22.3 -> 25.3 ms/step with the forced RCCL path, all step kernels on one queue in the
-  rocprofv3 trace, ``profiles/r2_ddp_force_queues.txt``).  An explicit setting is kept.
+* ``GPU_MAX_HW_QUEUES`` (at least 8 here; HIP's own default, and the value the GPU pool exports, is
+  4): every HIP stream is bound to a hardware queue when it is created, round-robin over this many.
+  A pcmp training process uses the compute stream, the WGRAD/downsample side stream, the DDP comm
+  stream and RCCL's streams; with 4 queues the side stream landed on the compute stream's queue
+  once the RCCL streams existed, which serialises WGRAD behind DGRAD and RCCL's ring kernels behind
+  backward (measured: ResNet-50 22.2 -> 24.9 ms/step with the RCCL path active, all step kernels on
+  one queue in the rocprofv3 trace, ``profiles/r2_ddp_force_queues.txt``).  A smaller inherited
+  value is raised to 8 (a larger one is kept); ``PCMP_HW_QUEUES=<n>`` pins the count exactly.
 """
 import os as _os
 
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+MIN_HW_QUEUES = 8
+
+
+def ensure_hw_queues(environ=_os.environ) -> int:
+    """Set ``GPU_MAX_HW_QUEUES`` for this process (must run before the HIP runtime initialises)."""
+    pin = environ.get("PCMP_HW_QUEUES", "").strip()
+    if pin:
+        try:
+            n = min(32, max(1, int(pin)))
+        except ValueError:
+            n = MIN_HW_QUEUES
+    else:
+        try:
+            cur = int(environ.get("GPU_MAX_HW_QUEUES", "0"))
+        except ValueError:
+            cur = 0
+        n = min(32, max(cur, MIN_HW_QUEUES))
+    environ["GPU_MAX_HW_QUEUES"] = str(n)
+    return n
+
+
+ensure_hw_queues()

@@ -269,3 +269,15 @@ def test_keras_flow_from_directory(tmp_path):
     out = _run("resnet.py", "--data-dir", str(tmp_path), "--image-size", "32", "--batch-size", "4", "--epochs", "1")
     assert "Found 6 images belonging to 3 classes." in out and "the inference takes" in out
     assert _last_json(out)["data"] == "real"
+
+
+def test_hw_queue_floor():
+    """The pool exports GPU_MAX_HW_QUEUES=4: pcmp raises it to 8 (forced-RCCL step 24.9 -> 22.2 ms),
+    keeps a larger inherited value, and PCMP_HW_QUEUES pins it exactly (clamped to 1..32)."""
+    import pcmp
+    for env, want in (({"GPU_MAX_HW_QUEUES": "4"}, 8), ({}, 8), ({"GPU_MAX_HW_QUEUES": "16"}, 16),
+                      ({"GPU_MAX_HW_QUEUES": "4", "PCMP_HW_QUEUES": "4"}, 4),
+                      ({"PCMP_HW_QUEUES": "99"}, 32), ({"GPU_MAX_HW_QUEUES": "x"}, 8)):
+        e = dict(env)
+        assert pcmp.ensure_hw_queues(e) == want
+        assert e["GPU_MAX_HW_QUEUES"] == str(want)
