@@ -87,6 +87,64 @@ __global__ void maxpool_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restr
   }
 }
 
+// The ResNet stem's 3x3 / stride-2 / pad-1 pooling (B=256: 411 MB in, 154 MB out), one thread per
+// (output pixel, 8-channel vector), 32-bit index math, all nine window loads issued before any is
+// consumed (out-of-image taps read a clamped in-image address and are skipped in the fold).  The
+// generic kernel above spends its time in 64-bit divisions and a data-dependent tap loop that
+// serialises the loads: 212 us -> see profiles/r2_pool_ab.txt.  Fold order, NaN and tie handling
+// are the generic kernel's, so values and argmax indices are identical.
+__global__ void __launch_bounds__(256) maxpool3s2_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y,
+                                                             uint8_t* __restrict__ idx, unsigned total, int H, int W,
+                                                             int CV, int P, int Q, const float* __restrict__ sc,
+                                                             const float* __restrict__ sh) {
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= total) return;
+  const unsigned cv = i % (unsigned)CV, pix = i / (unsigned)CV;
+  const unsigned q = pix % (unsigned)Q, t = pix / (unsigned)Q;
+  const unsigned p = t % (unsigned)P, n = t / (unsigned)P;
+  const int C = CV * 8;
+  u16x8 raw[9];
+  bool ok[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int h = 2 * (int)p - 1 + r;
+    const bool hok = (unsigned)h < (unsigned)H;
+    const int hc = hok ? h : 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int w = 2 * (int)q - 1 + c;
+      const bool wok = (unsigned)w < (unsigned)W;
+      ok[r * 3 + c] = hok && wok;
+      raw[r * 3 + c] = *reinterpret_cast<const u16x8*>(x + ((n * H + hc) * W + (wok ? w : 0)) * (unsigned)C + cv * 8);
+    }
+  }
+  float best[8], a[8], b[8];
+  int bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    best[e] = -INFINITY; bi[e] = 0;
+    a[e] = sc ? sc[cv * 8 + e] : 1.f;
+    b[e] = sc ? sh[cv * 8 + e] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    if (!ok[j]) continue;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = bf2f(raw[j][e]);
+      if (sc) v = bf2f(f2bf(fmaxf(v * a[e] + b[e], 0.f)));
+      if (v > best[e] || (v != v)) { best[e] = v; bi[e] = j; }
+    }
+  }
+  st8(y + (size_t)i * 8, best);
+  if (idx) {
+    uint64_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) packed |= (uint64_t)(bi[e] & 0xff) << (8 * e);
+    *reinterpret_cast<uint64_t*>(idx + (size_t)i * 8) = packed;
+  }
+}
+
 // gather-form backward: dx[n,h,w,c] = sum of dy over the windows whose argmax is (h,w)
 __global__ void maxpool_bwd_kernel(const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
                                    __bf16* __restrict__ dx, int N, int H, int W, int C, int P, int Q,
@@ -129,8 +187,12 @@ __global__ void maxpool_bwd_kernel(const __bf16* __restrict__ dy, const uint8_t*
 // writes g = bf16(sum of dy over the windows whose argmax is the pixel) * mask and part [T][2][C]
 // = (sum g, sum g * (c - mean) * invstd).  Replaces maxpool_bwd + bn_bwd_reduce (which re-read the
 // gradient and the normalised activation).  Block = 256 threads = rpp pixel rows x tpr channel
-// vectors (C/8 <= 256).
-__global__ void maxpool_bwd_bnr_kernel(const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
+// vectors (C/8 <= 256).  K3S2: the stem's 3x3 / stride-2 / pad-1 window, where input pixel (h, w)
+// lies in output rows p = h/2 .. (h+1)/2 and columns q = w/2 .. (w+1)/2 (1-4 windows, r and c
+// always in range): the candidate loads are issued together, branch-free, and folded in the
+// generic kernel's (p, q) order, so the sums are bitwise the same.
+template <bool K3S2>
+__global__ void __launch_bounds__(256) maxpool_bwd_bnr_kernel(const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx,
                                        const __bf16* __restrict__ cx, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, const float* __restrict__ sc,
                                        const float* __restrict__ sh, __bf16* __restrict__ g_out,
@@ -151,12 +213,35 @@ __global__ void maxpool_bwd_bnr_kernel(const __bf16* __restrict__ dy, const uint
     a[e] = sc[cv * 8 + e]; b[e] = sh[cv * 8 + e];
   }
   if (tr < rpp) {
+#pragma unroll 2
     for (int row = r0 + tr; row < r1; row += rpp) {
-      const int w = row % W;
-      const int t = row / W;
-      const int h = t % H;
-      const int n = t / H;
+      const int w = (unsigned)row % (unsigned)W;
+      const int t = (unsigned)row / (unsigned)W;
+      const int h = (unsigned)t % (unsigned)H;
+      const int n = (unsigned)t / (unsigned)H;
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (K3S2) {
+        const int p0 = h >> 1, q0 = w >> 1;
+        const int p1 = min(P - 1, (h + 1) >> 1), q1 = min(Q - 1, (w + 1) >> 1);
+        const int pp[4] = {p0, p0, p1, p1}, qq[4] = {q0, q1, q0, q1};
+        const bool use[4] = {true, q1 != q0, p1 != p0, p1 != p0 && q1 != q0};
+        uint64_t pk[4];
+        u16x8 gv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned o = (((unsigned)n * P + pp[j]) * Q + qq[j]) * (unsigned)C + cv * 8;
+          pk[j] = *reinterpret_cast<const uint64_t*>(idx + o);
+          gv[j] = *reinterpret_cast<const u16x8*>(dy + o);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!use[j]) continue;
+          const int pos = (h - (2 * pp[j] - 1)) * 3 + (w - (2 * qq[j] - 1));
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((int)((pk[j] >> (8 * e)) & 0xff) == pos) acc[e] += bf2f(gv[j][e]);
+        }
+      } else {
       const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
       const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
       for (int p = p_lo; p <= p_hi; ++p) {
@@ -174,6 +259,7 @@ __global__ void maxpool_bwd_bnr_kernel(const __bf16* __restrict__ dy, const uint
           for (int e = 0; e < 8; ++e)
             if ((int)((packed >> (8 * e)) & 0xff) == pos) acc[e] += gg[e];
         }
+      }
       }
       const size_t oi = (size_t)row * C + cv * 8;
       float xv[8];
@@ -464,6 +550,13 @@ __global__ void image_to_s2d_kernel(const T* __restrict__ x, __bf16* __restrict_
 }
 
 // ---------------------------------------------------------------- host ---------------------------
+// specialised 3x3 / stride-2 / pad-1 pooling kernels (32-bit indexing); knob pool3s2=0 -> generic
+static Knob kn_pool3s2("pool3s2", 1);
+
+static bool pool3s2_ok(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
+  return kn_pool3s2.get() && k == 3 && s == 2 && pad == 1 && x.numel() < (int64_t)INT_MAX;
+}
+
 std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
                                     const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift) {
   PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
@@ -479,9 +572,15 @@ std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, i
   auto y = at::empty({N, P, Q, C}, x.options());
   at::Tensor idx = want_idx ? at::empty({N, P, Q, C}, x.options().dtype(at::kByte)) : at::Tensor();
   const int64_t total = (int64_t)N * P * Q * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
-                     ptr<__bf16>(y), want_idx ? ptr<uint8_t>(idx) : nullptr, N, H, W, C, P, Q, (int)k, (int)s,
-                     (int)pad, bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr);
+  if (pool3s2_ok(x, k, s, pad)) {
+    hipLaunchKernelGGL(maxpool3s2_fwd_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, cur_stream(),
+                       ptr<__bf16>(x), ptr<__bf16>(y), want_idx ? ptr<uint8_t>(idx) : nullptr, (unsigned)total, H, W,
+                       C / 8, P, Q, bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr);
+  } else {
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                       ptr<__bf16>(y), want_idx ? ptr<uint8_t>(idx) : nullptr, N, H, W, C, P, Q, (int)k, (int)s,
+                       (int)pad, bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr);
+  }
   PCMP_LAUNCH_CHECK();
   if (want_idx) return {y, idx};
   return {y};
@@ -519,7 +618,9 @@ std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& 
   const int T = ceil_div(M, rpb);
   auto g = at::empty_like(cx);
   auto part = at::empty({T, 2, C}, cx.options().dtype(at::kFloat));
-  hipLaunchKernelGGL(maxpool_bwd_bnr_kernel, dim3(T), dim3(256), (size_t)rpp * 2 * C * sizeof(float), cur_stream(),
+  auto kfn = pool3s2_ok(cx, k, s, pad) && P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1 ? &maxpool_bwd_bnr_kernel<true>
+                                                                                     : &maxpool_bwd_bnr_kernel<false>;
+  hipLaunchKernelGGL(kfn, dim3(T), dim3(256), (size_t)rpp * 2 * C * sizeof(float), cur_stream(),
                      ptr<__bf16>(dy), ptr<uint8_t>(idx), ptr<__bf16>(cx), ptr<float>(mean), ptr<float>(invstd),
                      ptr<float>(scale), ptr<float>(shift), ptr<__bf16>(g), ptr<float>(part), N, H, W, C, P, Q,
                      (int)k, (int)s, (int)pad, rpb);

@@ -416,6 +416,34 @@ def test_stem_fused_bn_maxpool(gpu):
     close(part.sum(0), pref.sum(0), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("H,W", [(28, 28), (17, 23), (112, 112)])
+def test_pool3s2_specialised(gpu, H, W):
+    """The specialised 3x3/s2/p1 stem pooling kernels (knob pool3s2) == the generic kernels, bitwise:
+    plain and BN-prologue forward (values + argmax, with ties and a NaN), fused backward (g + partials)."""
+    ops = _ops()
+    torch.manual_seed(H * W)
+    N, C = 2 if H > 100 else 3, 64
+    c = rnd(N, H, W, C, dev=gpu)
+    c[0, 1:3, 1:3, :8] = 0.5                  # ties inside a window
+    c[1, 4, 5, 9] = float("nan")
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3
+    mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    res = {}
+    try:
+        for v in (0, 1):
+            ops.set_knob("pool3s2", v)
+            y, i = ops.maxpool_fwd(c, 3, 2, 1, True)
+            yb, ib = ops.maxpool_fwd(c, 3, 2, 1, True, sc, sh)
+            dy = torch.Generator(device=gpu).manual_seed(7)
+            dy = torch.randn(yb.shape, device=gpu, generator=dy).to(torch.bfloat16)
+            g, part = ops.maxpool_bwd_bnr(dy, ib, c, mean, invstd, sc, sh, 3, 2, 1)
+            res[v] = (y, i, yb, ib, g, part)
+    finally:
+        ops.set_knob("pool3s2", 1)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b) or (a.is_floating_point() and torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0)))
+
+
 @pytest.mark.parametrize("src", ["f32", "u8", "nhwc"])
 def test_image_to_s2d(gpu, src):
     """Stem space-to-depth kernel == the PyTorch reference (NCHW f32 / u8 with scale, NHWC bf16)."""
