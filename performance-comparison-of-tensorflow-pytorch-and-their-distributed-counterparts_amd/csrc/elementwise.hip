@@ -522,9 +522,15 @@ __global__ void image_to_s2d_kernel(const T* __restrict__ x, __bf16* __restrict_
   const int64_t total = (int64_t)N * Hs * Ws;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int j = t % Ws;
-    const int64_t r = t / Ws;
-    const int i = r % Hs, n = r / Hs;
+    int j, i, n;
+    if (total < INT_MAX) {   // 32-bit index math (64-bit division is a long VALU sequence)
+      const unsigned u = (unsigned)t, r = u / (unsigned)Ws;
+      j = u - r * (unsigned)Ws; i = r % (unsigned)Hs; n = r / (unsigned)Hs;
+    } else {
+      j = t % Ws;
+      const int64_t r = t / Ws;
+      i = r % Hs; n = r / Hs;
+    }
     float v[16];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
@@ -755,15 +761,15 @@ at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c1
   const int64_t total = (int64_t)N * Hs * Ws;
   if (nhwc) {
     PCMP_CHECK_BF16(x);
-    hipLaunchKernelGGL((image_to_s2d_kernel<__bf16, true>), dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+    hipLaunchKernelGGL((image_to_s2d_kernel<__bf16, true>), dim3(grid_for(total, 256, INT_MAX)), dim3(256), 0, cur_stream(),
                        ptr<__bf16>(x), ptr<__bf16>(y), N, Cin, H, W, Cs, Hs, Ws, (int)pad, 1.f, nullptr, nullptr);
   } else if (x.scalar_type() == at::kFloat) {
-    hipLaunchKernelGGL((image_to_s2d_kernel<float, false>), dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+    hipLaunchKernelGGL((image_to_s2d_kernel<float, false>), dim3(grid_for(total, 256, INT_MAX)), dim3(256), 0, cur_stream(),
                        ptr<float>(x), ptr<__bf16>(y), N, Cin, H, W, 0, Hs, Ws, (int)pad, (float)scale,
                        optr<float>(mean), optr<float>(stdv));
   } else {
     TORCH_CHECK(x.scalar_type() == at::kByte, "image_to_s2d: f32 or u8 NCHW input");
-    hipLaunchKernelGGL((image_to_s2d_kernel<uint8_t, false>), dim3(grid_for(total)), dim3(256), 0, cur_stream(),
+    hipLaunchKernelGGL((image_to_s2d_kernel<uint8_t, false>), dim3(grid_for(total, 256, INT_MAX)), dim3(256), 0, cur_stream(),
                        ptr<uint8_t>(x), ptr<__bf16>(y), N, Cin, H, W, 0, Hs, Ws, (int)pad, (float)scale,
                        optr<float>(mean), optr<float>(stdv));
   }
