@@ -104,6 +104,9 @@ constexpr int NT = 256;
 // DGRAD + BN-backward-reduce epilogue: register-ring depth of its resid / x / mask loads (2 = one
 // step ahead, round 1; 4 = three steps ahead).  A/B knob (tools/gemm_knob_ab.py).
 static Knob kn_epi_depth("epi_depth", 4);   // measured: profiles/r2_epilogue_depth_ab.txt
+// the dual BN-reduce epilogue (EPI_BNR2) at depth 4 needs 256 VGPRs and spills; depth 2 fits and
+// is 0-6 % faster (profiles/r2_bnr2_ab.txt)
+static Knob kn_epi_depth_bnr2("epi_depth_bnr2", 2);
 
 // XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // consecutive logical tiles land on the same XCD so they share its L2.
@@ -1824,7 +1827,7 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
       if (deep) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR); }
       else if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR); else PCMP_IGEMM_LAUNCH(false, EPI_BNR);
     } else if (epi == EPI_BNR2) {
-      if (deep) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR2); }
+      if (kn_epi_depth_bnr2.get() >= 4) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR2); }
       else if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH(false, EPI_BNR2);
 #undef PCMP_IGEMM_LAUNCH_D
     } else {
@@ -1908,7 +1911,8 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
 #define PCMP_DMA_LAUNCH(E)                                                                              \
   do {                                                                                                \
     constexpr bool can_deep = (E == EPI_BNR || E == EPI_BNR2) && NTHR == 256;                                        \
-    auto kfn = (can_deep && kn_epi_depth.get() >= 4) ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4> \
+    auto kfn = (can_deep && (E == EPI_BNR2 ? kn_epi_depth_bnr2 : kn_epi_depth).get() >= 4)                         \
+                   ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>                                     \
                                                      : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>; \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
@@ -1973,6 +1977,10 @@ static int use_dma4(int mode, const IgemmParams& p) {
 static Knob kn_stream_maxk("stream_maxk", 4);     // use it for gk/BK <= N K-steps (0 = off)
 static Knob kn_stream_fwd("stream_fwd", 0);       // 1: also for FWD
 static Knob kn_stream_grid("stream_grid", 512);   // resident blocks (2 per CU)
+// dual BN-reduce DGRADs (EPI_BNR2): the streaming kernel spills with that epilogue (256 VGPRs +
+// 112 B scratch per lane) and runs 19-29 % slower than the one-tile kernels: off by default
+// (profiles/r2_bnr2_ab.txt)
+static Knob kn_stream_bnr2("stream_bnr2", 0);
 
 template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_stream(IgemmParams& p, hipStream_t st) {
@@ -2124,6 +2132,7 @@ static int use_stream(int mode, const IgemmParams& p) {
   const int cin = mode == MODE_FWD ? p.C : p.K;
   if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK > mk || p.gm < 4096) return 0;
   if (mode == MODE_DGRAD && !kn_stream_fwd.get() && p.gn < 256) return 0;
+  if (mode == MODE_DGRAD && p.bn_x2 && !kn_stream_bnr2.get()) return 0;
   return p.gn <= 64 ? 2 : 1;
 }
 

@@ -564,6 +564,37 @@ def test_bn_group_reduction_in_kernel(gpu, mode):
         torch.testing.assert_close(pa.sum(0), pc.double().sum(0), rtol=1e-5, atol=1e-3)
 
 
+def test_dgrad_bnr2_kernel_variants(gpu):
+    """Dual BN-reduce DGRAD (the DGRAD into a block tail with a downsample BN): the one-tile kernel at
+    epilogue depth 2 (default), at depth 4, and the streaming kernel (knob stream_bnr2) give the same
+    masked gradient bitwise and the same BN-backward sums."""
+    torch.manual_seed(5)
+    ops = _ops()
+    N, H, C, K = 16, 28, 256, 64          # 12,544 rows: wide short-K GEMM (gk = 64, gn = 256)
+    w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
+    dy = rnd(N, H, H, K, dev=gpu)
+    xb, x2, res = rnd(N, H, H, C, dev=gpu), rnd(N, H, H, C, dev=gpu), rnd(N, H, H, C, dev=gpu)
+    mean, mean2 = torch.randn(C, device=gpu) * 0.1, torch.randn(C, device=gpu) * 0.1
+    istd, istd2 = torch.rand(C, device=gpu) + 0.5, torch.rand(C, device=gpu) + 0.5
+    bits = torch.randint(0, 256, (N * H * H * C // 8,), device=gpu, dtype=torch.uint8)
+    outs = []
+    try:
+        for knobs in ({}, {"epi_depth_bnr2": 4}, {"stream_bnr2": 1}):
+            for k, v in knobs.items():
+                ops.set_knob(k, v)
+            r = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, res, None, xb, mean, istd, x2, mean2, istd2, None, None, None, bits)
+            outs.append([t.clone() for t in r])
+            ops.set_knob("epi_depth_bnr2", 2)
+            ops.set_knob("stream_bnr2", 0)
+    finally:
+        ops.set_knob("epi_depth_bnr2", 2)
+        ops.set_knob("stream_bnr2", 0)
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0])
+        for pa, pb in zip(o[1:], outs[0][1:]):
+            torch.testing.assert_close(pa.double().sum(0), pb.double().sum(0), rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,C,k", [(1, 1000, 1), (256, 1000, 1), (64, 10, 5), (37, 1000, 8), (5, 3, 3)])
 def test_topk_rows_vs_stable_sort(gpu, dtype, B, C, k):

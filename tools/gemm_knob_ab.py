@@ -74,6 +74,18 @@ def build_cases(modes, only):
                 return ops.conv_dgrad_bnr(dy, w, H, W, s, p, res.clone() if s == 2 else res, None, xb, mean, istd,
                                           None, None, None, None, None, None, bits)
             cases.append((f"dgrad_bnr {name}", flops, byts, dg))
+            if s == 1 and R == 1 and K < C:
+                # dual BN-reduce form (the DGRAD into a block whose tail has a downsample BN): the main
+                # and downsample BN inputs, both reductions, residual gradient, mask bits
+                x2 = torch.randn(N, H, W, C, device=dev, generator=g).to(torch.bfloat16)
+                mean2 = torch.randn(C, device=dev, generator=g) * 0.1
+                istd2 = torch.rand(C, device=dev, generator=g) + 0.5
+
+                def dg2(dy=dy, w=w, H=H, W=W, p=p, xb=xb, res=res, mean=mean, istd=istd, bits=bits, x2=x2,
+                        mean2=mean2, istd2=istd2):
+                    return ops.conv_dgrad_bnr(dy, w, H, W, 1, p, res, None, xb, mean, istd, x2, mean2, istd2,
+                                              None, None, None, bits)
+                cases.append((f"dgrad_bnr2 {name}", flops, byts + x2.numel() * 2, dg2))
             if s == 1 and R == 3:
                 # intermediate-layer form (the model's conv2 DGRAD): mask recomputed from x, no residual
                 msc, msh = torch.rand(C, device=dev, generator=g) + 0.5, torch.randn(C, device=dev, generator=g) * 0.1
