@@ -1849,7 +1849,10 @@ static Knob kn_shortk_bm64("shortk_bm64", 0);   // FWD/DGRAD with gk <= N: 64x12
 // 3x3 (256 filters x 2304 columns) 95 -> 86 us, layer-4 3x3 unchanged, the 1x1 filters 12-19 %
 // slower (short per-block reductions after the split), so it runs the 3x3 filters with 256 output
 // channels.  Knob wgrad8: 0 off, 1 that policy, 2 every filter with >= 256 x 256 (A/B).
-static Knob kn_wgrad8("wgrad8", 1);
+// In the whole step, where WGRAD shares the CUs with the DGRAD chain on the other stream, the
+// 4-wave kernel wins instead: wgrad8=0 ahead in 8 of 8 interleaved rounds (+0.2-0.9 %,
+// profiles/r2_knob_sweep.txt), so the 8-wave WGRAD is off by default.
+static Knob kn_wgrad8("wgrad8", 0);
 static bool use_wgrad8(const IgemmParams& p) {
   const int k = kn_wgrad8.get();
   if (!k || p.gm < 256 || p.gn < 256) return false;
@@ -1974,7 +1977,10 @@ static int use_dma4(int mode, const IgemmParams& p) {
 // on the wide short-K DGRAD + BN-backward GEMMs (layer-1 256->64 351 -> 343 us, layer-2 512->128
 // 209 -> 203, layer-3 1024->256 130 -> 122) and loses on the FWD + statistics ones (layer-1 64->256
 // 153 -> 185 us), so by default it runs DGRAD with >= 256 output channels and <= 4 K-steps.
-static Knob kn_stream_maxk("stream_maxk", 4);     // use it for gk/BK <= N K-steps (0 = off)
+// Whole-step A/B on the round-2 build (profiles/r2_knob_sweep.txt): with the BNR2 DGRADs moved to
+// the one-tile kernels, the streaming kernel no longer pays on the remaining BNR shapes either
+// (stream_maxk=0 ahead of 4 in 5 of 5 interleaved rounds, +0.7 % mean), so it is off by default.
+static Knob kn_stream_maxk("stream_maxk", 0);     // use it for gk/BK <= N K-steps (0 = off)
 static Knob kn_stream_fwd("stream_fwd", 0);       // 1: also for FWD
 static Knob kn_stream_grid("stream_grid", 512);   // resident blocks (2 per CU)
 // dual BN-reduce DGRADs (EPI_BNR2): the streaming kernel spills with that epilogue (256 VGPRs +

@@ -564,10 +564,52 @@ def test_bn_group_reduction_in_kernel(gpu, mode):
         torch.testing.assert_close(pa.sum(0), pc.double().sum(0), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("v", [1, 2])
+def test_wgrad8_kernel_knob(gpu, v):
+    """The 8-wave 256x256 WGRAD kernel (off by default, knob wgrad8) == the fp32 reference."""
+    torch.manual_seed(7 + v)
+    ops = _ops()
+    N, H, C, K, R = 8, 14, 256, 256, 3 if v == 1 else 1
+    x = rnd(N, H, H, C, dev=gpu)
+    dy = rnd(N, H, H, K, dev=gpu)
+    out = torch.empty(K, R, R, C, device=gpu)
+    outr = torch.empty_like(out)
+    try:
+        ops.set_knob("wgrad8", v)
+        ops.conv_wgrad(dy, x, out, R, R, 1, R // 2, False)
+    finally:
+        ops.set_knob("wgrad8", 0)
+    ref.conv_wgrad(dy, x, outr, R, R, 1, R // 2, False)
+    close(out, outr, rtol=1e-2, atol=1e-1)
+
+
+def test_dgrad_bnr_stream_kernel_knob(gpu):
+    """The persistent streaming kernel (off by default, knob stream_maxk) == the one-tile kernel on a
+    wide short-K DGRAD + BN-backward reduction with residual and mask bits."""
+    torch.manual_seed(6)
+    ops = _ops()
+    N, H, C, K = 16, 28, 256, 64
+    w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
+    dy = rnd(N, H, H, K, dev=gpu)
+    xb, res = rnd(N, H, H, C, dev=gpu), rnd(N, H, H, C, dev=gpu)
+    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    bits = torch.randint(0, 256, (N * H * H * C // 8,), device=gpu, dtype=torch.uint8)
+    outs = []
+    try:
+        for v in (0, 4):
+            ops.set_knob("stream_maxk", v)
+            r = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, res, None, xb, mean, istd, None, None, None, None, None, None, bits)
+            outs.append([t.clone() for t in r])
+    finally:
+        ops.set_knob("stream_maxk", 0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[0][1].double().sum(0), outs[1][1].double().sum(0), rtol=1e-5, atol=1e-3)
+
+
 def test_dgrad_bnr2_kernel_variants(gpu):
     """Dual BN-reduce DGRAD (the DGRAD into a block tail with a downsample BN): the one-tile kernel at
-    epilogue depth 2 (default), at depth 4, and the streaming kernel (knob stream_bnr2) give the same
-    masked gradient bitwise and the same BN-backward sums."""
+    epilogue depth 2 (default), at depth 4, and the streaming kernel (knobs stream_maxk, stream_bnr2;
+    off by default) give the same masked gradient bitwise and the same BN-backward sums."""
     torch.manual_seed(5)
     ops = _ops()
     N, H, C, K = 16, 28, 256, 64          # 12,544 rows: wide short-K GEMM (gk = 64, gn = 256)
@@ -579,16 +621,18 @@ def test_dgrad_bnr2_kernel_variants(gpu):
     bits = torch.randint(0, 256, (N * H * H * C // 8,), device=gpu, dtype=torch.uint8)
     outs = []
     try:
-        for knobs in ({}, {"epi_depth_bnr2": 4}, {"stream_bnr2": 1}):
+        for knobs in ({}, {"epi_depth_bnr2": 4}, {"stream_maxk": 4, "stream_bnr2": 1}):
             for k, v in knobs.items():
                 ops.set_knob(k, v)
             r = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, res, None, xb, mean, istd, x2, mean2, istd2, None, None, None, bits)
             outs.append([t.clone() for t in r])
             ops.set_knob("epi_depth_bnr2", 2)
             ops.set_knob("stream_bnr2", 0)
+            ops.set_knob("stream_maxk", 0)
     finally:
         ops.set_knob("epi_depth_bnr2", 2)
         ops.set_knob("stream_bnr2", 0)
+        ops.set_knob("stream_maxk", 0)
     for o in outs[1:]:
         assert torch.equal(o[0], outs[0][0])
         for pa, pb in zip(o[1:], outs[0][1:]):
