@@ -174,12 +174,18 @@ def test_bert_grads_at_bf16_noise_level(gpu):
 
 
 def test_resnet18_convergence_parity_with_autocast(gpu):
+    """pcmp (bitwise deterministic) and torch autocast train the same ResNet-18 from the same weights
+    on the same batches.  At lr 0.05 the autocast reference itself was bimodal across runs (last-20
+    mean loss 0.000-0.99 over six runs on one box, MIOpen algorithm choice varies run to run), so
+    the comparison runs at lr 0.02 with MIOpen's deterministic algorithms."""
     from pcmp.data.synthetic import SyntheticImages
     from pcmp.models.resnet import resnet18
     from pcmp.models.torch_ref import TorchResNet
     from pcmp.optim import SGD
     from pcmp.utils.flat import FlatParams
-    steps, B, res, lr0, warm = 150, 64, 64, 0.05, 30
+    steps, B, res, lr0, warm = 150, 64, 64, 0.02, 30
+    det = (torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark)
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
     ds = SyntheticImages(steps * B, 10, res, seed=5, device=gpu)
     batches = [ds.get_batch(list(range(i * B, (i + 1) * B))) for i in range(steps)]
     torch.manual_seed(0)
@@ -205,6 +211,7 @@ def test_resnet18_convergence_parity_with_autocast(gpu):
         tl.backward()
         topt.step()
         lt.append(tl.detach())
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det
     lh = torch.stack(lh).float().cpu()
     lt = torch.stack(lt).float().cpu()
     first_h, last_h = lh[:10].mean().item(), lh[-20:].mean().item()
