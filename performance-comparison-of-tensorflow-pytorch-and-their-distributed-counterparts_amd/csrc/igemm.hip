@@ -1757,9 +1757,13 @@ __global__ void wt_transpose_kernel(const unsigned short* __restrict__ w, unsign
 }
 
 // Batched weight transpose of a whole model's conv weights in ONE launch (after each optimizer
-// step, instead of one wt_transpose launch per DGRAD): desc[i] = {src_off, dst_off, K, RS, C,
-// first_block} (elements of the flat bf16 shadow / transposed-shadow buffers); block b handles one
-// 64x64 (k, c) tile of one tap of tensor i = the last i with first_block <= b.
+// step, instead of one wt_transpose launch per DGRAD): desc[i] = {src_off, dst_off, K, T, C,
+// first_block, S, RS, r0, s0, step, subS} (offsets in elements of the flat bf16 shadow /
+// transposed-shadow buffers); block b handles one 64x64 (k, c) tile of one tap of entry i = the
+// last i with first_block <= b.  Entry tap t (of T) reads source tap
+// (r0 + step*(t / subS)) * S + s0 + step*(t % subS) of the [K][RS][C] weight and writes
+// dst[c][t][k]: the whole filter (r0 = s0 = 0, step 1, subS = S) or one stride-2 sub-pixel class
+// (step 2), whose DGRAD GEMM then reads its taps without a per-call transpose.
 __global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src, unsigned short* __restrict__ dst,
                                           const int64_t* __restrict__ desc, int n) {
   __shared__ unsigned short tile[64][65];
@@ -1767,21 +1771,23 @@ __global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src
   int lo = 0, hi = n - 1;   // binary search on first_block (block-uniform)
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (desc[mid * 6 + 5] <= b) lo = mid; else hi = mid - 1;
+    if (desc[mid * 12 + 5] <= b) lo = mid; else hi = mid - 1;
   }
-  const int64_t* d = desc + lo * 6;
+  const int64_t* d = desc + lo * 12;
   const unsigned short* w = src + d[0];
   unsigned short* wt = dst + d[1];
   const int K = (int)d[2], T = (int)d[3], C = (int)d[4];
+  const int S = (int)d[6], RS = (int)d[7], r0 = (int)d[8], s0 = (int)d[9], step = (int)d[10], subS = (int)d[11];
   const int nc = (C + 63) / 64, nk = (K + 63) / 64;
   int local = b - (int)d[5];
   const int t = local / (nc * nk);
   local -= t * nc * nk;
   const int k0 = (local / nc) * 64, c0 = (local % nc) * 64;
+  const int ts = (r0 + step * (t / subS)) * S + s0 + step * (t % subS);
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int k = k0 + r, c = c0 + tx;
-    tile[r][tx] = (k < K && c < C) ? w[((size_t)k * T + t) * C + c] : 0;
+    tile[r][tx] = (k < K && c < C) ? w[((size_t)k * RS + ts) * C + c] : 0;
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
@@ -2654,12 +2660,20 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   auto st = cur_stream();
   // a pre-transposed weight [C][R][S][K] (batched refresh, pcmp.utils.flat) replaces the per-call
   // transpose wherever the GEMM uses every tap: stride 1, and 1x1 stride 2 (one parity class)
-  at::Tensor wt_full;
+  // A 1-D wt (stride 2 only) is the class-blocked layout of utils/flat.py: the sub-pixel classes
+  // (oph, opw) = (0,0), (0,1), (1,0), (1,1) one after another, each [C][subR][subS][K] -- every
+  // class GEMM reads its taps from there instead of transposing them per call.
+  at::Tensor wt_full, wt_cls;
   if (wt_given.has_value() && wt_given->defined()) {
     PCMP_CHECK_BF16(*wt_given); PCMP_CHECK_CONTIG(*wt_given);
-    TORCH_CHECK(wt_given->numel() == w.numel() && wt_given->size(0) == C && wt_given->size(-1) == K,
-                "conv_dgrad: transposed weight must be [C,R,S,K]");
-    wt_full = *wt_given;
+    TORCH_CHECK(wt_given->numel() == w.numel(), "conv_dgrad: transposed weight numel");
+    if (wt_given->dim() == 1) {
+      TORCH_CHECK(stride == 2, "conv_dgrad: class-blocked transposed weight needs stride 2");
+      wt_cls = *wt_given;
+    } else {
+      TORCH_CHECK(wt_given->size(0) == C && wt_given->size(-1) == K, "conv_dgrad: transposed weight must be [C,R,S,K]");
+      wt_full = *wt_given;
+    }
   }
   if (stride == 2) {
     struct Cls { int oph, opw, r0, s0, subR, subS, dH, dW; };
@@ -2712,10 +2726,23 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
       part = at::empty({T, 2, C}, fopts);
       if (two) part2 = at::empty({T, 2, C}, fopts);
     }
+    // element offset of each class block in a class-blocked wt (every class counted, as utils/flat.py does)
+    int64_t cls_off[2][2] = {{0, 0}, {0, 0}}, cls_total = 0;
+    for (int oph = 0; oph < 2; ++oph)
+      for (int opw = 0; opw < 2; ++opw) {
+        const int r0 = (oph + pad) & 1, s0 = (opw + pad) & 1;
+        const int subR = r0 < R ? (R - r0 + 1) / 2 : 0, subS = s0 < S ? (S - s0 + 1) / 2 : 0;
+        cls_off[oph][opw] = cls_total;
+        cls_total += (int64_t)C * subR * subS * K;
+      }
+    TORCH_CHECK(!wt_cls.defined() || cls_total == wt_cls.numel(), "conv_dgrad: class-blocked weight size");
     int toff = 0;
     for (auto& c : cls) {
       const bool whole = c.subR == R && c.subS == S && wt_full.defined();
-      at::Tensor wt = whole ? wt_full : transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st);
+      at::Tensor wt = wt_cls.defined()
+                          ? wt_cls.narrow(0, cls_off[c.oph][c.opw], (int64_t)C * c.subR * c.subS * K)
+                                .view({C, c.subR, c.subS, K})
+                          : (whole ? wt_full : transpose_taps(w, c.r0, c.s0, 2, c.subR, c.subS, st));
       IgemmParams q = class_params(c, wt);
       if (bn) {
         q.stats = ptr<float>(part) + (size_t)toff * 2 * C;
@@ -2930,11 +2957,11 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   wgrad_run(p, nsplit, ptr<float>(out), accumulate, out.options(), st);
 }
 
-// src/dst: flat bf16 buffers; desc: int64 [n][6] on device (see wt_transpose_multi_kernel)
+// src/dst: flat bf16 buffers; desc: int64 [n][12] on device (see wt_transpose_multi_kernel)
 void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor& desc, int64_t blocks) {
   PCMP_CHECK_CUDA(src); PCMP_CHECK_BF16(src); PCMP_CHECK_BF16(dst); PCMP_CHECK_CONTIG(src); PCMP_CHECK_CONTIG(dst);
   TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.is_contiguous() && desc.dim() == 2 &&
-              desc.size(1) == 6, "wt_transpose_multi: desc must be int64 [n,6] on the device");
+              desc.size(1) == 12, "wt_transpose_multi: desc must be int64 [n,12] on the device");
   const int n = desc.size(0);
   if (n == 0 || blocks <= 0) return;
   hipLaunchKernelGGL(wt_transpose_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, cur_stream(),

@@ -38,6 +38,10 @@ class ConvBN(nn.Module):
         wk = torch.zeros(cout, k, k, cin_p)
         wk[..., :cin] = w.permute(0, 2, 3, 1)
         self.weight = nn.Parameter(wk)
+        if stride == 2 and k > 1:
+            # its DGRAD runs as four sub-pixel class GEMMs: the flat arena keeps the transposed
+            # weight class-blocked for them (utils/flat.py)
+            self.weight._pcmp_s2_pad = pad
         self.gamma = nn.Parameter(torch.zeros(cout) if zero_init_gamma else torch.ones(cout))
         self.beta = nn.Parameter(torch.zeros(cout))
         self.register_buffer("running_mean", torch.zeros(cout))

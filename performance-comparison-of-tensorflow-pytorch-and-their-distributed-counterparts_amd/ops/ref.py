@@ -367,11 +367,13 @@ def cast_to_bf16(x, y):
 
 
 def wt_transpose_multi(src, dst, desc, blocks):
-    """dst[C][R*S][K] = src[K][R*S][C] for every tensor described by desc rows
-    (src_off, dst_off, K, RS, C, first_block) -- the batched DGRAD weight transpose."""
-    for so, do, K, T, C, _ in desc.tolist():
-        n = K * T * C
-        dst[do:do + n].copy_(src[so:so + n].view(K, T, C).permute(2, 1, 0).reshape(-1))
+    """dst[C][T][K] = src[K][tap(t)][C] for every entry described by desc rows (src_off, dst_off, K,
+    T, C, first_block, S, RS, r0, s0, step, subS), tap(t) = (r0 + step*(t // subS))*S + s0 +
+    step*(t % subS) -- the batched DGRAD weight transpose (whole filters and stride-2 classes)."""
+    for so, do, K, T, C, _, S, RS, r0, s0, step, subS in desc.tolist():
+        taps = [(r0 + step * (t // subS)) * S + s0 + step * (t % subS) for t in range(T)]
+        w = src[so:so + K * RS * C].view(K, RS, C)[:, taps, :]
+        dst[do:do + K * T * C].copy_(w.permute(2, 1, 0).reshape(-1))
 
 
 # ------------------------------------------------------------------------------ text / LSTM

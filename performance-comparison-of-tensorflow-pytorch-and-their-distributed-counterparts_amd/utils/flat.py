@@ -14,6 +14,8 @@ first in backward, so the first DDP bucket fills (and starts its all-reduce) ear
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 ALIGN = 16  # elements (64 B fp32) — every slice starts on a 16-byte vector boundary for bf16 too
@@ -71,9 +73,25 @@ class FlatParams:
                 (K, C), R, S = p.shape, 1, 1
             else:
                 continue
-            rows.append([o, off, K, R * S, C, blocks])
-            p._t_slice = (off, (C, R, S, K))
-            blocks += R * S * ((K + 63) // 64) * ((C + 63) // 64)
+            tiles = ((K + 63) // 64) * ((C + 63) // 64)
+            pad = getattr(p, "_pcmp_s2_pad", None)
+            if pad is not None and R > 1 and S > 1 and os.environ.get("PCMP_S2_CLASS_T", "1") != "0":
+                # stride-2 conv: the four sub-pixel classes (oph, opw) of its DGRAD one after another,
+                # each [C][subR][subS][K] (the layout csrc/igemm.hip dgrad_impl slices; no per-call
+                # transpose of the class taps)
+                coff = 0
+                for oph in (0, 1):
+                    for opw in (0, 1):
+                        r0, s0 = (oph + pad) & 1, (opw + pad) & 1
+                        sub_r, sub_s = (R - r0 + 1) // 2, (S - s0 + 1) // 2
+                        rows.append([o, off + coff, K, sub_r * sub_s, C, blocks, S, R * S, r0, s0, 2, sub_s])
+                        blocks += sub_r * sub_s * tiles
+                        coff += C * sub_r * sub_s * K
+                p._t_slice = (off, (p.numel(),))
+            else:
+                rows.append([o, off, K, R * S, C, blocks, S, R * S, 0, 0, 1, S])
+                p._t_slice = (off, (C, R, S, K))
+                blocks += R * S * tiles
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         if not rows:
             return
@@ -88,7 +106,8 @@ class FlatParams:
                 p._flat_owner = self
 
     def transposed(self, p):
-        """[C,R,S,K] bf16 compute weight of a conv weight ``p`` (batched refresh when stale)."""
+        """[C,R,S,K] bf16 compute weight of a conv weight ``p`` (batched refresh when stale); for a
+        stride-2 conv weight (``_pcmp_s2_pad``) the 1-D class-blocked layout instead."""
         from ..ops.params import WEIGHT_GEN
         if self._t_gen != WEIGHT_GEN[0]:
             from ..ops.kernels import K

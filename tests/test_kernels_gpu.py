@@ -369,18 +369,38 @@ def test_batched_weight_transpose_and_dgrad_with_pretransposed(gpu):
     from pcmp.utils.flat import FlatParams
     shapes = [(64, 3, 3, 64), (256, 1, 1, 64), (72, 7, 7, 8), (512, 1, 1, 256), (128, 3, 3, 128)]
     ps = [torch.nn.Parameter(torch.randn(*s, device=gpu) * 0.05) for s in shapes]
+    ps[2]._pcmp_s2_pad = 3     # stride-2 7x7 and 3x3 (ConvBN marks them): class-blocked layout
+    ps[4]._pcmp_s2_pad = 1
     lin = torch.nn.Parameter(torch.randn(40, 24, device=gpu))     # 2-D: no transposed copy
     flat = FlatParams(ps + [lin])
     assert getattr(lin, "_flat_owner", None) is None
     for p in ps:
         wt = compute_weight_t(p, torch.bfloat16)
-        assert torch.equal(wt, compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0).contiguous())
+        full = compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0).contiguous()   # [C,R,S,K]
+        pad = getattr(p, "_pcmp_s2_pad", None)
+        if pad is None:
+            assert torch.equal(wt, full)
+            continue
+        blocks = [full[:, (oph + pad) & 1::2, (opw + pad) & 1::2, :].reshape(-1) for oph in (0, 1) for opw in (0, 1)]
+        assert wt.dim() == 1 and torch.equal(wt, torch.cat(blocks))
     # stale after a weight change -> refreshed on the next request
     flat.master.mul_(-1.0)
     flat.refresh_shadows()
     p = ps[0]
     assert torch.equal(compute_weight_t(p, torch.bfloat16), compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0).contiguous())
     bump_weight_gen()
+    # the class-blocked stride-2 weight feeds the fused DGRAD + BN-reduce path too
+    p4 = ps[4]
+    dy4 = rnd(2, 7, 7, 128, dev=gpu)
+    x4 = rnd(2, 14, 14, 128, dev=gpu)
+    mean4, istd4 = torch.randn(128, device=gpu) * 0.1, torch.rand(128, device=gpu) + 0.5
+    sc4, sh4 = torch.rand(128, device=gpu) + 0.5, torch.randn(128, device=gpu) * 0.1
+    w4 = compute_weight(p4, torch.bfloat16)
+    r_a = _ops().conv_dgrad_bnr(dy4, w4, 14, 14, 2, 1, None, None, x4, mean4, istd4, None, None, None, sc4, sh4)
+    r_b = _ops().conv_dgrad_bnr(dy4, w4, 14, 14, 2, 1, None, None, x4, mean4, istd4, None, None, None, sc4, sh4,
+                                compute_weight_t(p4, torch.bfloat16))
+    for ta, tb in zip(r_a, r_b):
+        assert torch.equal(ta, tb)
     for (K_, R, S, C), p, (s, pad) in zip(shapes, ps, [(1, 1), (1, 0), (2, 3), (2, 0), (2, 1)]):
         N, H, W = 2, 14, 14
         P, Q = (H + 2 * pad - R) // s + 1, (W + 2 * pad - S) // s + 1
