@@ -1859,6 +1859,7 @@ static Knob kn_shortk_bm64("shortk_bm64", 0);   // FWD/DGRAD with gk <= N: 64x12
 // 4-wave kernel wins instead: wgrad8=0 ahead in 8 of 8 interleaved rounds (+0.2-0.9 %,
 // profiles/r2_knob_sweep.txt), so the 8-wave WGRAD is off by default.
 static Knob kn_wgrad8("wgrad8", 0);
+static Knob kn_wgrad_wgs("wgrad_wgs", 0);   // > 0: fixed split-K workgroup target (side-stream WGRADs)
 static bool use_wgrad8(const IgemmParams& p) {
   const int k = kn_wgrad8.get();
   if (!k || p.gm < 256 || p.gn < 256) return false;
@@ -2892,6 +2893,10 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
     return !(e && std::atoi(e) == 0);
   }();
   if (fixed_target) return nsplit_for(fixed_target);
+  // WGRADs launched on the side stream (ops/params.py run_on_side sets the knob around them) share
+  // the CUs with the DGRAD chain: there a fixed 384-workgroup target beats the isolated autotune
+  // (ResNet-50 step +0.5-0.7 %, 3 of 3 interleaved rounds, profiles/r2_knob_sweep.txt sweep 6)
+  if (kn_wgrad_wgs.get() > 0) return nsplit_for(std::max(64, kn_wgrad_wgs.get()));
   const int dflt = nsplit_for(1024);
   if (!tune) return dflt;
   static std::mutex mu;

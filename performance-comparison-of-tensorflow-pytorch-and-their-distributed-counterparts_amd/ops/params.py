@@ -153,6 +153,20 @@ def join_side(result, ev):
     return result
 
 
+_SIDE_WGS = []
+
+
+def _side_wgrad_wgs() -> int:
+    """Split-K workgroup target of side-stream WGRADs (``PCMP_SIDE_WGRAD_WGS``, default 384; 0 keeps
+    the per-shape autotune, which times each WGRAD alone)."""
+    if not _SIDE_WGS:
+        try:
+            _SIDE_WGS.append(max(0, int(os.environ.get("PCMP_SIDE_WGRAD_WGS", "384"))))
+        except ValueError:
+            _SIDE_WGS.append(384)
+    return _SIDE_WGS[0]
+
+
 def run_on_side(fn: Callable[[], None], keep_alive) -> None:
     """Run ``fn`` (kernel launches) on the device's WGRAD stream, ordered after the compute stream's
     work so far; ``keep_alive`` tensors are recorded on the side stream for the caching allocator."""
@@ -164,8 +178,16 @@ def run_on_side(fn: Callable[[], None], keep_alive) -> None:
     key = ("active", dev.index)
     _SIDE[key] = (main, side)
     side.wait_stream(main)
+    wgs = _side_wgrad_wgs()
     with torch.cuda.stream(side):
-        fn()
+        if wgs:
+            torch.ops.pcmp.set_knob("wgrad_wgs", wgs)
+            try:
+                fn()
+            finally:
+                torch.ops.pcmp.set_knob("wgrad_wgs", 0)
+        else:
+            fn()
     for t in keep_alive:
         t.record_stream(side)
     if not _JOIN_QUEUED[0]:
