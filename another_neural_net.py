@@ -63,6 +63,7 @@ def build_image_model(args, device):
         else:
             m = resnet.resnet50_transfer(10)
             opt = dict(optimizer="adam", lr=args.lr or 0.003)      # Adam(model.fc.parameters(), lr=0.003)
+    cli.load_pretrained(m, getattr(args, "weights", None))   # models.resnet50(pretrained=True) (:95, :244)
     return m.to(device), opt
 
 

@@ -26,10 +26,22 @@ BASELINE.json's metric.  ``--infer-images 0`` skips it.
 all-reduce even at one rank, so the multi-GPU communication path runs on a one-GPU box;
 ``--grad-dtype bf16`` all-reduces bf16 gradient copies (half the xGMI bytes).
 
+``--gpus N`` without a launcher (no ``WORLD_SIZE`` in the environment) starts ``torch.distributed.run``
+with N ranks as a CHILD process before anything touches the GPU, waits for it and exits with its
+status: a ``--gpus 8`` run never reports a one-GPU number.  Under a launcher, ``--gpus`` must equal
+``WORLD_SIZE`` or the run fails.  The JSON line proves the communicator's size (``comm.world_check``
+= an all-reduce of ones over the process group) and reports the gradient buckets and the exposed
+(non-overlapped) all-reduce time per step (``comm.exposed_ms``: from the compute stream reaching
+the end of backward to the last collective finishing, CUDA events, mean over the timed steps).
+
+The learning rate ramps linearly over the warm-up steps to ``--lr`` and stays constant in the timed
+steps (no per-step host work in the timed region); ``final_loss`` (the loss of the last timed step on
+the fixed synthetic batch) then sits below ln(num_classes), a cheap numerics sanity signal.
+
 ``vs_baseline`` is null: the reference publishes no full-network training number (its only
 training figure, BASELINE.md P1a = 1.43 img/s, is frozen-backbone transfer learning on a CPU
-Colab runtime), so no like-for-like ratio exists.  ``vs_stock_pytorch`` compares against the
-stock PyTorch-ROCm self-baseline of the same step on the same GPU (BASELINE.md, 6,540 img/s).
+Colab runtime), so no like-for-like ratio exists.  The stock PyTorch-ROCm self-baseline of the same
+step (MIOpen, ``--impl torch``) is a builder-measured figure in BASELINE.md, not part of this line.
 """
 from __future__ import annotations
 
@@ -48,8 +60,6 @@ import pcmp  # noqa: E402,F401
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-STOCK_TORCH_IMG_PER_SEC = {"resnet50": 6540.0, "resnet18": 16850.0}  # BASELINE.md self-baseline, 1 GPU, B=256
-
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -61,7 +71,8 @@ def parse():
     ap.add_argument("--impl", default="hip", choices=["hip", "torch"])
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--num-classes", type=int, default=1000)
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=0.02,
+                    help="peak SGD lr, reached by a linear ramp over the warm-up steps")
     ap.add_argument("--profile", default=None, help="write a torch.profiler chrome trace here")
     ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over all ranks (SyncBN)")
     ap.add_argument("--graph", action="store_true",
@@ -73,8 +84,33 @@ def parse():
                     help="gradient all-reduce dtype (default fp32, exact)")
     ap.add_argument("--infer-images", type=int, default=200,
                     help="batch-1 inference latency images measured after the timed loop (0 = skip)")
+    ap.add_argument("--watchdog", type=float, default=0.0,
+                    help="abort (exit 3) if a step makes no progress for this many seconds (0 = off)")
+    ap.add_argument("--master-port", type=int, default=0, help="self-launch rendezvous port (0 = pick a free one)")
     ap.add_argument("--local_rank", "--local-rank", type=int, default=None)
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> int | None:
+    """``--gpus N`` (N > 1) with no launcher environment: run this script under
+    ``torch.distributed.run`` with N ranks as a child process and return its exit status.  Must run
+    before anything initialises the HIP runtime (no exec from a GPU-initialised process)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ or "LOCAL_RANK" in os.environ:
+        return None
+    import subprocess
+    port = args.master_port or _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"[bench] --gpus {args.gpus} without a launcher: starting {args.gpus} ranks under torch.distributed.run "
+          f"(127.0.0.1:{port})", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def graph_step(step, x, y):
@@ -137,6 +173,8 @@ def build_hip(args, env):
         return loss
 
     step.model = model
+    step.ddp = ddp
+    step.opt = opt
     return step
 
 
@@ -190,12 +228,24 @@ def batch1_latency(model, args, env):
 
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     import pcmp
     from pcmp.parallel import launch
+    from pcmp.utils.misc import Watchdog
 
     env = launch.init(args.local_rank, force_init=args.ddp_force)
-    if env.world_size != args.gpus and env.is_main:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    if env.world_size != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the job has WORLD_SIZE={env.world_size} ranks: refusing to "
+                         f"report a {env.world_size}-rank number as {args.gpus} GPUs")
+    wd = Watchdog(args.watchdog, abort=True).start() if args.watchdog > 0 else None
+    # the communicator really spans WORLD_SIZE ranks: all-reduce of ones over the process group
+    world_check = 1
+    if dist.is_initialized():
+        one = torch.ones(1, device=env.device)
+        dist.all_reduce(one)
+        world_check = int(one.item())
     if env.device.type == "cuda":
         torch.backends.cudnn.benchmark = True
     B = args.batch_size
@@ -213,8 +263,19 @@ def main():
         if env.device.type == "cuda":
             torch.cuda.synchronize()
 
+    opt = getattr(step, "opt", None)
+    ddp = getattr(step, "ddp", None)
+    ramp = max(1, args.warmup)
     for i in range(args.warmup):
+        if opt is not None:
+            opt.set_lr(args.lr * (i + 1) / ramp)
         loss = step(x, y)
+        if wd is not None:
+            wd.kick(i, "warmup")
+    if opt is not None:
+        opt.set_lr(args.lr)
+    if ddp is not None:
+        ddp.time_exposed(True)
     graphed = bool(args.graph and args.impl == "hip" and env.world_size == 1 and env.device.type == "cuda")
     if graphed:
         step = graph_step(step, x, y)
@@ -228,8 +289,13 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(x, y)
+        if wd is not None:
+            wd.kick(args.warmup + i, "timed")
     sync()
     dt = time.perf_counter() - t0
+    comm = {"backend": env.backend, "world_check": world_check}
+    if ddp is not None:
+        comm.update(ddp.comm_report())
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(args.profile)
@@ -261,16 +327,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "vs_stock_pytorch": (round(img_s / env.world_size / STOCK_TORCH_IMG_PER_SEC[args.model], 3)
-                                 if args.model in STOCK_TORCH_IMG_PER_SEC and B == 256 else None),
-            "dtype": "bf16",
+            "dtype": "bf16" if (env.device.type == "cuda" or args.impl == "torch") else "fp32",
             "data": "synthetic",
             "config": {"model": args.model, "global_batch": B * env.world_size, "per_gpu_batch": B,
                        "image_size": args.image_size, "num_classes": args.num_classes,
                        "seq_len": None, "parallelism": f"dp{env.world_size}", "impl": args.impl,
                        "optimizer": "sgd_momentum", "final_loss": round(final_loss, 4),
                        "hipgraph": graphed, "ddp_force": bool(args.ddp_force),
-                       "grad_allreduce_dtype": args.grad_dtype or "fp32"},
+                       "grad_allreduce_dtype": args.grad_dtype or "fp32", "lr": args.lr,
+                       "lr_warmup_steps": ramp if opt is not None else 0},
+            "comm": comm,
         }
         if infer is not None:
             rec["inference_p50_ms"] = round(infer["p50_ms"], 4)
@@ -280,6 +346,8 @@ def main():
                                        "host_input": "pinned", "conv_plan": "autotuned small-M",
                                        "per_image": "h2d copy + graph replay + argmax + d2h index"}
         print(json.dumps(rec), flush=True)
+    if wd is not None:
+        wd.stop()
     launch.shutdown()
 
 

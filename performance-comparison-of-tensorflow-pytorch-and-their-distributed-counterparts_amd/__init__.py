@@ -13,6 +13,7 @@ once when it initialises (the first device query), before any pcmp or torch.cuda
   value is raised to 8 (a larger one is kept); ``PCMP_HW_QUEUES=<n>`` pins the count exactly.
 """
 import os as _os
+import sys as _sys
 
 MIN_HW_QUEUES = 8
 
@@ -31,8 +32,24 @@ def ensure_hw_queues(environ=_os.environ) -> int:
         except ValueError:
             cur = 0
         n = min(32, max(cur, MIN_HW_QUEUES))
+        if cur and n != cur and environ.get("PCMP_QUIET") != "1":
+            # the override is deliberate (see above) but never silent
+            print(f"[pcmp] GPU_MAX_HW_QUEUES {cur} -> {n} (compute + side + comm + RCCL streams; "
+                  f"PCMP_HW_QUEUES=<n> pins it)", file=_sys.stderr)
     environ["GPU_MAX_HW_QUEUES"] = str(n)
     return n
 
 
+def _hip_already_initialised() -> bool:
+    torch = _sys.modules.get("torch")
+    try:
+        return bool(torch is not None and torch.cuda.is_initialized())
+    except Exception:
+        return False
+
+
+if _hip_already_initialised():
+    import warnings as _w
+    _w.warn("pcmp imported after the HIP runtime initialised: GPU_MAX_HW_QUEUES can no longer take effect "
+            "for this process (import pcmp before any torch.cuda call)", RuntimeWarning)
 ensure_hw_queues()

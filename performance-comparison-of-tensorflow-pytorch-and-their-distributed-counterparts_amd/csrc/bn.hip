@@ -159,9 +159,9 @@ typedef __attribute__((address_space(1))) int gi32;
 // grid (ceil(C/32), G), 256 threads = 64 columns (sum 0 and sum 1 of 32 channels) x 4 row lanes.
 // Stage 1 is partials_reduce_kernel's arithmetic column for column (same rows, same order); each
 // block publishes its fp64 row of `red` with write-through (sc1) 8-byte agent-scope atomic stores,
-// drains them, and takes a ticket on its channel group's counter with a relaxed agent-scope
-// fetch_add -- no release fence, so no L2 write-back (cdna_hip_programming.md Guideline 16, R1
-// form; an agent release per block, i.e. buffer_wbl2, cost 3.6% of the ResNet-50 step).  The last of
+// drains them, and takes a ticket on its channel group's counter with an agent-scope release
+// fetch_add (the last arriver acquires before reading; an agent release per block, i.e. a
+// buffer_wbl2, cost 3.6% of the ResNet-50 step, which is why the knob stays off).  The last of
 // the G blocks reads the rows with sc1 (agent-scope atomic) loads, which bypass its L1, and runs
 // the finalize over the G rows in bn_finalize_kernel's order (lane g sums rows g, g+4, ...; lanes
 // added 0..3), so the result is bitwise that of the two-launch path, whichever block arrives last.
@@ -204,12 +204,15 @@ __global__ __launch_bounds__(256) void partials_reduce_finalize_kernel(const flo
   __syncthreads();
   gi32* my = (gi32*)cnt + blockIdx.x;
   if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(my, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release/acquire pair in the HIP memory model: the ticket is an agent-scope
+    // release, the last arriver issues an agent-scope acquire before reading the rows.  This path
+    // is off by default (knob bn_fused_fin=0), so the extra L2 write-back costs the default nothing.
+    const int t = __hip_atomic_fetch_add(my, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     flag = (t == (int)gridDim.y - 1) ? 1 : 0;
   }
   __syncthreads();
   if (!flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the loads below the ticket
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int G = gridDim.y;
   const int q = threadIdx.x & 31, lane = (threadIdx.x >> 5) & 3;
   const int c = cb + q;

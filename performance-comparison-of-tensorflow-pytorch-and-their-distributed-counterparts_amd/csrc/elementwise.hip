@@ -373,6 +373,65 @@ __global__ void xent_kernel(const T* __restrict__ logits, const int64_t* __restr
   if (lane == 0 && loss_rows) loss_rows[row] = valid ? (lse - ldv<T>(z, (int)y)) : 0.f;
 }
 
+
+// ---------------------------------------------------------------- loss mean / grad scale --------
+// mean over valid rows of the per-row losses (one workgroup, fixed summation order: deterministic):
+// out[0] = sum(loss_rows) / max(1, valid), out[1] = valid (row count whose label is not ignored).
+// Replaces the sum / count / clamp / divide torch launches of the cross-entropy forward.
+__global__ __launch_bounds__(256) void loss_mean_kernel(const float* __restrict__ loss_rows,
+                                                        const int64_t* __restrict__ labels, int B, int V,
+                                                        int ignore_index, float* __restrict__ out) {
+  __shared__ float sh[2][4];
+  float s = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < B; i += 256) {
+    s += loss_rows[i];
+    const int64_t y = labels[i];
+    c += (y != ignore_index && y >= 0 && y < V) ? 1.f : 0.f;
+  }
+  s = warp_sum(s);
+  c = warp_sum(c);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[0][w] = s; sh[1][w] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float ts = (sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3]);
+    const float tc = (sh[1][0] + sh[1][1]) + (sh[1][2] + sh[1][3]);
+    out[0] = ts / fmaxf(tc, 1.f);
+    out[1] = tc;
+  }
+}
+
+// dl * (gout[0] / max(1, valid[0])): the cross-entropy backward's upstream-gradient scale on device
+template <typename T>
+__global__ __launch_bounds__(256) void xent_grad_scale_kernel(const T* __restrict__ dl, const float* __restrict__ gout,
+                                                              const float* __restrict__ valid, T* __restrict__ out,
+                                                              int64_t n) {
+  const float sc = gout[0] / fmaxf(valid[0], 1.f);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if constexpr (std::is_same<T, float>::value) out[i] = dl[i] * sc;
+    else reinterpret_cast<unsigned short*>(out)[i] = f2bf(bf2f(reinterpret_cast<const unsigned short*>(dl)[i]) * sc);
+  }
+}
+
+// log-softmax backward: dz = g - exp(logp) * sum_row(g); one wave per row, logp fp32, g/dz T
+template <typename T>
+__global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const T* __restrict__ g, const float* __restrict__ logp,
+                                                              T* __restrict__ dz, int B, int V) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const T* gr = g + (size_t)row * V;
+  const float* lr = logp + (size_t)row * V;
+  float sg = 0.f;
+  for (int i = lane; i < V; i += 64) sg += ldv<T>(gr, i);
+  sg = warp_sum(sg);
+  for (int i = lane; i < V; i += 64) {
+    const float v = ldv<T>(gr, i) - __expf(lr[i]) * sg;
+    if constexpr (std::is_same<T, float>::value) dz[(size_t)row * V + i] = v;
+    else reinterpret_cast<unsigned short*>(dz)[(size_t)row * V + i] = f2bf(v);
+  }
+}
+
 // ---------------------------------------------------------------- dropout ----------------------
 // y = x * keep / (1-p), keep = uniform(seed, offset+i) >= p ; same call in backward on dy.
 __global__ void dropout_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y, int64_t n, float p,
@@ -690,6 +749,53 @@ std::vector<at::Tensor> softmax_xent(const at::Tensor& logits, const c10::option
   return r;
 }
 
+
+at::Tensor loss_mean(const at::Tensor& loss_rows, const at::Tensor& labels, int64_t V, int64_t ignore_index) {
+  PCMP_CHECK_CUDA(loss_rows); PCMP_CHECK_F32(loss_rows); PCMP_CHECK_CONTIG(loss_rows); PCMP_CHECK_CONTIG(labels);
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == loss_rows.numel(), "loss_mean: int64 labels [B]");
+  auto out = at::empty({2}, loss_rows.options());
+  hipLaunchKernelGGL(loss_mean_kernel, dim3(1), dim3(256), 0, cur_stream(), ptr<float>(loss_rows),
+                     labels.data_ptr<int64_t>(), (int)loss_rows.numel(), (int)V, (int)ignore_index, ptr<float>(out));
+  PCMP_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor xent_grad_scale(const at::Tensor& dl, const at::Tensor& gout, const at::Tensor& valid) {
+  PCMP_CHECK_CUDA(dl); PCMP_CHECK_CONTIG(dl); PCMP_CHECK_F32(gout); PCMP_CHECK_F32(valid);
+  auto out = at::empty_like(dl);
+  const int64_t n = dl.numel();
+  if (n == 0) return out;
+  const int grid = (int)std::min<int64_t>(ceil_div(n, (int64_t)256), 4096);
+  if (dl.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(xent_grad_scale_kernel<float>, dim3(grid), dim3(256), 0, cur_stream(), ptr<float>(dl),
+                       ptr<float>(gout), ptr<float>(valid), ptr<float>(out), n);
+  else {
+    PCMP_CHECK_BF16(dl);
+    hipLaunchKernelGGL(xent_grad_scale_kernel<__bf16>, dim3(grid), dim3(256), 0, cur_stream(), ptr<__bf16>(dl),
+                       ptr<float>(gout), ptr<float>(valid), ptr<__bf16>(out), n);
+  }
+  PCMP_LAUNCH_CHECK();
+  return out;
+}
+
+at::Tensor log_softmax_bwd(const at::Tensor& g, const at::Tensor& logp) {
+  PCMP_CHECK_CUDA(g); PCMP_CHECK_CONTIG(g); PCMP_CHECK_F32(logp); PCMP_CHECK_CONTIG(logp);
+  TORCH_CHECK(g.dim() == 2 && logp.sizes() == g.sizes(), "log_softmax_bwd: g, logp [B,V]");
+  const int B = g.size(0), V = g.size(1);
+  auto dz = at::empty_like(g);
+  if (B == 0) return dz;
+  if (g.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(log_softmax_bwd_kernel<float>, dim3(ceil_div(B, 4)), dim3(256), 0, cur_stream(), ptr<float>(g),
+                       ptr<float>(logp), ptr<float>(dz), B, V);
+  else {
+    PCMP_CHECK_BF16(g);
+    hipLaunchKernelGGL(log_softmax_bwd_kernel<__bf16>, dim3(ceil_div(B, 4)), dim3(256), 0, cur_stream(),
+                       ptr<__bf16>(g), ptr<float>(logp), ptr<__bf16>(dz), B, V);
+  }
+  PCMP_LAUNCH_CHECK();
+  return dz;
+}
+
 at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   TORCH_CHECK(x.numel() % 8 == 0, "dropout: numel % 8");
@@ -874,7 +980,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 __global__ __launch_bounds__(256) void synth_images_kernel(const int64_t* __restrict__ labels,
                                                            const float* __restrict__ color,
                                                            const float* __restrict__ freq, int B, int C, int S,
-                                                           uint64_t seed, float noise, float* __restrict__ out) {
+                                                           int K, uint64_t seed, float noise, float* __restrict__ out) {
   const int S4 = S / 4;
   const int64_t total = (int64_t)B * C * S * S4;
   const float step = 6.283185307179586f / (float)(S - 1);
@@ -885,7 +991,7 @@ __global__ __launch_bounds__(256) void synth_images_kernel(const int64_t* __rest
     const int i = r % S; r /= S;
     const int c = r % C;
     const int b = r / C;
-    const int y = (int)labels[b];
+    const int y = (int)min(max(labels[b], (int64_t)0), (int64_t)(K - 1));   // out-of-range labels clamp, never read OOB
     const float fy = freq[2 * y], fx = freq[2 * y + 1];
     const float base = 0.5f * color[y * C + c];
     const float sy = sinf(fy * (i * step));
@@ -910,13 +1016,14 @@ at::Tensor synth_images(const at::Tensor& labels, const at::Tensor& color, const
   TORCH_CHECK(color.dim() == 2 && freq.dim() == 2 && freq.size(1) == 2 && freq.size(0) == color.size(0),
               "synth_images: color [K,C], freq [K,2]");
   TORCH_CHECK(S >= 4 && S % 4 == 0, "synth_images: image size must be a multiple of 4");
+  TORCH_CHECK(color.size(0) >= 1, "synth_images: at least one class");
   const int B = labels.size(0), C = color.size(1);
   auto out = at::empty({B, C, S, S}, color.options());
   if (B == 0) return out;
   const int64_t total = (int64_t)B * C * S * (S / 4);
   const int grid = (int)std::min<int64_t>(ceil_div(total, (int64_t)256), 8192);
   hipLaunchKernelGGL(synth_images_kernel, dim3(grid), dim3(256), 0, cur_stream(), ptr<int64_t>(labels),
-                     ptr<float>(color), ptr<float>(freq), B, C, (int)S, (uint64_t)seed, (float)noise, ptr<float>(out));
+                     ptr<float>(color), ptr<float>(freq), B, C, (int)S, (int)color.size(0), (uint64_t)seed, (float)noise, ptr<float>(out));
   PCMP_LAUNCH_CHECK();
   return out;
 }
@@ -966,6 +1073,9 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("softmax_xent(Tensor logits, Tensor? labels, bool want_logp, bool want_grad, float grad_scale, "
         "int ignore_index) -> Tensor[]",
         &pcmp::softmax_xent);
+  m.def("loss_mean(Tensor loss_rows, Tensor labels, int V, int ignore_index) -> Tensor", &pcmp::loss_mean);
+  m.def("xent_grad_scale(Tensor dl, Tensor gout, Tensor valid) -> Tensor", &pcmp::xent_grad_scale);
+  m.def("log_softmax_bwd(Tensor g, Tensor logp) -> Tensor", &pcmp::log_softmax_bwd);
   m.def("dropout(Tensor x, float p, int seed, int offset) -> Tensor", &pcmp::dropout);
   m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &pcmp::relu_bwd);
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()", &pcmp::colsum);

@@ -38,6 +38,10 @@ def common_parser(desc):
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
                     help="bf16 = HIP kernels (default); fp32 = the reference's precision as an explicit "
                          "parity mode on the PyTorch reference ops (the HIP kernels are bf16-only)")
+    ap.add_argument("--weights", default=None,
+                    help="pretrained weights (torchvision ResNet/VGG or HF BERT state_dict; .pth/.pt loaded with "
+                         "torch.load(weights_only=True), or .safetensors) -- the reference's pretrained backbones")
+    ap.add_argument("--weights-vgg", default=None, help="pretrained VGG16 weights where a script runs both families")
     ap.add_argument("--json", default=None, help="append a JSON metrics record to this file")
     ap.add_argument("--profile", default=None,
                     help="torch.profiler chrome trace path (per-rank suffix .rankN under DDP)")
@@ -87,6 +91,43 @@ def run_context(args, env):
             path = f"{path}.rank{env.rank}"
         stack.enter_context(chrome_trace(path))
         yield
+
+
+def read_state_dict(path: str) -> dict:
+    """A state_dict from ``path`` through loaders that execute nothing from the file: safetensors,
+    or ``torch.load(weights_only=True)``.  A checkpoint written by :mod:`pcmp.utils.checkpoint`
+    (``{"model": state_dict, ...}``) is unwrapped."""
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path)
+    import torch
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    for key in ("state_dict", "model"):
+        if isinstance(obj, dict) and isinstance(obj.get(key), dict):
+            obj = obj[key]
+    if not isinstance(obj, dict):
+        raise ValueError(f"{path}: not a state_dict")
+    return obj
+
+
+def load_pretrained(model, path: str | None, load_head: bool | None = None):
+    """``--weights PATH``: load pretrained weights into a framework model (ResNet / VGG16:
+    torchvision layout; BERT: HF layout).  No-op without a path.  Returns the model."""
+    if not path:
+        return model
+    sd = read_state_dict(path)
+    if hasattr(model, "load_torchvision"):
+        if load_head is None:
+            model.load_torchvision(sd)
+        else:
+            model.load_torchvision(sd, load_head=load_head)
+    elif hasattr(model, "load_hf"):
+        model.load_hf(sd)
+    else:
+        raise ValueError(f"--weights: {type(model).__name__} has no pretrained-weight loader")
+    from ..utils.report import rprint
+    rprint(f"[pcmp] loaded pretrained weights from {path}")
+    return model
 
 
 def write_json(args, record):

@@ -142,8 +142,8 @@ class BertForSequenceClassification(nn.Module):
 
     @torch.no_grad()
     def load_hf(self, hf):
-        """Copy weights from a transformers BertForSequenceClassification."""
-        sd = hf.state_dict()
+        """Copy weights from a transformers BertForSequenceClassification (module or its state_dict)."""
+        sd = hf if isinstance(hf, dict) else hf.state_dict()
         self.word.copy_(sd["bert.embeddings.word_embeddings.weight"])
         self.position.copy_(sd["bert.embeddings.position_embeddings.weight"])
         self.token_type.copy_(sd["bert.embeddings.token_type_embeddings.weight"])

@@ -177,6 +177,61 @@ class ResNet(nn.Module):
     def backbone_modules(self):
         return [self.stem, self.layer1, self.layer2, self.layer3, self.layer4]
 
+    # ---- pretrained weights ------------------------------------------------------------------
+    @torch.no_grad()
+    def load_torchvision(self, sd: dict, load_head: bool | None = None):
+        """Load a torchvision-layout ResNet state_dict (``resnet50-19c8e357.pth``, the reference's
+        ``models.resnet50(pretrained=True)``: nb :389,397-410, another_neural_net.py:95) or one saved
+        from :class:`pcmp.models.torch_ref.TorchResNet`: KCRS conv weights -> KRSC (stem Cin padded to
+        8), BN affine + running statistics, and the head when its shape matches (``fc.weight`` for a
+        Linear, ``fc.0`` / ``fc.3`` for the reference's MLP head; ``load_head=False`` skips it, e.g.
+        when a new TL head replaces the 1000-way fc).  Returns the list of state_dict keys used."""
+        from .layers import Linear, MLPHead
+        used = []
+
+        def cbn(L, conv_key, bn_key):
+            bn = {k: sd[f"{bn_key}.{k}"] for k in ("weight", "bias", "running_mean", "running_var")}
+            w = sd[f"{conv_key}.weight"]
+            assert tuple(w.shape) == (L.cout, L.cin, L.R, L.S), f"{conv_key}: {tuple(w.shape)} vs {(L.cout, L.cin, L.R, L.S)}"
+            L.load_torch_conv_bn(w.to(L.weight.dtype), {k: v.to(L.gamma.dtype) for k, v in bn.items()})
+            nbt = sd.get(f"{bn_key}.num_batches_tracked")
+            if nbt is not None:
+                L.num_batches_tracked.copy_(nbt)
+            used.extend([f"{conv_key}.weight"] + [f"{bn_key}.{k}" for k in bn])
+
+        cbn(self.stem.conv, "conv1", "bn1")
+        for li, layer in enumerate([self.layer1, self.layer2, self.layer3, self.layer4], 1):
+            for bi, blk in enumerate(layer):
+                pre = f"layer{li}.{bi}"
+                for ci, L in enumerate(blk.main_layers(), 1):
+                    cbn(L, f"{pre}.conv{ci}", f"{pre}.bn{ci}")
+                if blk.downsample is not None:
+                    cbn(blk.downsample, f"{pre}.downsample.0", f"{pre}.downsample.1")
+
+        def lin(L, key):
+            w, b = sd.get(f"{key}.weight"), sd.get(f"{key}.bias")
+            if w is None or tuple(w.shape) != (L.out_features, L.in_features):
+                return False
+            L.load_torch(w.to(L.weight.dtype), None if b is None else b.to(L.weight.dtype))
+            used.extend([f"{key}.weight"] + ([f"{key}.bias"] if b is not None else []))
+            return True
+
+        if load_head is not False:
+            if isinstance(self.fc, Linear):
+                ok = lin(self.fc, "fc")
+            elif isinstance(self.fc, MLPHead):
+                ok = lin(self.fc.fc1, "fc.0") and lin(self.fc.fc2, "fc.3")
+            else:
+                ok = False
+            if load_head and not ok:
+                raise ValueError("load_torchvision: head weights missing or of another shape")
+        for p in self.parameters():   # bf16 compute shadows of a flat arena follow the new masters
+            owner = getattr(p, "_flat_owner", None)
+            if owner is not None:
+                owner.refresh_shadows()
+                break
+        return used
+
 
 def resnet18(num_classes=1000, **kw):
     return ResNet("resnet18", num_classes, **kw)

@@ -84,7 +84,7 @@ class VGG(nn.Module):
         return self
 
     @torch.no_grad()
-    def load_torchvision(self, sd: dict):
+    def load_torchvision(self, sd: dict, load_head: bool | None = None):
         convs = [m for m in self.features if isinstance(m, Conv2d)]
         keys = sorted({k.rsplit(".", 1)[0] for k in sd if k.startswith("features.")}, key=lambda s: int(s.split(".")[1]))
         for conv, k in zip(convs, keys):
@@ -95,8 +95,18 @@ class VGG(nn.Module):
         w0 = sd["classifier.0.weight"].view(4096, 512, 7, 7).permute(0, 2, 3, 1).reshape(4096, -1)
         self.classifier[0].load_torch(w0, sd["classifier.0.bias"])
         self.classifier[2].load_torch(sd["classifier.3.weight"], sd["classifier.3.bias"])
-        if isinstance(self.classifier[4], Linear):
-            self.classifier[4].load_torch(sd["classifier.6.weight"], sd["classifier.6.bias"])
+        w6 = sd.get("classifier.6.weight")
+        head = self.classifier[-1]
+        if load_head is not False and isinstance(head, Linear) and w6 is not None and \
+                tuple(w6.shape) == (head.out_features, head.in_features):
+            head.load_torch(w6, sd["classifier.6.bias"])
+        elif load_head:
+            raise ValueError("load_torchvision: head weights missing or of another shape")
+        for p in self.parameters():   # bf16 compute shadows of a flat arena follow the new masters
+            owner = getattr(p, "_flat_owner", None)
+            if owner is not None:
+                owner.refresh_shadows()
+                break
         return self
 
 

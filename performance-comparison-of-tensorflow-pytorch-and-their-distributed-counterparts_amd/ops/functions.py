@@ -98,18 +98,17 @@ class SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
         need = ctx.needs_input_grad[0]
-        r = K.softmax_xent(logits.contiguous(), labels, False, need, 1.0, ignore_index)
-        loss_rows = r[0]
-        valid = (labels != ignore_index).sum().clamp_min(1).float()
+        logits = logits.contiguous()
+        r = K.softmax_xent(logits, labels, False, need, 1.0, ignore_index)
+        lm = K.loss_mean(r[0], labels.contiguous(), logits.shape[1], ignore_index)   # [mean, valid rows]
         if need:
-            ctx.save_for_backward(r[1], valid)
-        return loss_rows.sum() / valid
+            ctx.save_for_backward(r[1], lm)
+        return lm[0]
 
     @staticmethod
     def backward(ctx, gout):
-        dl, valid = ctx.saved_tensors
-        scale = (gout / valid).to(torch.float32)
-        return (dl.float() * scale).to(dl.dtype), None, None
+        dl, lm = ctx.saved_tensors
+        return K.xent_grad_scale(dl, gout.reshape(1).to(torch.float32).contiguous(), lm[1:2]), None, None
 
 
 class LogSoftmaxFn(torch.autograd.Function):
@@ -124,9 +123,9 @@ class LogSoftmaxFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (logp,) = ctx.saved_tensors
-        g = g.float()
-        dz = g - torch.exp(logp) * g.sum(1, keepdim=True)
-        return dz.to(ctx.dtype)
+        if g.dtype != ctx.dtype:
+            g = g.to(ctx.dtype)
+        return K.log_softmax_bwd(g.contiguous(), logp)
 
 
 def linear(x, weight, bias=None, relu=False):

@@ -48,6 +48,9 @@ def compute_weight_t(p: torch.Tensor, dtype: torch.dtype):
     owner = getattr(p, "_flat_owner", None)
     if owner is None or dtype != torch.bfloat16:
         return None
+    from . import _lib
+    if _lib.backend() == "torch":
+        return None    # the reference backend computes DGRAD from w; the arena's class-blocked form is HIP-only
     return owner.transposed(p)
 
 
@@ -181,11 +184,11 @@ def run_on_side(fn: Callable[[], None], keep_alive) -> None:
     wgs = _side_wgrad_wgs()
     with torch.cuda.stream(side):
         if wgs:
-            torch.ops.pcmp.set_knob("wgrad_wgs", wgs)
+            prev = torch.ops.pcmp.set_knob("wgrad_wgs", wgs)
             try:
                 fn()
             finally:
-                torch.ops.pcmp.set_knob("wgrad_wgs", 0)
+                torch.ops.pcmp.set_knob("wgrad_wgs", prev)   # keep a PCMP_KNOBS=wgrad_wgs=N setting
         else:
             fn()
     for t in keep_alive:

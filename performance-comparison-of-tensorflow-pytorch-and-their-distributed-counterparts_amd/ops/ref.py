@@ -37,7 +37,10 @@ def conv_fwd(x, w, stride, pad, bias=None, resid=None, relu=False, want_stats=Fa
 
 def conv_dgrad(dy, w, H, W, stride, pad, resid=None, wt=None):
     if wt is not None:   # the pre-transposed weight must agree with w (checked, then unused)
-        assert wt.shape == (w.shape[3], w.shape[1], w.shape[2], w.shape[0]), "conv_dgrad: wt must be [C,R,S,K]"
+        if wt.dim() == 1:    # class-blocked stride-2 form of the flat arena: same elements, other order
+            assert wt.numel() == w.numel(), "conv_dgrad: class-blocked wt must hold w.numel() elements"
+        else:
+            assert wt.shape == (w.shape[3], w.shape[1], w.shape[2], w.shape[0]), "conv_dgrad: wt must be [C,R,S,K]"
     N, K, R, S, C = dy.shape[0], w.shape[0], w.shape[1], w.shape[2], w.shape[3]
     dx = torch.nn.grad.conv2d_input((N, C, H, W), _nchw(w), _nchw(dy), stride=stride, padding=pad)
     dx = _nhwc(dx)
@@ -240,6 +243,20 @@ def softmax_xent(logits, labels, want_logp, want_grad, grad_scale, ignore_index)
         g = torch.where(valid.view(-1, 1), g * grad_scale, torch.zeros_like(g))
         out.append(g.to(logits.dtype))
     return out
+
+
+def loss_mean(loss_rows, labels, V, ignore_index):
+    valid = ((labels != ignore_index) & (labels >= 0) & (labels < V)).sum().float()
+    return torch.stack([loss_rows.float().sum() / valid.clamp_min(1.0), valid])
+
+
+def xent_grad_scale(dl, gout, valid):
+    return (dl.float() * (gout.float().reshape(-1)[0] / valid.float().reshape(-1)[0].clamp_min(1.0))).to(dl.dtype)
+
+
+def log_softmax_bwd(g, logp):
+    gf = g.float()
+    return (gf - torch.exp(logp.float()) * gf.sum(1, keepdim=True)).to(g.dtype)
 
 
 # ------------------------------------------------------------------------------ dropout RNG

@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -134,8 +135,37 @@ class DistributedDataParallel(torch.nn.Module):
         for p in flat.params:
             p._grad_ready_hook = self._on_grad_ready
         self._next_launch = 0
+        self._timing = False
+        self._exposed = []      # per step: (compute-done event, comm-done event) or host seconds
         if self.world > 1:
             self._broadcast_state(broadcast_buffers)
+
+    # ------------------------------------------------------------------------------------------
+    def time_exposed(self, on: bool = True):
+        """Record, per step, how long the optimizer waits for communication after backward: from
+        the compute stream reaching ``finish_gradient_sync`` to the last collective (and its bf16
+        cast-back) finishing on the comm stream.  CUDA events (no host sync); host seconds on CPU."""
+        self._timing = bool(on)
+        self._exposed = []
+
+    def comm_report(self) -> dict:
+        """Bucket plan + exposed communication time (mean/max ms over the timed steps)."""
+        esz = self.flat.grad.element_size()
+        rep = {"active": bool(self.active), "world": self.world, "buckets": len(self.buckets),
+               "bucket_mb": [round((b.end - b.start) * esz / 2 ** 20, 2) for b in self.buckets],
+               "grad_allreduce_dtype": str(self.grad_dtype).replace("torch.", "")}
+        vals = []
+        for e in self._exposed:
+            if isinstance(e, tuple):
+                e[1].synchronize()
+                vals.append(max(0.0, e[0].elapsed_time(e[1])))
+            else:
+                vals.append(e * 1e3)
+        if vals:
+            rep["exposed_ms"] = round(sum(vals) / len(vals), 4)
+            rep["exposed_ms_max"] = round(max(vals), 4)
+            rep["timed_steps"] = len(vals)
+        return rep
 
     # ------------------------------------------------------------------------------------------
     def _broadcast_state(self, buffers: bool):
@@ -227,10 +257,15 @@ class DistributedDataParallel(torch.nn.Module):
         (their slices hold zeros from ``zero_grad``), then joins every outstanding all-reduce.
         GPU: the comm stream waits for RCCL, casts low-precision sums back into the fp32 arena,
         and the compute stream waits for the comm stream once; the host never blocks."""
+        cs = self._comm_stream
+        timing = self._timing and self.active and self.require_sync
+        if timing and cs is not None:
+            ev_a = torch.cuda.Event(enable_timing=True)
+            ev_a.record(torch.cuda.current_stream(cs.device))
+        t0 = time.perf_counter()
         for b in self.buckets:
             b.pending = 0
         self._launch_ready()
-        cs = self._comm_stream
         ctx = torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()
         with ctx:
             for b in self.buckets:
@@ -239,6 +274,12 @@ class DistributedDataParallel(torch.nn.Module):
                     if self._lowp is not None:
                         self.flat.grad[b.start:b.end].copy_(self._lowp[b.start:b.end])
                     b.work = None
+            if timing and cs is not None:
+                ev_b = torch.cuda.Event(enable_timing=True)
+                ev_b.record(cs)
+                self._exposed.append((ev_a, ev_b))
+        if timing and cs is None:
+            self._exposed.append(time.perf_counter() - t0)
         if cs is not None:
             torch.cuda.current_stream(cs.device).wait_stream(cs)
         self._reset()

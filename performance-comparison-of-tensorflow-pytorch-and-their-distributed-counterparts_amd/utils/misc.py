@@ -83,6 +83,7 @@ class Watchdog:
         self.state = {"step": 0, "phase": "init"}   # step = kicks so far
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
+        self._exit = os._exit            # replaceable in tests
 
     def start(self):
         global _ACTIVE_WATCHDOG
@@ -116,10 +117,36 @@ class Watchdog:
             if time.monotonic() - self.last > self.timeout:
                 print(f"[watchdog] no progress for {self.timeout:.0f}s at step={self.state['step']} "
                       f"phase={self.state['phase']} (rank {os.environ.get('RANK', '0')})", file=self.stream, flush=True)
-                faulthandler.dump_traceback(file=self.stream)
+                try:
+                    _dump_stacks(self.stream)
+                except Exception as e:   # never let a reporting failure skip the abort below
+                    try:
+                        print(f"[watchdog] stack dump failed: {e!r}", file=sys.__stderr__, flush=True)
+                    except Exception:
+                        pass
                 if self.abort:
-                    os._exit(3)
+                    self._exit(3)
                 self.last = time.monotonic()
+
+
+def _dump_stacks(stream) -> None:
+    """All Python thread stacks to ``stream``: faulthandler when the stream has a real file
+    descriptor (works even with the GIL held by a stuck thread), else formatted frames (StringIO,
+    pytest capture, notebook streams, which have no ``fileno``)."""
+    try:
+        stream.fileno()
+        has_fd = True
+    except (AttributeError, OSError, ValueError):
+        has_fd = False
+    if has_fd:
+        stream.flush()
+        faulthandler.dump_traceback(file=stream)
+        return
+    import traceback
+    for tid, frame in sys._current_frames().items():
+        stream.write(f"Thread 0x{tid:x} (most recent call last):\n")
+        stream.write("".join(traceback.format_stack(frame)))
+    stream.flush()
 
 
 def _env_int(name: str, default: int) -> int:

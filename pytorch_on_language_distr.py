@@ -76,7 +76,7 @@ def main(argv=None):
         cfg = BertConfig(num_labels=2)
         if args.layers:
             cfg.num_hidden_layers = args.layers
-        model = BertForSequenceClassification(cfg).to(dev)
+        model = cli.load_pretrained(BertForSequenceClassification(cfg), args.weights).to(dev)   # from_pretrained (:155)
         lr = args.lr or 2e-5
     else:
         from pcmp.models.bilstm import BiLSTMClassifier

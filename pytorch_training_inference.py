@@ -60,12 +60,12 @@ def main(argv=None):
         for name in args.models.split(","):
             if name == "resnet50":
                 spec = {"builder": "pcmp.models.resnet:resnet50_transfer", "kwargs": {"num_classes": 10}}
-                model = resnet.resnet50_transfer(10).to(dev)
+                model = cli.load_pretrained(resnet.resnet50_transfer(10), args.weights).to(dev)   # nb :389
                 state = make_state(model, "adam", lr=args.lr or 0.003)
                 early = None
             else:
                 spec = {"builder": "pcmp.models.vgg:vgg16_transfer", "kwargs": {"num_classes": 10}}
-                model = vgg.vgg16_transfer(10).to(dev)
+                model = cli.load_pretrained(vgg.vgg16_transfer(10), args.weights_vgg).to(dev)   # nb :1968
                 state = make_state(model, "adam", lr=args.lr or 1e-3)
                 early = 1
             path = os.path.join(save_dir, f"{name}_model.pt")

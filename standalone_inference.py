@@ -57,7 +57,11 @@ def main(argv=None):
         for name in args.models.split(","):
             fam, arch = name.split("-")
             model = (resnet.ResNet("resnet50", 1000, variant="keras" if fam == "keras" else "torchvision")
-                     if arch == "resnet50" else vgg.vgg16(1000)).to(dev).eval()
+                     if arch == "resnet50" else vgg.vgg16(1000))
+            wpath = args.weights if arch == "resnet50" else args.weights_vgg
+            if fam == "pt":
+                cli.load_pretrained(model, wpath)   # models.resnet50 / vgg16(pretrained=True)
+            model = model.to(dev).eval()
             pre = (lambda x: preprocess_input_caffe(x.permute(0, 2, 3, 1) * 255.0)) if fam == "keras" else (lambda x: x)
             # single-image sanity prediction (E3)
             top = predict_topk(model, pre(images[:1]).to(dev), None, 5 if fam == "pt" else 3)
@@ -76,7 +80,7 @@ def main(argv=None):
             R.rprint(R.standalone_inference_line(total))
             results[name] = {"total_s": total, **R.latency_stats(lat)}
     cli.write_json(args, {"script": "standalone_inference", "n_images": int(images.shape[0]), "results": results,
-                          "weights": "random-init", "data": "real" if args.data_dir else "synthetic"})
+                          "weights": args.weights or args.weights_vgg or "random-init", "data": "real" if args.data_dir else "synthetic"})
     return 0
 
 

@@ -245,6 +245,25 @@ def test_watchdog_fires_and_is_kicked():
     watchdog_kick("after")  # no active watchdog: a no-op
 
 
+def test_watchdog_abort_reached_on_stream_without_fd():
+    """A StringIO stream has no fileno (faulthandler refuses it): the stacks are still written and
+    the abort is still reached."""
+    import io
+    import threading
+    import time as _t
+    from pcmp.utils.misc import Watchdog
+    buf = io.StringIO()
+    fired = threading.Event()
+    codes = []
+    wd = Watchdog(0.3, abort=True, stream=buf)
+    wd._exit = lambda code: (codes.append(code), fired.set(), wd._stop.set())
+    with wd:
+        assert fired.wait(5.0)
+    assert codes == [3]
+    out = buf.getvalue()
+    assert "[watchdog] no progress" in out and "most recent call last" in out
+
+
 def test_profile_and_watchdog_flags_on_entrypoint(tmp_path):
     trace = tmp_path / "trace.json"
     _run("another_neural_net.py", "--preset", "mlp-cpu", "--watchdog", "120", "--profile", str(trace))
@@ -281,3 +300,14 @@ def test_hw_queue_floor():
         e = dict(env)
         assert pcmp.ensure_hw_queues(e) == want
         assert e["GPU_MAX_HW_QUEUES"] == str(want)
+
+
+def test_weights_flag_loads_torchvision_resnet(tmp_path):
+    """--weights PATH on the TL entry point: the torchvision-layout backbone is read with
+    torch.load(weights_only=True) and loaded before training (another_neural_net.py:95)."""
+    from pcmp.models.torch_ref import TorchResNet
+    path = tmp_path / "resnet50.pth"
+    torch.save(TorchResNet("resnet50", 1000).state_dict(), path)
+    out = _run("another_neural_net.py", "--model", "resnet50", "--train-size", "16", "--image-size", "32",
+               "--batch-size", "8", "--epochs", "1", "--num-images", "2", "--weights", str(path))
+    assert f"loaded pretrained weights from {path}" in out and "Training time per epoch is" in out

@@ -29,6 +29,16 @@ def close(a, b, rtol=2e-2, atol=2e-2):
     assert err <= lim, f"max err {err} > {lim}"
 
 
+def close_el(a, b, rel=1e-2, abs_frac=5e-3):
+    """Element-wise bound |a - b| <= rel*|b| + abs_frac*max|b|: a localised error (one wrong tile,
+    one wrong channel) fails even when it is small against the tensor's maximum."""
+    a, b = a.float(), b.float()
+    lim = rel * b.abs() + abs_frac * b.abs().max()
+    bad = ((a - b).abs() > lim)
+    nbad = int(bad.sum().item())
+    assert nbad == 0, f"{nbad} elements outside the element-wise bound (worst {((a - b).abs() - lim).max().item():.3g})"
+
+
 CONV_SHAPES = [
     # N, H, W, C, K, R, stride, pad
     (2, 32, 32, 8, 64, 7, 2, 3),      # stem (Cin padded 3->8)
@@ -55,6 +65,7 @@ def test_conv_fwd(gpu, shape):
     y, st = _ops().conv_fwd(x, w, s, p, None, None, False, True)
     yr, str_ = ref.conv_fwd(x, w, s, p, None, None, False, True)
     close(y, yr)
+    close_el(y, yr)
     close(st.sum(0), str_.sum(0), rtol=2e-2, atol=1e-1)
     # fused bias + residual + relu epilogue
     res = rnd(*yr.shape, dev=gpu)
@@ -251,6 +262,29 @@ def test_softmax_xent(gpu, V):
         close(a, b, 1e-4, 1e-5)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_loss_mean_grad_scale_log_softmax_bwd(gpu, dtype):
+    V = 10
+    z = torch.randn(37, V, device=gpu).to(dtype)
+    y = torch.randint(0, V, (37,), device=gpu)
+    y[3] = -100
+    y[5] = -100
+    r = _ops().softmax_xent(z, y, True, True, 1.0, -100)
+    lm = _ops().loss_mean(r[0], y, V, -100)
+    lmr = ref.loss_mean(r[0], y, V, -100)
+    close(lm, lmr, 1e-5, 1e-6)
+    assert lm[1].item() == 35.0
+    gout = torch.tensor([0.7], device=gpu)
+    close(_ops().xent_grad_scale(r[2], gout, lm[1:2]), ref.xent_grad_scale(r[2], gout, lm[1:2]), 1e-2, 1e-6)
+    # log-softmax backward against autograd of torch.log_softmax in fp32
+    g = torch.randn(37, V, device=gpu).to(dtype)
+    zf = z.float().requires_grad_(True)
+    torch.log_softmax(zf, 1).backward(g.float())
+    dz = _ops().log_softmax_bwd(g, r[1])
+    assert dz.dtype == dtype
+    close(dz, zf.grad, 1e-2 if dtype == torch.bfloat16 else 1e-5, 1e-6)
+
+
 def test_dropout_matches_reference_rng(gpu):
     x = rnd(4096, dev=gpu)
     y = _ops().dropout(x, 0.2, 1234, 77 << 32)
@@ -338,6 +372,7 @@ def test_conv_large_shapes_8wave(gpu, shape):
     y, st = _ops().conv_fwd(x, w, s, p, None, None, False, True)
     yr, str_ = ref.conv_fwd(x, w, s, p, None, None, False, True)
     close(y, yr)
+    close_el(y, yr)
     close(st.sum(0), str_.sum(0), rtol=2e-2, atol=5e-1)
     bias = torch.randn(K, device=gpu)
     res = rnd(*yr.shape, dev=gpu)

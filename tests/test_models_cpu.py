@@ -186,3 +186,47 @@ def test_block_boundary_bn_fusion_matches_unfused(monkeypatch):
         monkeypatch.undo()
         for a, b in zip(g_fused, g_plain):
             assert torch.allclose(a, b, rtol=1e-4, atol=1e-6)
+
+
+def _randomise_bn_stats(tm):
+    g = torch.Generator().manual_seed(3)
+    for m in tm.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.bias.data.copy_(torch.randn(m.num_features, generator=g) * 0.1)
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_resnet_load_torchvision_state_dict(tmp_path, arch):
+    """A torchvision-layout state_dict (TorchResNet has torchvision's module names) saved to disk and
+    read back with weights_only=True loads into the framework ResNet: eval logits agree (fp32, CPU)."""
+    from pcmp.models import resnet
+    from pcmp.models.torch_ref import TorchResNet
+    torch.manual_seed(0)
+    tm = TorchResNet(arch, 1000).eval()
+    _randomise_bn_stats(tm)
+    path = tmp_path / "w.pth"
+    torch.save(tm.state_dict(), path)
+    sd = torch.load(path, weights_only=True)
+    m = getattr(resnet, arch)(1000).eval()
+    used = m.load_torchvision(sd)
+    assert set(used) == {k for k in sd if not k.endswith("num_batches_tracked")}
+    x = torch.rand(2, 3, 64, 64)
+    with torch.no_grad():
+        ref = tm(x)
+        out = m(x)
+    assert (out - ref).abs().max().item() <= 1e-3 * ref.abs().max().item() + 1e-4
+
+
+def test_resnet_load_torchvision_into_tl_model():
+    """The reference's TL flow: pretrained 1000-way backbone, new MLP head (another_neural_net.py:95-112).
+    The 1000-way fc in the file is skipped (its shape does not match the head)."""
+    from pcmp.models import resnet
+    from pcmp.models.torch_ref import TorchResNet
+    tm = TorchResNet("resnet50", 1000)
+    m = resnet.resnet50_transfer(10)
+    used = m.load_torchvision(tm.state_dict())
+    assert "fc.weight" not in used and "layer4.2.bn3.running_var" in used
+    assert torch.equal(m.layer4[2].conv3.weight.permute(0, 3, 1, 2), tm.layer4[2].conv3.weight)
