@@ -17,6 +17,7 @@
 // coefficients), then bn_bwd_apply_kernel dx = k1*g + k2*x + k3 (optionally also writing g for
 // the identity path).
 #include "common.h"
+#include "f32.h"
 
 namespace pcmp {
 
@@ -705,6 +706,7 @@ static void check_act(const at::Tensor& t, const char* name) {
 
 // x: [..., C] bf16 -> partial stats [T][2][C]
 at::Tensor bn_partials(const at::Tensor& x) {
+  if (x.scalar_type() == at::kFloat) return f32::bn_partials(x);
   check_act(x, "bn_partials");
   const int C = x.size(-1);
   const int M = x.numel() / C;
@@ -810,6 +812,7 @@ static int ew_blocks(int64_t nvec) { return (int)std::min<int64_t>(4096, (nvec +
 at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
                     const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
                     const c10::optional<at::Tensor>& shift2, bool relu, const c10::optional<at::Tensor>& mbits) {
+  if (x.scalar_type() == at::kFloat) return f32::bn_apply(x, scale, shift, x2, scale2, shift2, relu, mbits);
   check_act(x, "bn_apply");
   const int C = x.size(-1);
   auto y = at::empty_like(x);
@@ -845,6 +848,7 @@ std::vector<at::Tensor> bn_bwd_reduce(const at::Tensor& dy, const c10::optional<
                                       const at::Tensor& x, const at::Tensor& mean, const at::Tensor& invstd,
                                       const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
                                       const c10::optional<at::Tensor>& invstd2) {
+  if (dy.scalar_type() == at::kFloat) return f32::bn_bwd_reduce(dy, ymask, x, mean, invstd, x2, mean2, invstd2);
   check_act(dy, "bn_bwd dy");
   check_act(x, "bn_bwd x");
   const int C = x.size(-1);
@@ -904,6 +908,7 @@ std::vector<at::Tensor> bn_bwd_apply(const at::Tensor& dy, const c10::optional<a
                                      const at::Tensor& x, const at::Tensor& coef,
                                      const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& coef2,
                                      bool want_g) {
+  if (dy.scalar_type() == at::kFloat) return f32::bn_bwd_apply(dy, ymask, x, coef, x2, coef2, want_g);
   check_act(dy, "bn_bwd_apply dy");
   const int C = x.size(-1);
   auto dx = at::empty_like(x);

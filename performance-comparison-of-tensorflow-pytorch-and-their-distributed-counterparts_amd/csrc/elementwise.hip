@@ -11,6 +11,7 @@
 //   * ToTensor/normalise of the image pipeline — fused NCHW f32/u8 -> NHWC bf16
 //     with zero channel padding to a multiple of 8 (the stem conv's MFMA K granularity)
 #include "common.h"
+#include "f32.h"
 
 #include <climits>
 #include <mutex>
@@ -567,6 +568,124 @@ __global__ void nchw_to_nhwc_kernel(const T* __restrict__ x, __bf16* __restrict_
   }
 }
 
+
+// fp32 variant of the input conversion (the reference-precision path, ``--dtype fp32``)
+template <typename T>
+__global__ void nchw_to_nhwc_f32_kernel(const T* __restrict__ x, float* __restrict__ y, int N, int Cin, int HW,
+                                        int Cpad, float scale) {
+  const int64_t total = (int64_t)N * HW * Cpad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = i % Cpad;
+    const int64_t r = i / Cpad;
+    const int n = r / HW, hw = r % HW;
+    y[i] = c < Cin ? (float)x[((size_t)n * Cin + c) * HW + hw] * scale : 0.f;
+  }
+}
+
+
+// ---------------------------------------------------------------- device image resize -----------
+// PIL-exact bilinear (antialiased) resize of uint8 HWC images on the device: SURVEY §2.4.6 /
+// B6 — the reference's per-image ``Resize((224,224))`` + ``ToTensor`` (another_neural_net.py:170-187;
+// nb :847-862) without the host PIL resize.  Same algorithm as Pillow's ImagingResample for 8-bit
+// images: separable triangle filter with support max(1, in/out), coefficients computed in double
+// (no fma contraction) and rounded to 22-bit fixed point, horizontal pass first with a clipped
+// uint8 intermediate, then the vertical pass.  Output either a CHW uint8 image (bit-identical to
+// PIL's) or, fused, the model input: NHWC with channels padded to cpad, (v*scale - mean)/std, in
+// bf16 or fp32.
+constexpr int RS_PREC = 22;
+constexpr int RS_MAXK = 64;   // taps per output pixel (support <= 31.5: downscale ratios up to 31x)
+
+__device__ __forceinline__ int resize_coeffs(int xx, int in_size, int out_size, int* kint) {
+#pragma clang fp contract(off)
+  const double scale = (double)in_size / (double)out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;
+  const double center = ((double)xx + 0.5) * scale;
+  const double ss = 1.0 / filterscale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > in_size) xmax = in_size;
+  xmax -= xmin;
+  if (xmax > RS_MAXK) xmax = RS_MAXK;
+  auto tri = [&](int x) {   // Pillow's bilinear_filter at tap x
+    double t = ((double)(x + xmin) - center + 0.5) * ss;
+    if (t < 0.0) t = -t;
+    return t < 1.0 ? 1.0 - t : 0.0;
+  };
+  double ww = 0.0;
+  for (int x = 0; x < xmax; ++x) ww += tri(x);
+  for (int x = 0; x < xmax; ++x) {
+    const double w = tri(x);
+    const double k = ww != 0.0 ? w / ww : w;
+    kint[x] = (int)(k * (double)(1 << RS_PREC) + (k < 0.0 ? -0.5 : 0.5));
+  }
+  return (xmin << 8) | xmax;   // xmax <= 64 fits 8 bits
+}
+
+__device__ __forceinline__ unsigned char clip8(int v) {
+  if (v >= (1 << RS_PREC << 8)) return 255;
+  if (v <= 0) return 0;
+  return (unsigned char)(v >> RS_PREC);
+}
+
+// horizontal pass: src [N][H][W][C] u8 -> tmp [N][H][Wo][C] u8 (one thread per output pixel, all C)
+__global__ __launch_bounds__(256) void resize_h_kernel(const unsigned char* __restrict__ src,
+                                                       unsigned char* __restrict__ tmp, int N, int H, int W, int C,
+                                                       int Wo) {
+  const int64_t total = (int64_t)N * H * Wo;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int xo = t % Wo;
+    const int64_t row = t / Wo;   // n*H + y
+    int k[RS_MAXK];
+    const int b = resize_coeffs(xo, W, Wo, k);
+    const int xmin = b >> 8, nt = b & 255;
+    const unsigned char* s = src + (size_t)row * W * C;
+    for (int c = 0; c < C; ++c) {
+      int acc = 1 << (RS_PREC - 1);
+      for (int x = 0; x < nt; ++x) acc += (int)s[(size_t)(xmin + x) * C + c] * k[x];
+      tmp[((size_t)row * Wo + xo) * C + c] = clip8(acc);
+    }
+  }
+}
+
+// vertical pass: tmp [N][H][Wo][C] -> out.  MODE 0: CHW u8 image [N][C][Ho][Wo]; MODE 1/2: NHWC
+// [N][Ho][Wo][cpad] bf16 / fp32 of (v*scale - mean[c]) / std[c] (zero in the padded channels).
+template <int MODE>
+__global__ __launch_bounds__(256) void resize_v_kernel(const unsigned char* __restrict__ tmp, void* __restrict__ out,
+                                                       int N, int H, int Wo, int C, int Ho, int cpad, float scale,
+                                                       const float* __restrict__ mean, const float* __restrict__ stdv) {
+  const int64_t total = (int64_t)N * Ho * Wo;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int xo = t % Wo;
+    const int yo = (t / Wo) % Ho;
+    const int n = t / ((int64_t)Wo * Ho);
+    int k[RS_MAXK];
+    const int b = resize_coeffs(yo, H, Ho, k);
+    const int ymin = b >> 8, nt = b & 255;
+    const int cmax = MODE == 0 ? C : cpad;
+    for (int c = 0; c < cmax; ++c) {
+      float v = 0.f;
+      unsigned char u = 0;
+      if (c < C) {
+        int acc = 1 << (RS_PREC - 1);
+        for (int y = 0; y < nt; ++y) acc += (int)tmp[(((size_t)n * H + ymin + y) * Wo + xo) * C + c] * k[y];
+        u = clip8(acc);
+        v = (float)u * scale;
+        if (mean) v = (v - mean[c]) / stdv[c];
+      }
+      if constexpr (MODE == 0) {
+        reinterpret_cast<unsigned char*>(out)[(((size_t)n * C + c) * Ho + yo) * Wo + xo] = u;
+      } else if constexpr (MODE == 1) {
+        reinterpret_cast<unsigned short*>(out)[(((size_t)n * Ho + yo) * Wo + xo) * cpad + c] = f2bf(v);
+      } else {
+        reinterpret_cast<float*>(out)[(((size_t)n * Ho + yo) * Wo + xo) * cpad + c] = v;
+      }
+    }
+  }
+}
+
 // Stem space-to-depth.  A 7x7 / stride-2 / pad-p convolution over X equals a 4x4 / stride-1 /
 // unpadded convolution over S[n][i][j][(dy*2+dx)*4 + c] = X[n][c][2i+dy-p][2j+dx-p] (zero outside
 // the image and for c >= Cin) with the 7x7 filter embedded in an 8x8 one (ops/conv_blocks.py
@@ -624,6 +743,7 @@ static bool pool3s2_ok(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
 
 std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
                                     const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift) {
+  if (x.scalar_type() == at::kFloat) return f32::maxpool_fwd(x, k, s, pad, want_idx, scale, shift);
   PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   const bool bn = scale.has_value() && scale->defined();
   if (bn) {
@@ -653,6 +773,7 @@ std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, i
 
 at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s,
                        int64_t pad) {
+  if (dy.scalar_type() == at::kFloat) return f32::maxpool_bwd(dy, idx, H, W, k, s, pad);
   PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy);
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
   auto dx = at::empty({N, H, W, C}, dy.options());
@@ -667,6 +788,7 @@ at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, i
 std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& cx,
                                         const at::Tensor& mean, const at::Tensor& invstd, const at::Tensor& scale,
                                         const at::Tensor& shift, int64_t k, int64_t s, int64_t pad) {
+  if (dy.scalar_type() == at::kFloat) return f32::maxpool_bwd_bnr(dy, idx, cx, mean, invstd, scale, shift, k, s, pad);
   PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy); PCMP_CHECK_BF16(cx); PCMP_CHECK_CONTIG(cx);
   TORCH_CHECK(idx.scalar_type() == at::kByte && idx.is_contiguous() && idx.numel() == dy.numel(), "maxpool_bwd_bnr: idx");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
@@ -694,6 +816,7 @@ std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& 
 }
 
 at::Tensor gap_fwd(const at::Tensor& x) {
+  if (x.scalar_type() == at::kFloat) return f32::gap_fwd(x);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   const int N = x.size(0), C = x.size(-1);
   const int HW = x.numel() / ((int64_t)N * C);
@@ -706,6 +829,7 @@ at::Tensor gap_fwd(const at::Tensor& x) {
 }
 
 at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
+  if (dy.scalar_type() == at::kFloat) return f32::gap_bwd(dy, H, W);
   PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy);
   const int N = dy.size(0), C = dy.size(1);
   auto dx = at::empty({N, H, W, C}, dy.options());
@@ -797,6 +921,7 @@ at::Tensor log_softmax_bwd(const at::Tensor& g, const at::Tensor& logp) {
 }
 
 at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
+  if (x.scalar_type() == at::kFloat) return f32::dropout(x, p, seed, offset);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   TORCH_CHECK(x.numel() % 8 == 0, "dropout: numel % 8");
   auto y = at::empty_like(x);
@@ -807,6 +932,7 @@ at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) 
 }
 
 at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y) {
+  if (dy.scalar_type() == at::kFloat) return f32::relu_bwd(dy, y);
   PCMP_CHECK_BF16(dy); PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(y);
   TORCH_CHECK(dy.numel() % 8 == 0, "relu_bwd: numel % 8");
   auto dx = at::empty_like(dy);
@@ -817,6 +943,7 @@ at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y) {
 }
 
 void colsum(const at::Tensor& x, at::Tensor out, bool accumulate) {
+  if (x.scalar_type() == at::kFloat) return f32::colsum(x, out, accumulate);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
   const int C = x.size(-1);
   const int M = x.numel() / C;
@@ -851,6 +978,62 @@ at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad, double scale, const c
   }
   PCMP_LAUNCH_CHECK();
   return y;
+}
+
+
+at::Tensor nchw_to_nhwc_f32(const at::Tensor& x, int64_t cpad, double scale) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_CONTIG(x);
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(cpad % 4 == 0 && cpad >= Cin, "nchw_to_nhwc_f32: cpad");
+  auto y = at::empty({N, H, W, cpad}, x.options().dtype(at::kFloat));
+  const int64_t total = (int64_t)N * H * W * cpad;
+  if (total == 0) return y;
+  const int grid = (int)std::min<int64_t>(ceil_div(total, (int64_t)256), 8192);
+  if (x.scalar_type() == at::kFloat)
+    hipLaunchKernelGGL(nchw_to_nhwc_f32_kernel<float>, dim3(grid), dim3(256), 0, cur_stream(), ptr<float>(x),
+                       ptr<float>(y), N, Cin, H * W, (int)cpad, (float)scale);
+  else {
+    TORCH_CHECK(x.scalar_type() == at::kByte, "nchw_to_nhwc_f32: f32 or u8 input");
+    hipLaunchKernelGGL(nchw_to_nhwc_f32_kernel<uint8_t>, dim3(grid), dim3(256), 0, cur_stream(), ptr<uint8_t>(x),
+                       ptr<float>(y), N, Cin, H * W, (int)cpad, (float)scale);
+  }
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+
+// x: uint8 [N, H, W, C] (decoded HWC images, C <= 4).  mode 0: PIL-exact resize -> uint8 [N, C, Ho, Wo];
+// mode 1 / 2: fused model input, NHWC [N, Ho, Wo, cpad] bf16 / fp32 = (u8 * scale - mean) / std.
+at::Tensor resize_image(const at::Tensor& x, int64_t Ho, int64_t Wo, int64_t mode, int64_t cpad, double scale,
+                        const c10::optional<at::Tensor>& mean, const c10::optional<at::Tensor>& stdv) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_CONTIG(x);
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) <= 4, "resize_image: uint8 [N,H,W,C<=4]");
+  TORCH_CHECK(mode >= 0 && mode <= 2 && Ho > 0 && Wo > 0, "resize_image: mode / size");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK((double)H / Ho <= 31.0 && (double)W / Wo <= 31.0, "resize_image: downscale ratio above 31");
+  if (mode) TORCH_CHECK(cpad >= C, "resize_image: cpad < channels");
+  if (mean.has_value() && mean->defined()) {
+    PCMP_CHECK_F32(*mean); PCMP_CHECK_F32(*stdv);
+    TORCH_CHECK(mean->numel() >= C && stdv->numel() >= C, "resize_image: mean/std");
+  }
+  auto tmp = at::empty({N, H, Wo, C}, x.options());
+  at::Tensor out;
+  if (mode == 0) out = at::empty({N, C, Ho, Wo}, x.options());
+  else out = at::empty({N, Ho, Wo, cpad}, x.options().dtype(mode == 1 ? at::kBFloat16 : at::kFloat));
+  if (N == 0) return out;
+  const int64_t th = (int64_t)N * H * Wo, tv = (int64_t)N * Ho * Wo;
+  hipLaunchKernelGGL(resize_h_kernel, dim3((int)std::min<int64_t>(ceil_div(th, (int64_t)256), 4096)), dim3(256), 0,
+                     cur_stream(), ptr<unsigned char>(x), ptr<unsigned char>(tmp), N, H, W, C, (int)Wo);
+  PCMP_LAUNCH_CHECK();
+  const dim3 gv((int)std::min<int64_t>(ceil_div(tv, (int64_t)256), 4096));
+  const float* mp = optr<float>(mean);
+  const float* sp = optr<float>(stdv);
+#define PCMP_RV(M) hipLaunchKernelGGL(resize_v_kernel<M>, gv, dim3(256), 0, cur_stream(), ptr<unsigned char>(tmp), \
+                                      out.data_ptr(), N, H, (int)Wo, C, (int)Ho, (int)cpad, (float)scale, mp, sp)
+  if (mode == 0) PCMP_RV(0); else if (mode == 1) PCMP_RV(1); else PCMP_RV(2);
+#undef PCMP_RV
+  PCMP_LAUNCH_CHECK();
+  return out;
 }
 
 at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c10::optional<at::Tensor>& mean,
@@ -1080,6 +1263,9 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &pcmp::relu_bwd);
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()", &pcmp::colsum);
   m.def("nchw_to_nhwc(Tensor x, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor", &pcmp::nchw_to_nhwc);
+  m.def("nchw_to_nhwc_f32(Tensor x, int cpad, float scale) -> Tensor", &pcmp::nchw_to_nhwc_f32);
+  m.def("resize_image(Tensor x, int Ho, int Wo, int mode, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor",
+        &pcmp::resize_image);
   m.def("image_to_s2d(Tensor x, int pad, float scale, Tensor? mean, Tensor? stdv, bool nhwc) -> Tensor", &pcmp::image_to_s2d);
   m.def("topk_rows(Tensor x, int k, bool want_values) -> Tensor[]", &pcmp::topk_rows);
   m.def("synth_images(Tensor labels, Tensor color, Tensor freq, int S, int seed, float noise) -> Tensor", &pcmp::synth_images);

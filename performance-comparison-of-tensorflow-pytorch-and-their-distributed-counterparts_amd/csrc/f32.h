@@ -1,0 +1,55 @@
+// fp32 compute path (the reference's precision: another_neural_net.py:95-115, nb :655-702 run fp32
+// everywhere): entry points called by the op wrappers of igemm.hip / bn.hip /
+// elementwise.hip when their activations are fp32 (``--dtype fp32``).  Kernels in f32.hip.
+#pragma once
+#include "common.h"
+
+#include <vector>
+
+namespace pcmp {
+namespace f32 {
+
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
+                                 bool relu, bool want_stats);
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                      const c10::optional<at::Tensor>& resid);
+std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
+                                       int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
+                                       const c10::optional<at::Tensor>& ymask, const at::Tensor& x,
+                                       const at::Tensor& mean, const at::Tensor& invstd,
+                                       const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                                       const c10::optional<at::Tensor>& invstd2, const c10::optional<at::Tensor>& mscale,
+                                       const c10::optional<at::Tensor>& mshift,
+                                       const c10::optional<at::Tensor>& ymask_bits);
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                int64_t pad, bool accumulate);
+
+at::Tensor bn_partials(const at::Tensor& x);
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
+                    const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
+                    const c10::optional<at::Tensor>& shift2, bool relu, const c10::optional<at::Tensor>& mbits);
+std::vector<at::Tensor> bn_bwd_reduce(const at::Tensor& dy, const c10::optional<at::Tensor>& ymask,
+                                      const at::Tensor& x, const at::Tensor& mean, const at::Tensor& invstd,
+                                      const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                                      const c10::optional<at::Tensor>& invstd2);
+std::vector<at::Tensor> bn_bwd_apply(const at::Tensor& dy, const c10::optional<at::Tensor>& ymask,
+                                     const at::Tensor& x, const at::Tensor& coef,
+                                     const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& coef2,
+                                     bool want_g);
+
+std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
+                                    const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift);
+at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s,
+                       int64_t pad);
+std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& cx,
+                                        const at::Tensor& mean, const at::Tensor& invstd, const at::Tensor& scale,
+                                        const at::Tensor& shift, int64_t k, int64_t s, int64_t pad);
+at::Tensor gap_fwd(const at::Tensor& x);
+at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
+at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset);
+at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y);
+void colsum(const at::Tensor& x, at::Tensor out, bool accumulate);
+
+}  // namespace f32
+}  // namespace pcmp

@@ -1,0 +1,866 @@
+// fp32 compute path: the reference's precision on the HIP kernels (``--dtype fp32``).
+//
+// The reference trains and infers in fp32 everywhere (another_neural_net.py:95-115,244-259;
+// pytorch_training_inference_on_image.ipynb:655-702; no autocast).  The bf16 kernels
+// of igemm.hip / bn.hip / elementwise.hip dispatch here when their activations are fp32, so the
+// reference-precision runs stay on hand-written HIP code instead of MIOpen / hipBLASLt.
+//
+// * Convolutions and Linear layers: one implicit-GEMM kernel for FWD / DGRAD / WGRAD on
+//   v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fma chain, cdna_hip_programming.md §3
+//   "FP32-input MFMA"; 1/16 of the bf16 MFMA rate, the f32 VALU peak).  64x64 block tile, 4 waves
+//   of 32x32, BK = 16, register-staged double-buffered LDS images stored reduction-index-major so
+//   every MFMA operand read is one ds_read_b32 of 16 consecutive rows.  FWD epilogue: bias,
+//   residual, ReLU and per-tile BatchNorm partial statistics; WGRAD: split-K fp32 slabs reduced
+//   in fixed order (deterministic).
+// * BatchNorm (partials, apply with residual / ReLU / mask bits, backward reduce / apply, the
+//   masked reductions of a DGRAD or pooling backward), pooling, dropout, ReLU backward and bias
+//   column sums as vectorised fp32 kernels (float4 = 4 channels per thread).
+// Layouts are those of the bf16 path: NHWC activations, KRSC weights ([Cout][kh][kw][Cin]).
+#include "f32.h"
+
+#include <algorithm>
+
+namespace pcmp {
+namespace f32 {
+
+enum { F_FWD = 0, F_DGRAD = 1, F_WGRAD = 2 };
+
+struct ConvP {
+  const float* a;       // FWD: x; DGRAD: dy; WGRAD: dy
+  const float* b;       // FWD: w; DGRAD: w; WGRAD: x
+  float* out;           // FWD/DGRAD [gm][gn]; WGRAD [nsplit][gm][gn]
+  const float* bias;    // [gn]
+  const float* resid;   // [gm][gn]
+  float* stats;         // [tiles_m][2][gn]
+  int gm, gn, gk;
+  int N, H, W, C, K, R, S, P, Q, stride, pad;
+  int relu, ksplit, tiles_m, tiles_n;
+};
+
+constexpr int FBM = 64, FBN = 64, FBK = 16, FLD = 68;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float fget(const float4& v, int e) {
+  return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void igemm_f32_kernel(const ConvP p) {
+  __shared__ __attribute__((aligned(16))) float As[2][FBK][FLD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][FBK][FLD];
+  __shared__ float red[2][2][FBN];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = blockIdx.x / tiles_mn, tl = blockIdx.x - split * tiles_mn;
+  const int tile_m = tl / p.tiles_n, tile_n = tl - (tl / p.tiles_n) * p.tiles_n;
+  const int m0 = tile_m * FBM, n0 = tile_n * FBN;
+  const int kbeg = split * p.ksplit, kend = min(p.gk, kbeg + p.ksplit);
+  const int nk = (kend - kbeg + FBK - 1) / FBK;
+
+  // loader roles: "row-k" (4 consecutive reduction indices of one row: A of FWD / DGRAD, B of FWD)
+  // and "k-col" (4 consecutive columns of one reduction index: B of DGRAD, A and B of WGRAD)
+  const int rk_row = tid >> 2, rk_k = (tid & 3) * 4;
+  const int kc_k = tid >> 4, kc_c = (tid & 15) * 4;
+  // FWD: A row = output pixel; DGRAD: A row = input pixel (decoded once)
+  int a_n = 0, a_y = 0, a_x = 0;
+  bool a_ok = false;
+  if constexpr (MODE != F_WGRAD) {
+    const int m = m0 + rk_row;
+    a_ok = m < p.gm;
+    const int mm = a_ok ? m : 0;
+    if constexpr (MODE == F_FWD) {
+      a_n = mm / (p.P * p.Q);
+      const int rem = mm - a_n * p.P * p.Q;
+      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
+      a_y = pp * p.stride - p.pad;
+      a_x = qq * p.stride - p.pad;
+    } else {
+      a_n = mm / (p.H * p.W);
+      const int rem = mm - a_n * p.H * p.W;
+      a_y = rem / p.W + p.pad;           // h + pad
+      a_x = rem - (rem / p.W) * p.W + p.pad;
+    }
+  }
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  auto load_a = [&](int k0) -> float4 {
+    if constexpr (MODE == F_FWD) {
+      const int k = k0 + rk_k;
+      if (!a_ok || k >= kend) return z4;
+      const int c = k % p.C, rs = k / p.C;
+      const int s = rs % p.S, r = rs / p.S;
+      const int y = a_y + r, x = a_x + s;
+      if ((unsigned)y >= (unsigned)p.H || (unsigned)x >= (unsigned)p.W) return z4;
+      return ld4(p.a + (((size_t)a_n * p.H + y) * p.W + x) * p.C + c);
+    } else if constexpr (MODE == F_DGRAD) {
+      const int k = k0 + rk_k;
+      if (!a_ok || k >= kend) return z4;
+      const int co = k % p.K, rs = k / p.K;
+      const int s = rs % p.S, r = rs / p.S;
+      const int ph = a_y - r, pw = a_x - s;
+      if (ph < 0 || pw < 0 || ph % p.stride || pw % p.stride) return z4;
+      const int py = ph / p.stride, px = pw / p.stride;
+      if (py >= p.P || px >= p.Q) return z4;
+      return ld4(p.a + (((size_t)a_n * p.P + py) * p.Q + px) * p.K + co);
+    } else {   // WGRAD A[co][m] = dy[m][co] (k-col: rows = co)
+      const int m = k0 + kc_k, co = m0 + kc_c;
+      if (m >= kend || co >= p.gm) return z4;
+      return ld4(p.a + (size_t)m * p.K + co);
+    }
+  };
+  auto load_b = [&](int k0) -> float4 {
+    if constexpr (MODE == F_FWD) {   // row-k: W[n][k]
+      const int n = n0 + rk_row, k = k0 + rk_k;
+      if (n >= p.gn || k >= kend) return z4;
+      return ld4(p.b + (size_t)n * p.gk + k);
+    } else if constexpr (MODE == F_DGRAD) {   // k-col: B[k=(r,s,co)][c] = W[co][r][s][c]
+      const int k = k0 + kc_k, c = n0 + kc_c;
+      if (k >= kend || c >= p.gn) return z4;
+      const int co = k % p.K, rs = k / p.K;
+      const int s = rs % p.S, r = rs / p.S;
+      return ld4(p.b + (((size_t)co * p.R + r) * p.S + s) * p.C + c);
+    } else {   // k-col: B[m][j=(r,s,c)] = x[n, p*st-pad+r, q*st-pad+s, c]
+      const int m = k0 + kc_k, j = n0 + kc_c;
+      if (m >= kend || j >= p.gn) return z4;
+      const int n = m / (p.P * p.Q);
+      const int rem = m - n * p.P * p.Q;
+      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
+      const int c = j % p.C, rs = j / p.C;
+      const int s = rs % p.S, r = rs / p.S;
+      const int y = pp * p.stride - p.pad + r, x = qq * p.stride - p.pad + s;
+      if ((unsigned)y >= (unsigned)p.H || (unsigned)x >= (unsigned)p.W) return z4;
+      return ld4(p.b + (((size_t)n * p.H + y) * p.W + x) * p.C + c);
+    }
+  };
+  auto store_a = [&](int buf, const float4& v) {
+    if constexpr (MODE == F_WGRAD) {
+      st4(&As[buf][kc_k][kc_c], v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[buf][rk_k + e][rk_row] = fget(v, e);
+    }
+  };
+  auto store_b = [&](int buf, const float4& v) {
+    if constexpr (MODE == F_FWD) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[buf][rk_k + e][rk_row] = fget(v, e);
+    } else {
+      st4(&Bs[buf][kc_k][kc_c], v);
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    float4 ra = load_a(kbeg), rb = load_b(kbeg);
+    store_a(0, ra);
+    store_b(0, rb);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const bool nxt = t + 1 < nk;
+      if (nxt) {   // next tile's loads in flight during this tile's MFMAs
+        ra = load_a(kbeg + (t + 1) * FBK);
+        rb = load_b(kbeg + (t + 1) * FBK);
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < FBK / 4; ++k4) {
+        const int kr = k4 * 4 + (lane >> 4);
+        float af[2], bfv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[buf][kr][wr * 32 + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfv[j] = Bs[buf][kr][wc * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+      if (nxt) {
+        store_a(buf ^ 1, ra);
+        store_b(buf ^ 1, rb);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: D element e of lane -> row (lane>>4)*4+e, column lane&15 of its 16x16 tile
+  if constexpr (MODE == F_WGRAD) {
+    float* o = p.out + (size_t)split * p.gm * p.gn;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc * 32 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + e;
+          if (m < p.gm && n < p.gn) o[(size_t)m * p.gn + n] = acc[i][j][e];
+        }
+      }
+  } else {
+    float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wc * 32 + j * 16 + (lane & 15);
+      const bool nok = n < p.gn;
+      const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + e;
+          if (m < p.gm && nok) {
+            float v = acc[i][j][e] + bv;
+            if (p.resid) v += p.resid[(size_t)m * p.gn + n];
+            if (p.relu) v = fmaxf(v, 0.f);
+            p.out[(size_t)m * p.gn + n] = v;
+            cs[j] += v;
+            cq[j] += v * v;
+          }
+        }
+    }
+    if (p.stats) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        cs[j] += __shfl_xor(cs[j], 16, 64);
+        cs[j] += __shfl_xor(cs[j], 32, 64);
+        cq[j] += __shfl_xor(cq[j], 16, 64);
+        cq[j] += __shfl_xor(cq[j], 32, 64);
+        if (lane < 16) {
+          red[wr][0][wc * 32 + j * 16 + lane] = cs[j];
+          red[wr][1][wc * 32 + j * 16 + lane] = cq[j];
+        }
+      }
+      __syncthreads();
+      if (tid < 2 * FBN) {
+        const int q = tid >> 6, c = tid & 63, n = n0 + c;
+        if (n < p.gn) p.stats[((size_t)tile_m * 2 + q) * p.gn + n] = red[0][q][c] + red[1][q][c];
+      }
+    }
+  }
+}
+
+// out[i] (+)= sum_s ws[s][i], fixed split order (deterministic)
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                         int64_t n, int nsplit, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += ws[(size_t)k * n + i];
+    out[i] = accumulate ? out[i] + s : s;
+  }
+}
+
+static void geometry(ConvP& p, int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
+  p.N = N; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.stride = stride; p.pad = pad;
+  p.P = (H + 2 * pad - R) / stride + 1;
+  p.Q = (W + 2 * pad - S) / stride + 1;
+  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.relu = 0;
+}
+
+template <int MODE>
+static void launch(ConvP& p, int nsplit) {
+  p.tiles_m = ceil_div(p.gm, FBM);
+  p.tiles_n = ceil_div(p.gn, FBN);
+  const int grid = p.tiles_m * p.tiles_n * nsplit;
+  if (grid == 0) return;
+  hipLaunchKernelGGL(igemm_f32_kernel<MODE>, dim3(grid), dim3(256), 0, cur_stream(), p);
+  PCMP_LAUNCH_CHECK();
+}
+
+static void check_f32(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), what,
+              ": contiguous fp32 GPU tensor expected");
+}
+
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
+                                 bool relu, bool want_stats) {
+  check_f32(x, "conv_fwd(fp32) x");
+  check_f32(w, "conv_fwd(fp32) w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(3) == x.size(3), "conv_fwd(fp32): NHWC x, KRSC w");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = w.size(0);
+  TORCH_CHECK(C % 4 == 0 && K % 4 == 0, "conv_fwd(fp32): channel counts must be multiples of 4");
+  ConvP p;
+  geometry(p, N, H, W, C, K, w.size(1), w.size(2), stride, pad);
+  p.gm = N * p.P * p.Q; p.gn = K; p.gk = p.R * p.S * C;
+  auto y = at::empty({N, p.P, p.Q, K}, x.options());
+  at::Tensor part;
+  if (want_stats) part = at::empty({ceil_div(p.gm, FBM), 2, K}, x.options());
+  p.a = ptr<float>(x); p.b = ptr<float>(w); p.out = ptr<float>(y);
+  if (bias.has_value() && bias->defined()) { check_f32(*bias, "conv_fwd(fp32) bias"); p.bias = ptr<float>(*bias); }
+  if (resid.has_value() && resid->defined()) {
+    check_f32(*resid, "conv_fwd(fp32) resid");
+    TORCH_CHECK(resid->numel() == y.numel(), "conv_fwd(fp32): residual shape");
+    p.resid = ptr<float>(*resid);
+  }
+  p.relu = relu;
+  p.stats = want_stats ? ptr<float>(part) : nullptr;
+  p.ksplit = p.gk;
+  launch<F_FWD>(p, 1);
+  if (want_stats) return {y, part};
+  return {y};
+}
+
+at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                      const c10::optional<at::Tensor>& resid) {
+  check_f32(dy, "conv_dgrad(fp32) dy");
+  check_f32(w, "conv_dgrad(fp32) w");
+  const int N = dy.size(0), K = w.size(0), C = w.size(3);
+  TORCH_CHECK(C % 4 == 0 && K % 4 == 0, "conv_dgrad(fp32): channel counts must be multiples of 4");
+  ConvP p;
+  geometry(p, N, H, W, C, K, w.size(1), w.size(2), stride, pad);
+  TORCH_CHECK(dy.size(1) == p.P && dy.size(2) == p.Q && dy.size(3) == K, "conv_dgrad(fp32): dy shape");
+  p.gm = N * H * W; p.gn = C; p.gk = p.R * p.S * K;
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  p.a = ptr<float>(dy); p.b = ptr<float>(w); p.out = ptr<float>(dx);
+  if (resid.has_value() && resid->defined()) {
+    check_f32(*resid, "conv_dgrad(fp32) resid");
+    TORCH_CHECK(resid->numel() == dx.numel(), "conv_dgrad(fp32): residual shape");
+    p.resid = ptr<float>(*resid);
+  }
+  p.ksplit = p.gk;
+  launch<F_DGRAD>(p, 1);
+  return dx;
+}
+
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
+                int64_t pad, bool accumulate) {
+  check_f32(dy, "conv_wgrad(fp32) dy");
+  check_f32(x, "conv_wgrad(fp32) x");
+  check_f32(out, "conv_wgrad(fp32) out");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = dy.size(3);
+  TORCH_CHECK(C % 4 == 0 && K % 4 == 0, "conv_wgrad(fp32): channel counts must be multiples of 4");
+  ConvP p;
+  geometry(p, N, H, W, C, K, R, S, stride, pad);
+  TORCH_CHECK(dy.size(1) == p.P && dy.size(2) == p.Q, "conv_wgrad(fp32): dy shape");
+  TORCH_CHECK(out.numel() == (int64_t)K * R * S * C, "conv_wgrad(fp32): out numel");
+  p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
+  p.a = ptr<float>(dy); p.b = ptr<float>(x);
+  const int tiles = ceil_div(p.gm, FBM) * ceil_div(p.gn, FBN);
+  // split the long pixel reduction until ~2 blocks per CU, >= 32 K-steps per split
+  int nsplit = std::max(1, std::min(ceil_div(512, tiles), ceil_div(p.gk, 32 * FBK)));
+  p.ksplit = ceil_div(ceil_div(p.gk, nsplit), FBK) * FBK;
+  nsplit = ceil_div(p.gk, p.ksplit);
+  if (nsplit == 1 && !accumulate) {
+    p.out = ptr<float>(out);
+    launch<F_WGRAD>(p, 1);
+    return;
+  }
+  auto ws = at::empty({nsplit, p.gm, p.gn}, out.options());
+  p.out = ptr<float>(ws);
+  launch<F_WGRAD>(p, nsplit);
+  const int64_t n = (int64_t)p.gm * p.gn;
+  const int grid = (int)std::min<int64_t>(ceil_div(n, (int64_t)256), 2048);
+  hipLaunchKernelGGL(splitk_sum_kernel, dim3(grid), dim3(256), 0, cur_stream(), ptr<float>(ws), ptr<float>(out), n,
+                     nsplit, accumulate ? 1 : 0);
+  PCMP_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------------
+// BatchNorm.  Per-channel partial sums: grid (ceil(C/4 / 64), T) of 256 threads; thread (quad q =
+// 4 channels, row lane rl of 4) sums rows r0 + rl, r0 + rl + 4, ... of its block's row chunk; the 4
+// row lanes are combined through LDS in fixed order.  MODE 0: (sum x, sum x^2); MODE 1: the BN
+// backward (sum g, sum g * xhat[, sum g * xhat2]) with g = dy masked by a mask tensor, mask bits or
+// relu(x * msc + msh) > 0, optionally writing g.
+struct RedP {
+  const float* x;      // MODE 0: the tensor; MODE 1: dy (or dgrad output)
+  const float* mask;   // MODE 1: ymask tensor (> 0 keeps), or null
+  const uint8_t* bits; // MODE 1: mask bits, or null
+  const float* msc; const float* msh;   // MODE 1: mask from relu(bx * msc + msh) > 0
+  const float* bx; const float* mean; const float* istd;
+  const float* bx2; const float* mean2; const float* istd2;
+  float* g;            // MODE 1: masked gradient out (optional)
+  float* part; float* part2;   // [T][2][C]
+  int64_t M; int C; int rows_per;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void chan_reduce_kernel(const RedP p) {
+  __shared__ float sh[3][4][64][4];
+  const int q = blockIdx.x * 64 + (threadIdx.x & 63), rl = threadIdx.x >> 6;
+  const int CQ = p.C / 4;
+  float4 s0 = make_float4(0, 0, 0, 0), s1 = s0, s2 = s0;
+  if (q < CQ) {
+    const int c = q * 4;
+    float4 mu = s0, is = s0, mu2 = s0, is2 = s0, sc = s0, sf = s0;
+    if constexpr (MODE == 1) {
+      mu = ld4(p.mean + c); is = ld4(p.istd + c);
+      if (p.bx2) { mu2 = ld4(p.mean2 + c); is2 = ld4(p.istd2 + c); }
+      if (p.msc) { sc = ld4(p.msc + c); sf = ld4(p.msh + c); }
+    }
+    const int64_t r0 = (int64_t)blockIdx.y * p.rows_per, r1 = std::min<int64_t>(p.M, r0 + p.rows_per);
+    for (int64_t r = r0 + rl; r < r1; r += 4) {
+      const size_t off = (size_t)r * p.C + c;
+      float4 v = ld4(p.x + off);
+      if constexpr (MODE == 0) {
+        s0.x += v.x; s0.y += v.y; s0.z += v.z; s0.w += v.w;
+        s1.x += v.x * v.x; s1.y += v.y * v.y; s1.z += v.z * v.z; s1.w += v.w * v.w;
+      } else {
+        const float4 xb = ld4(p.bx + off);
+        float keep[4] = {1.f, 1.f, 1.f, 1.f};
+        if (p.mask) {
+          const float4 mk = ld4(p.mask + off);
+          keep[0] = mk.x > 0.f; keep[1] = mk.y > 0.f; keep[2] = mk.z > 0.f; keep[3] = mk.w > 0.f;
+        } else if (p.bits) {
+          const unsigned b = p.bits[off >> 3] >> (off & 7);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) keep[e] = (b >> e) & 1u;
+        } else if (p.msc) {
+          keep[0] = xb.x * sc.x + sf.x > 0.f; keep[1] = xb.y * sc.y + sf.y > 0.f;
+          keep[2] = xb.z * sc.z + sf.z > 0.f; keep[3] = xb.w * sc.w + sf.w > 0.f;
+        }
+        v.x = keep[0] ? v.x : 0.f; v.y = keep[1] ? v.y : 0.f; v.z = keep[2] ? v.z : 0.f; v.w = keep[3] ? v.w : 0.f;
+        if (p.g) st4(p.g + off, v);
+        s0.x += v.x; s0.y += v.y; s0.z += v.z; s0.w += v.w;
+        s1.x += v.x * (xb.x - mu.x) * is.x; s1.y += v.y * (xb.y - mu.y) * is.y;
+        s1.z += v.z * (xb.z - mu.z) * is.z; s1.w += v.w * (xb.w - mu.w) * is.w;
+        if (p.bx2) {
+          const float4 x2 = ld4(p.bx2 + off);
+          s2.x += v.x * (x2.x - mu2.x) * is2.x; s2.y += v.y * (x2.y - mu2.y) * is2.y;
+          s2.z += v.z * (x2.z - mu2.z) * is2.z; s2.w += v.w * (x2.w - mu2.w) * is2.w;
+        }
+      }
+    }
+  }
+  const int ql = threadIdx.x & 63;
+  sh[0][rl][ql][0] = s0.x; sh[0][rl][ql][1] = s0.y; sh[0][rl][ql][2] = s0.z; sh[0][rl][ql][3] = s0.w;
+  sh[1][rl][ql][0] = s1.x; sh[1][rl][ql][1] = s1.y; sh[1][rl][ql][2] = s1.z; sh[1][rl][ql][3] = s1.w;
+  sh[2][rl][ql][0] = s2.x; sh[2][rl][ql][1] = s2.y; sh[2][rl][ql][2] = s2.z; sh[2][rl][ql][3] = s2.w;
+  __syncthreads();
+  // 3 sums x 64 quads x 4 channels = 768 outputs over 256 threads
+  for (int o = threadIdx.x; o < 3 * 256; o += 256) {
+    const int which = o >> 8, rem = o & 255, qq = rem >> 2, e = rem & 3;
+    const int qg = blockIdx.x * 64 + qq;
+    if (qg >= CQ) continue;
+    const float v = (sh[which][0][qq][e] + sh[which][1][qq][e]) + (sh[which][2][qq][e] + sh[which][3][qq][e]);
+    const int c = qg * 4 + e;
+    const size_t base = (size_t)blockIdx.y * 2 * p.C;
+    if (which == 0) {
+      p.part[base + c] = v;
+      if (p.part2) p.part2[base + c] = v;
+    } else if (which == 1) {
+      p.part[base + p.C + c] = v;
+    } else if (p.part2) {
+      p.part2[base + p.C + c] = v;
+    }
+  }
+}
+
+static void launch_reduce(RedP& p, int mode, const at::TensorOptions& o, at::Tensor& part, at::Tensor* part2) {
+  TORCH_CHECK(p.C % 4 == 0, "fp32 BN kernels: channels must be a multiple of 4");
+  const int64_t T64 = std::max<int64_t>(1, std::min<int64_t>(1024, (p.M + 255) / 256));
+  p.rows_per = (int)((p.M + T64 - 1) / T64);
+  const int T = (int)((p.M + p.rows_per - 1) / p.rows_per);
+  part = at::empty({std::max(T, 1), 2, p.C}, o);
+  p.part = ptr<float>(part);
+  p.part2 = nullptr;
+  if (part2) {
+    *part2 = at::empty({std::max(T, 1), 2, p.C}, o);
+    p.part2 = ptr<float>(*part2);
+  }
+  if (p.M == 0) { part.zero_(); if (part2) part2->zero_(); return; }
+  dim3 grid(ceil_div(p.C / 4, 64), T);
+  if (mode == 0) hipLaunchKernelGGL(chan_reduce_kernel<0>, grid, dim3(256), 0, cur_stream(), p);
+  else hipLaunchKernelGGL(chan_reduce_kernel<1>, grid, dim3(256), 0, cur_stream(), p);
+  PCMP_LAUNCH_CHECK();
+}
+
+static RedP red_params() {
+  RedP p;
+  p.x = nullptr; p.mask = nullptr; p.bits = nullptr; p.msc = nullptr; p.msh = nullptr;
+  p.bx = nullptr; p.mean = nullptr; p.istd = nullptr; p.bx2 = nullptr; p.mean2 = nullptr; p.istd2 = nullptr;
+  p.g = nullptr; p.part = nullptr; p.part2 = nullptr; p.M = 0; p.C = 0; p.rows_per = 1;
+  return p;
+}
+
+at::Tensor bn_partials(const at::Tensor& x) {
+  check_f32(x, "bn_partials(fp32)");
+  RedP p = red_params();
+  p.C = x.size(-1);
+  p.M = x.numel() / p.C;
+  p.x = ptr<float>(x);
+  at::Tensor part;
+  launch_reduce(p, 0, x.options(), part, nullptr);
+  return part;
+}
+
+// masked BN-backward reduction; writes g when asked.  Returns [g?, part, part2?]
+static std::vector<at::Tensor> masked_reduce(const at::Tensor& dy, const float* mask, const uint8_t* bits,
+                                             const float* msc, const float* msh, const at::Tensor& x,
+                                             const at::Tensor& mean, const at::Tensor& invstd,
+                                             const c10::optional<at::Tensor>& x2,
+                                             const c10::optional<at::Tensor>& mean2,
+                                             const c10::optional<at::Tensor>& invstd2, bool want_g) {
+  check_f32(dy, "bn backward(fp32) dy");
+  check_f32(x, "bn backward(fp32) x");
+  TORCH_CHECK(x.numel() == dy.numel(), "bn backward(fp32): shapes");
+  RedP p = red_params();
+  p.C = x.size(-1);
+  p.M = x.numel() / p.C;
+  p.x = ptr<float>(dy); p.mask = mask; p.bits = bits; p.msc = msc; p.msh = msh;
+  p.bx = ptr<float>(x); p.mean = ptr<float>(mean); p.istd = ptr<float>(invstd);
+  const bool two = x2.has_value() && x2->defined();
+  if (two) {
+    check_f32(*x2, "bn backward(fp32) x2");
+    p.bx2 = ptr<float>(*x2); p.mean2 = ptr<float>(*mean2); p.istd2 = ptr<float>(*invstd2);
+  }
+  at::Tensor g;
+  if (want_g) { g = at::empty_like(dy); p.g = ptr<float>(g); }
+  at::Tensor part, part2;
+  launch_reduce(p, 1, x.options(), part, two ? &part2 : nullptr);
+  std::vector<at::Tensor> r;
+  if (want_g) r.push_back(g);
+  r.push_back(part);
+  if (two) r.push_back(part2);
+  return r;
+}
+
+std::vector<at::Tensor> bn_bwd_reduce(const at::Tensor& dy, const c10::optional<at::Tensor>& ymask,
+                                      const at::Tensor& x, const at::Tensor& mean, const at::Tensor& invstd,
+                                      const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                                      const c10::optional<at::Tensor>& invstd2) {
+  const float* mk = nullptr;
+  if (ymask.has_value() && ymask->defined()) { check_f32(*ymask, "bn_bwd_reduce(fp32) ymask"); mk = ptr<float>(*ymask); }
+  return masked_reduce(dy, mk, nullptr, nullptr, nullptr, x, mean, invstd, x2, mean2, invstd2, false);
+}
+
+std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
+                                       int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
+                                       const c10::optional<at::Tensor>& ymask, const at::Tensor& x,
+                                       const at::Tensor& mean, const at::Tensor& invstd,
+                                       const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& mean2,
+                                       const c10::optional<at::Tensor>& invstd2, const c10::optional<at::Tensor>& mscale,
+                                       const c10::optional<at::Tensor>& mshift,
+                                       const c10::optional<at::Tensor>& ymask_bits) {
+  at::Tensor dx = conv_dgrad(dy, w, H, W, stride, pad, resid);
+  const float* mk = nullptr;
+  const uint8_t* bits = nullptr;
+  const float *msc = nullptr, *msh = nullptr;
+  if (ymask_bits.has_value() && ymask_bits->defined()) {
+    TORCH_CHECK(ymask_bits->scalar_type() == at::kByte && ymask_bits->numel() * 8 >= dx.numel(), "mask bits");
+    bits = ymask_bits->data_ptr<uint8_t>();
+  } else if (ymask.has_value() && ymask->defined()) {
+    check_f32(*ymask, "conv_dgrad_bnr(fp32) ymask");
+    mk = ptr<float>(*ymask);
+  } else if (mscale.has_value() && mscale->defined()) {
+    msc = ptr<float>(*mscale);
+    msh = ptr<float>(*mshift);
+  }
+  return masked_reduce(dx, mk, bits, msc, msh, x, mean, invstd, x2, mean2, invstd2, true);
+}
+
+// y = x*scale + shift (+ x2*scale2 + shift2 | + x2) (relu); 8 elements per thread (mask bits byte)
+__global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                                                       const float* __restrict__ sf, const float* __restrict__ x2,
+                                                       const float* __restrict__ sc2, const float* __restrict__ sf2,
+                                                       int relu, float* __restrict__ y, uint8_t* __restrict__ bits,
+                                                       int64_t n8, int C) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t off = (size_t)i * 8;
+    const int c = (int)(off % C);
+    unsigned byte = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = c + 4 * h;
+      float4 v = ld4(x + off + 4 * h);
+      const float4 a = ld4(sc + ch), b = ld4(sf + ch);
+      v.x = v.x * a.x + b.x; v.y = v.y * a.y + b.y; v.z = v.z * a.z + b.z; v.w = v.w * a.w + b.w;
+      if (x2) {
+        float4 u = ld4(x2 + off + 4 * h);
+        if (sc2) {
+          const float4 a2 = ld4(sc2 + ch), b2 = ld4(sf2 + ch);
+          u.x = u.x * a2.x + b2.x; u.y = u.y * a2.y + b2.y; u.z = u.z * a2.z + b2.z; u.w = u.w * a2.w + b2.w;
+        }
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
+      if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      st4(y + off + 4 * h, v);
+      byte |= ((v.x > 0.f) | ((v.y > 0.f) << 1) | ((v.z > 0.f) << 2) | ((v.w > 0.f) << 3)) << (4 * h);
+    }
+    if (bits) bits[i] = (uint8_t)byte;
+  }
+}
+
+static int grid_n(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
+
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
+                    const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
+                    const c10::optional<at::Tensor>& shift2, bool relu, const c10::optional<at::Tensor>& mbits) {
+  check_f32(x, "bn_apply(fp32) x");
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "bn_apply(fp32): channels must be a multiple of 8");
+  auto y = at::empty_like(x);
+  const float* px2 = nullptr;
+  const float *ps2 = nullptr, *pf2 = nullptr;
+  if (x2.has_value() && x2->defined()) {
+    check_f32(*x2, "bn_apply(fp32) x2");
+    px2 = ptr<float>(*x2);
+    if (scale2.has_value() && scale2->defined()) { ps2 = ptr<float>(*scale2); pf2 = ptr<float>(*shift2); }
+  }
+  uint8_t* bits = nullptr;
+  if (mbits.has_value() && mbits->defined()) {
+    TORCH_CHECK(mbits->scalar_type() == at::kByte && mbits->numel() * 8 == x.numel(), "bn_apply(fp32): mbits");
+    bits = mbits->data_ptr<uint8_t>();
+  }
+  const int64_t n8 = x.numel() / 8;
+  if (n8 == 0) return y;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_n(n8)), dim3(256), 0, cur_stream(), ptr<float>(x), ptr<float>(scale),
+                     ptr<float>(shift), px2, ps2, pf2, relu ? 1 : 0, ptr<float>(y), bits, n8, C);
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+// out = k1*g + k2*x + k3 (and the same with x2 / coef2), g = masked dy (optionally returned)
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const float* __restrict__ dy, const float* __restrict__ mk,
+                                                           const float* __restrict__ x, const float* __restrict__ coef,
+                                                           const float* __restrict__ x2, const float* __restrict__ coef2,
+                                                           float* __restrict__ out, float* __restrict__ out2,
+                                                           float* __restrict__ gout, int64_t n4, int C) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const size_t off = (size_t)i * 4;
+    const int c = (int)(off % C);
+    float4 g = ld4(dy + off);
+    if (mk) {
+      const float4 m = ld4(mk + off);
+      g.x = m.x > 0.f ? g.x : 0.f; g.y = m.y > 0.f ? g.y : 0.f; g.z = m.z > 0.f ? g.z : 0.f; g.w = m.w > 0.f ? g.w : 0.f;
+    }
+    const float4 xv = ld4(x + off);
+    const float4 k1 = ld4(coef + c), k2 = ld4(coef + C + c), k3 = ld4(coef + 2 * C + c);
+    st4(out + off, make_float4(k1.x * g.x + k2.x * xv.x + k3.x, k1.y * g.y + k2.y * xv.y + k3.y,
+                               k1.z * g.z + k2.z * xv.z + k3.z, k1.w * g.w + k2.w * xv.w + k3.w));
+    if (x2) {
+      const float4 u = ld4(x2 + off);
+      const float4 a1 = ld4(coef2 + c), a2 = ld4(coef2 + C + c), a3 = ld4(coef2 + 2 * C + c);
+      st4(out2 + off, make_float4(a1.x * g.x + a2.x * u.x + a3.x, a1.y * g.y + a2.y * u.y + a3.y,
+                                  a1.z * g.z + a2.z * u.z + a3.z, a1.w * g.w + a2.w * u.w + a3.w));
+    }
+    if (gout) st4(gout + off, g);
+  }
+}
+
+std::vector<at::Tensor> bn_bwd_apply(const at::Tensor& dy, const c10::optional<at::Tensor>& ymask,
+                                     const at::Tensor& x, const at::Tensor& coef,
+                                     const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& coef2,
+                                     bool want_g) {
+  check_f32(dy, "bn_bwd_apply(fp32) dy");
+  check_f32(x, "bn_bwd_apply(fp32) x");
+  const int C = x.size(-1);
+  TORCH_CHECK(C % 4 == 0, "bn_bwd_apply(fp32): channels must be a multiple of 4");
+  const float* mk = nullptr;
+  if (ymask.has_value() && ymask->defined()) { check_f32(*ymask, "bn_bwd_apply(fp32) ymask"); mk = ptr<float>(*ymask); }
+  std::vector<at::Tensor> r{at::empty_like(dy)};
+  const bool two = x2.has_value() && x2->defined();
+  if (two) r.push_back(at::empty_like(dy));
+  at::Tensor g;
+  if (want_g) { g = at::empty_like(dy); r.push_back(g); }
+  const int64_t n4 = dy.numel() / 4;
+  if (n4 == 0) return r;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_n(n4)), dim3(256), 0, cur_stream(), ptr<float>(dy), mk,
+                     ptr<float>(x), ptr<float>(coef), two ? ptr<float>(*x2) : nullptr,
+                     two ? ptr<float>(*coef2) : nullptr, ptr<float>(r[0]), two ? ptr<float>(r[1]) : nullptr,
+                     want_g ? ptr<float>(g) : nullptr, n4, C);
+  PCMP_LAUNCH_CHECK();
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// pooling: max pool with an optional BN + ReLU prologue (the stem) and uint8 window indices
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                                                          const float* __restrict__ sf, float* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                          int P, int Q, int k, int s, int pad) {
+  const int64_t total = (int64_t)N * P * Q * C;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = t % C;
+    int64_t r = t / C;
+    const int q = r % Q; r /= Q;
+    const int pp = r % P;
+    const int n = r / P;
+    float best = -INFINITY;
+    int bi = 0;
+    for (int i = 0; i < k; ++i) {
+      const int h = pp * s - pad + i;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int j = 0; j < k; ++j) {
+        const int w = q * s - pad + j;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float v = x[(((size_t)n * H + h) * W + w) * C + c];
+        if (sc) v = fmaxf(v * sc[c] + sf[c], 0.f);
+        if (v > best) { best = v; bi = i * k + j; }
+      }
+    }
+    y[t] = best;
+    if (idx) idx[t] = (uint8_t)bi;
+  }
+}
+
+std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
+                                    const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift) {
+  check_f32(x, "maxpool_fwd(fp32)");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  auto y = at::empty({N, P, Q, C}, x.options());
+  at::Tensor idx;
+  if (want_idx) idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  const bool bn = scale.has_value() && scale->defined();
+  if (y.numel())
+    hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_n(y.numel())), dim3(256), 0, cur_stream(), ptr<float>(x),
+                       bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr, ptr<float>(y),
+                       want_idx ? idx.data_ptr<uint8_t>() : nullptr, N, H, W, C, P, Q, (int)k, (int)s, (int)pad);
+  PCMP_LAUNCH_CHECK();
+  if (want_idx) return {y, idx};
+  return {y};
+}
+
+// gather form: each input element sums the output gradients whose window argmax it is
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const float* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                          float* __restrict__ dx, int N, int H, int W, int C, int P,
+                                                          int Q, int k, int s, int pad) {
+  const int64_t total = (int64_t)N * H * W * C;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = t % C;
+    int64_t r = t / C;
+    const int w = r % W; r /= W;
+    const int h = r % H;
+    const int n = r / H;
+    float acc = 0.f;
+    const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
+    const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
+    for (int pp = p_lo; pp <= p_hi; ++pp) {
+      const int i = h - (pp * s - pad);
+      if (i < 0 || i >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int j = w - (q * s - pad);
+        if (j < 0 || j >= k) continue;
+        const size_t o = (((size_t)n * P + pp) * Q + q) * C + c;
+        if (idx[o] == i * k + j) acc += dy[o];
+      }
+    }
+    dx[t] = acc;
+  }
+}
+
+at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W, int64_t k, int64_t s,
+                       int64_t pad) {
+  check_f32(dy, "maxpool_bwd(fp32)");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == dy.numel(), "maxpool_bwd(fp32): idx");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  if (dx.numel())
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_n(dx.numel())), dim3(256), 0, cur_stream(), ptr<float>(dy),
+                       idx.data_ptr<uint8_t>(), ptr<float>(dx), N, (int)H, (int)W, C, P, Q, (int)k, (int)s, (int)pad);
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& cx,
+                                        const at::Tensor& mean, const at::Tensor& invstd, const at::Tensor& scale,
+                                        const at::Tensor& shift, int64_t k, int64_t s, int64_t pad) {
+  at::Tensor g = maxpool_bwd(dy, idx, cx.size(1), cx.size(2), k, s, pad);
+  c10::optional<at::Tensor> none;
+  return masked_reduce(g, nullptr, nullptr, ptr<float>(scale), ptr<float>(shift), cx, mean, invstd, none, none, none,
+                       true);
+}
+
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int N,
+                                                      int HW, int C) {
+  const int64_t total = (int64_t)N * C;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = t % C, n = t / C;
+    float s = 0.f;
+    for (int i = 0; i < HW; ++i) s += x[((size_t)n * HW + i) * C + c];
+    y[t] = s / (float)HW;
+  }
+}
+
+at::Tensor gap_fwd(const at::Tensor& x) {
+  check_f32(x, "gap_fwd(fp32)");
+  const int N = x.size(0), C = x.size(-1);
+  const int HW = x.numel() / ((int64_t)N * C);
+  auto y = at::empty({N, C}, x.options());
+  if (y.numel())
+    hipLaunchKernelGGL(gap_fwd_kernel, dim3(grid_n(y.numel())), dim3(256), 0, cur_stream(), ptr<float>(x),
+                       ptr<float>(y), N, HW, C);
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const float* __restrict__ dy, float* __restrict__ dx, int N,
+                                                      int HW, int C) {
+  const int64_t total = (int64_t)N * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int c = t % C;
+    const int n = t / ((int64_t)HW * C);
+    dx[t] = dy[(size_t)n * C + c] * inv;
+  }
+}
+
+at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
+  check_f32(dy, "gap_bwd(fp32)");
+  const int N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  if (dx.numel())
+    hipLaunchKernelGGL(gap_bwd_kernel, dim3(grid_n(dx.numel())), dim3(256), 0, cur_stream(), ptr<float>(dy),
+                       ptr<float>(dx), N, (int)(H * W), C);
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+// dropout with the bf16 kernel's counter RNG (same keep mask for the same seed / offset / index)
+__global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                                      float p, uint64_t seed, uint64_t offset) {
+  const float scale = 1.f / (1.f - p);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = uniform01(seed, offset + i) >= p ? x[i] * scale : 0.f;
+}
+
+at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
+  check_f32(x, "dropout(fp32)");
+  auto y = at::empty_like(x);
+  if (x.numel())
+    hipLaunchKernelGGL(dropout_kernel, dim3(grid_n(x.numel())), dim3(256), 0, cur_stream(), ptr<float>(x),
+                       ptr<float>(y), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset);
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                       float* __restrict__ dx, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dx[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y) {
+  check_f32(dy, "relu_bwd(fp32) dy");
+  check_f32(y, "relu_bwd(fp32) y");
+  auto dx = at::empty_like(dy);
+  if (dy.numel())
+    hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_n(dy.numel())), dim3(256), 0, cur_stream(), ptr<float>(dy),
+                       ptr<float>(y), ptr<float>(dx), dy.numel());
+  PCMP_LAUNCH_CHECK();
+  return dx;
+}
+
+void colsum(const at::Tensor& x, at::Tensor out, bool accumulate) {
+  check_f32(x, "colsum(fp32) x");
+  check_f32(out, "colsum(fp32) out");
+  RedP p = red_params();
+  p.C = x.size(-1);
+  p.M = x.numel() / p.C;
+  TORCH_CHECK(out.numel() >= p.C, "colsum(fp32): out");
+  p.x = ptr<float>(x);
+  at::Tensor part;
+  launch_reduce(p, 0, x.options(), part, nullptr);   // rows [T][0][C] = column sums (second row unused)
+  launch_col_reduce(ptr<float>(part), part.size(0), 2 * p.C, ptr<float>(out), accumulate, cur_stream(), nullptr, p.C);
+}
+
+}  // namespace f32
+}  // namespace pcmp

@@ -20,6 +20,7 @@
 // LDS-staged epilogue that writes 16-byte coalesced rows and emits per-column BatchNorm partial
 // statistics of the stored (bf16-rounded) output.
 #include "common.h"
+#include "f32.h"
 
 #include <algorithm>
 #include <mutex>
@@ -875,8 +876,13 @@ constexpr int NT8 = 512;
 constexpr int BM8 = 256;
 
 
-template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI, int EPD = 2>
+// SCHED: 0 = lock-step 4-phase schedule (DMA of tile t+1 issued during tile t), 1 = wave-row
+// staggered READ / MFMA slots (8 waves), 2 = early prefetch (each half-tile of tile t+2 is DMA'd
+// into the buffer being read as soon as its tile-t half has been consumed: 4-7 phases of lead
+// instead of 3, one counted vmcnt per K-tile)
+template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI, int EPD = 2, int SCHED = 0>
 __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams p) {
+  constexpr bool STAG = SCHED == 1;
   constexpr int NW = NTHR / 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1032,11 +1038,112 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][j][kk], fa[i][kk], acc[nh * TNH + j][mh * TMH + i], 0, 0, 0);
   };
 
+  if constexpr (SCHED == 2) {
+    // per-tile tap state (the halves of tiles t+1 and t+2 are in flight together)
+    struct KS { int k0, kc, ks, kr; };
+    auto adv = [&](KS st) {
+      st.k0 += BK; st.kc += BK;
+      if (st.kc >= CIN) { st.kc = 0; if (++st.ks == p.S) { st.ks = 0; ++st.kr; } }
+      return st;
+    };
+    auto set_state = [&](const KS& st) { k0 = st.k0; kc = st.kc; ks = st.ks; kr = st.kr; };
+    const KS s0{k0, kc, ks, kr};
+    KS s1 = adv(s0), s2 = adv(s1);
+    // prologue: all of tile 0 (buffer 0), then A0, B1, A1 of tile 1 (buffer 1)
+    issue_a(0, 0); issue_b(0, 0); issue_b(1, 0); issue_a(1, 0);
+    if (nk > 1) {
+      set_state(s1);
+      issue_a(0, 1); issue_b(1, 1); issue_a(1, 1);
+      wait_vm<2 * NA + NB>();
+    } else {
+      wait_vm<0>();
+    }
+    lds_barrier();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1, nb = buf ^ 1;
+      const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+      // P0: quadrant (0,0); DMA B0(t+1) into nb (its tile t-1 B0 was last read in P3(t-1))
+      read_a(0, buf); read_b(0, buf);
+      if (has1) { set_state(s1); issue_b(0, nb); }
+      mma(0, 0);
+      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+      // P1: quadrant (0,1); DMA A0(t+2) into buf (A0(t) read in P0)
+      read_b(1, buf);
+      if (has2) { set_state(s2); issue_a(0, buf); }
+      mma(0, 1);
+      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+      // P2: quadrant (1,1); DMA B1(t+2) into buf (B1(t) read in P1)
+      read_a(1, buf);
+      if (has2) issue_b(1, buf);
+      mma(1, 1);
+      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+      // P3: quadrant (1,0); DMA A1(t+2) into buf (A1(t) read in P2); retire all of tile t+1
+      read_b(0, buf);
+      if (has2) issue_a(1, buf);
+      mma(1, 0);
+      if (has2) wait_vm<2 * NA + NB>(); else wait_vm<0>();
+      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+      s1 = s2;
+      s2 = adv(s2);
+    }
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
+    return;
+  }
+
   // ---- prologue: tile 0 complete in buffer 0
   issue_a(0, 0); issue_b(0, 0); issue_b(1, 0); issue_a(1, 0);
   advance();
   wait_vm<0>();
   lds_barrier();
+
+  if constexpr (STAG) {
+    // Wave-row-staggered schedule (8 waves, 1 block per CU; cdna_hip_programming.md §5 "the 256^2
+    // 8-phase template").  Every quadrant phase q is split into a READ slot (its LDS fragment reads,
+    // the LDS-DMA of one half-tile of tile t+1, the counted vmcnt wait) and an MFMA slot, each
+    // closed by a workgroup barrier.  Wave row 1 starts one barrier late, so on every SIMD (one wave
+    // of each row) one wave issues its LDS reads / DMA while the other runs its 16 MFMAs: the matrix
+    // pipe no longer idles while both lock-stepped waves wait for their fragments.
+    //   slot s: row 0 runs its program slot s, row 1 its slot s-1.  Reads of half H(t) by row 0 in
+    //   READ_q come after barrier 8t+2q-1, which both rows pass only after the wait retiring H(t)
+    //   that sits in their READ_{q-1}: the retire point is one phase ahead of the first read, for
+    //   either row (hazard table in docs/PERF_NOTES.md, round 3).  The DMA of tile t+1 into buffer
+    //   nb starts at READ_0(t) of row 0, after row 1 has finished reading tile t-1 (its last reads,
+    //   READ_3(t-1), complete before its MFMA slot and the barrier that closes it).
+    const bool row1 = (__builtin_amdgcn_readfirstlane(tid >> 6) / WN) == 1;   // wave-uniform (SGPR) branch
+    auto mma_slot = [&](int mh, int nh) {
+      lds_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mma(mh, nh);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      lds_barrier();
+    };
+    if (row1) lds_barrier();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1, nb = buf ^ 1;
+      const bool nxt = t + 1 < nk;
+      // READ_0: A0, B0 of t; DMA A0(t+1); retire B1(t)
+      read_a(0, buf); read_b(0, buf);
+      if (nxt) { issue_a(0, nb); wait_vm<2 * NA>(); } else wait_vm<NA>();
+      mma_slot(0, 0);
+      // READ_1: B1 of t; DMA B0(t+1); retire A1(t)
+      read_b(1, buf);
+      if (nxt) { issue_b(0, nb); wait_vm<NA + NB>(); } else wait_vm<0>();
+      mma_slot(0, 1);
+      // READ_2: A1 of t; DMA B1(t+1)
+      read_a(1, buf);
+      if (nxt) issue_b(1, nb);
+      mma_slot(1, 1);
+      // READ_3: B0 of t (again); DMA A1(t+1); retire A0(t+1), B0(t+1) for READ_0(t+1)
+      read_b(0, buf);
+      if (nxt) { issue_a(1, nb); advance(); wait_vm<NA + NB>(); }
+      mma_slot(1, 0);
+    }
+    if (!row1) lds_barrier();   // re-align the rows: every wave's LDS reads are done past here
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
+    return;
+  }
 
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1, nb = buf ^ 1;
@@ -1900,6 +2007,11 @@ static int igemm8_min_tiles() {
   return v;
 }
 
+// 8-wave LDS-DMA kernel with the wave-row-staggered READ / MFMA schedule (STAG): A/B knob
+static Knob kn_dma8_stag("dma8_stag", 0);   // measured null (profiles/r3_stagger_ab.txt)
+// early-prefetch schedule (SCHED 2): bit 0 the 4-wave kernels, bit 1 the 8-wave kernel
+static Knob kn_dma_pf2("dma_pf2", 0);
+
 template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB>
 static void launch_dma(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
@@ -1921,13 +2033,22 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
 #define PCMP_DMA_LAUNCH(E)                                                                              \
   do {                                                                                                \
     constexpr bool can_deep = (E == EPI_BNR || E == EPI_BNR2) && NTHR == 256;                                        \
+    constexpr bool can_stag = NTHR == NT8 && WM == 2;                                                 \
     auto kfn = (can_deep && (E == EPI_BNR2 ? kn_epi_depth_bnr2 : kn_epi_depth).get() >= 4)                         \
                    ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>                                     \
                                                      : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>; \
+    if (can_stag && kn_dma8_stag.get()) kfn = &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, can_stag ? 1 : 0>; \
+    if (kn_dma_pf2.get() & (NTHR == NT8 ? 2 : 1))                                                     \
+      kfn = (can_deep && (E == EPI_BNR2 ? kn_epi_depth_bnr2 : kn_epi_depth).get() >= 4)              \
+                ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4, 2>                        \
+                : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, 2>;                       \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
       for (auto f : {&igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>,                       \
-                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>})                      \
+                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>,                       \
+                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, can_stag ? 1 : 0>,       \
+                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, 2>,                    \
+                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4, 2>})                   \
         PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f),                          \
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
       attr_set = true;                                                                                \
@@ -2534,6 +2655,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  const c10::optional<at::Tensor>& bias,
                                  const c10::optional<at::Tensor>& resid, bool relu, bool want_stats) {
+  if (x.scalar_type() == at::kFloat) return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats);
   PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(x); PCMP_CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: NHWC x and KRSC w expected");
@@ -2795,6 +2917,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
 // place into the residual buffer, which is CONSUMED (its memory becomes dx).
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride,
                       int64_t pad, const c10::optional<at::Tensor>& resid, const c10::optional<at::Tensor>& wt) {
+  if (dy.scalar_type() == at::kFloat) return f32::conv_dgrad(dy, w, H, W, stride, pad, resid);
   return dgrad_impl(dy, w, H, W, stride, pad, resid, nullptr, wt)[0];
 }
 
@@ -2811,6 +2934,9 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& mshift,
                                        const c10::optional<at::Tensor>& wt,
                                        const c10::optional<at::Tensor>& ymask_bits) {
+  if (dy.scalar_type() == at::kFloat)
+    return f32::conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2, mean2, invstd2, mscale,
+                               mshift, ymask_bits);
   const int64_t n = (int64_t)dy.size(0) * H * W * w.size(3);
   auto chk = [&](const at::Tensor& t, const char* nm) {
     PCMP_CHECK_BF16(t); PCMP_CHECK_CONTIG(t);
@@ -2944,6 +3070,7 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
 // dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
                 int64_t stride, int64_t pad, bool accumulate) {
+  if (dy.scalar_type() == at::kFloat) return f32::conv_wgrad(dy, x, out, R, S, stride, pad, accumulate);
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(x);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = dy.size(3);

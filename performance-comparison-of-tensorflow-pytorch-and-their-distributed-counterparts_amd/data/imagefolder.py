@@ -12,7 +12,10 @@ Parity with the reference's torchvision usage:
     flip, CenterCrop 224, ToTensor, ImageNet Normalize) / (Resize 256, CenterCrop 224, ...);
   * ``preprocess_single`` — B6; Keras variants in :mod:`pcmp.models.keras_resnet` (B7/B8).
 Decoded batches are uint8 NCHW host tensors (pinned when a GPU is present); the fused device
-kernel ``nchw_to_nhwc`` does the /255 scaling and layout change on the GPU.
+kernel ``nchw_to_nhwc`` does the /255 scaling and layout change on the GPU.  With
+``device_resize=True`` (the default when batches go to a GPU) the host only decodes the JPEG: the
+raw uint8 HWC image is copied to the device and ``resize_image`` (csrc/elementwise.hip) runs
+Pillow's bilinear resize there, bit-identical to ``PIL.Image.resize(..., BILINEAR)``.
 """
 from __future__ import annotations
 
@@ -61,14 +64,48 @@ class ImageFolder:
             a = np.asarray(im, dtype=np.uint8)
         return torch.from_numpy(a.copy()).permute(2, 0, 1), y
 
-    def get_batch(self, idx, device=None):
+    def load_raw(self, i):
+        """Decode only: uint8 HWC at the file's own size (the resize runs on the device)."""
+        Image = _pil()
+        path, y = self.samples[i]
+        with Image.open(path) as im:
+            a = np.asarray(im.convert("RGB"), dtype=np.uint8)
+        return torch.from_numpy(a.copy()), y
+
+    def get_batch(self, idx, device=None, device_resize=None):
+        on_gpu = device is not None and torch.device(device).type == "cuda"
+        if device_resize is None:
+            device_resize = on_gpu
+        if device_resize and on_gpu:
+            items = list(self.pool.map(self.load_raw, list(idx)))
+            x = torch.cat([resize_on_device(t, self.size, device) for t, _ in items])
+            y = torch.tensor([l for _, l in items], dtype=torch.long).to(device, non_blocking=True)
+            return x, y
         items = list(self.pool.map(self.load, list(idx)))
         x = torch.stack([t for t, _ in items])
         y = torch.tensor([l for _, l in items], dtype=torch.long)
-        if device is not None and torch.device(device).type == "cuda":
+        if on_gpu:
             x = x.pin_memory().to(device, non_blocking=True)
             y = y.to(device, non_blocking=True)
         return x, y
+
+
+def resize_on_device(img_hwc_u8: torch.Tensor, size, device, out="u8", cpad=8, scale=1.0, mean=None, std=None):
+    """One decoded image (uint8 HWC, host) -> device, Pillow-exact bilinear resize to ``size`` there.
+    ``out="u8"``: uint8 [1,3,S,S] (ToTensor happens in the model's input conversion); ``"bf16"`` /
+    ``"f32"``: the fused model input, NHWC [1,S,S,cpad] of (u8 * scale - mean) / std."""
+    from ..ops.kernels import K
+    s = (size, size) if isinstance(size, int) else tuple(size)
+    x = img_hwc_u8
+    if x.dim() == 3:
+        x = x.unsqueeze(0)
+    if not x.is_cuda:
+        x = x.pin_memory().to(device, non_blocking=True)
+    mode = {"u8": 0, "bf16": 1, "f32": 2}[out]
+    if mean is not None:
+        mean = torch.as_tensor(mean, dtype=torch.float32, device=x.device)
+        std = torch.as_tensor(std, dtype=torch.float32, device=x.device)
+    return K.resize_image(x.contiguous(), s[0], s[1], mode, cpad, scale, mean, std)
 
 
 def load_split_train_test(datadir, valid_size=0.2, batch_size=64, distributed=False, device=None,
@@ -123,11 +160,16 @@ def get_image_paths(root):
     return paths
 
 
-def preprocess_single(path, size=224):
-    """B6: PIL open -> RGB -> Resize -> ToTensor -> unsqueeze(0) (float NCHW in [0,1])."""
+def preprocess_single(path, size=224, device=None):
+    """B6: PIL open -> RGB -> Resize -> ToTensor -> unsqueeze(0) (float NCHW in [0,1]).  With a GPU
+    ``device`` only the decode runs on the host; the resize runs on the device (``resize_image``)."""
     Image = _pil()
     with Image.open(path) as im:
-        a = np.asarray(im.convert("RGB").resize((size, size), Image.BILINEAR), dtype=np.float32) / 255.0
+        im = im.convert("RGB")
+        if device is not None and torch.device(device).type == "cuda":
+            raw = torch.from_numpy(np.asarray(im, dtype=np.uint8).copy())
+            return resize_on_device(raw, size, device).float() / 255.0
+        a = np.asarray(im.resize((size, size), Image.BILINEAR), dtype=np.float32) / 255.0
     return torch.from_numpy(a).permute(2, 0, 1).unsqueeze(0)
 
 

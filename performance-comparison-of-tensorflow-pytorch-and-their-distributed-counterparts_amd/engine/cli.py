@@ -36,8 +36,8 @@ def common_parser(desc):
     ap.add_argument("--kernels", choices=["hip", "torch"], default="hip",
                     help="torch = PyTorch reference ops (parity runs only)")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
-                    help="bf16 = HIP kernels (default); fp32 = the reference's precision as an explicit "
-                         "parity mode on the PyTorch reference ops (the HIP kernels are bf16-only)")
+                    help="compute precision of the HIP kernels: bf16 (default) or fp32, the reference's "
+                         "precision (fp32 kernels of csrc/f32.hip)")
     ap.add_argument("--weights", default=None,
                     help="pretrained weights (torchvision ResNet/VGG or HF BERT state_dict; .pth/.pt loaded with "
                          "torch.load(weights_only=True), or .safetensors) -- the reference's pretrained backbones")
@@ -70,7 +70,7 @@ def setup(args):
     from ..parallel import launch
     from ..utils.misc import seed_everything
     _lib.set_backend(args.kernels)
-    _lib.set_precision(getattr(args, "dtype", "bf16"))   # fp32 also selects the reference ops
+    _lib.set_precision(getattr(args, "dtype", "bf16"))
     use_gpu = torch.cuda.is_available() if args.device == "auto" else args.device == "cuda"
     env = launch.init(args.local_rank, use_gpu=use_gpu)
     seed_everything(args.seed + (0 if args.kernels else 0))

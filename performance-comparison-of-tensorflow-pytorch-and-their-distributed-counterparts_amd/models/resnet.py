@@ -138,11 +138,9 @@ class ResNet(nn.Module):
                 h = K.image_to_s2d(x.contiguous(), self.stem.conv.pad, scale, None, None, False)
             else:
                 h = K.nchw_to_nhwc(x.contiguous(), STEM_CIN_PAD, scale, None, None)
-        else:  # fp32 parity path (CPU): no bf16 rounding of the input
-            h = x.float().permute(0, 2, 3, 1)
-            h = torch.nn.functional.pad(h, (0, STEM_CIN_PAD - h.shape[-1])).contiguous()
-            if x.dtype == torch.uint8:
-                h = h / 255.0
+        else:  # fp32 (the reference precision; CPU and --dtype fp32 on the GPU): no bf16 rounding
+            scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+            h = K.nchw_to_nhwc_f32(x.contiguous(), STEM_CIN_PAD, scale)
         return h if h.dtype == dt else h.to(dt)
 
     # ---- forward ----------------------------------------------------------------------------

@@ -51,9 +51,9 @@ class VGG(nn.Module):
         if dt == torch.bfloat16:
             scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
             h = K.nchw_to_nhwc(x.contiguous(), STEM_CIN_PAD, scale, None, None)
-        else:
-            h = x.float().permute(0, 2, 3, 1)
-            h = torch.nn.functional.pad(h, (0, STEM_CIN_PAD - h.shape[-1])).contiguous()
+        else:   # fp32: the reference precision
+            scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
+            h = K.nchw_to_nhwc_f32(x.contiguous(), STEM_CIN_PAD, scale)
         return h.to(dt)
 
     def features_flat(self, x):

@@ -76,18 +76,20 @@ def backend() -> str:
 
 
 def set_precision(name: str) -> None:
-    """``--dtype``: 'bf16' (default; the HIP kernels, bf16 storage with fp32 accumulation) or
-    'fp32' (the reference's precision).  The HIP kernels are bf16-only, so
-    fp32 is an explicit parity mode: it also selects the PyTorch reference backend, whose ops run
-    in fp32 on the GPU (MIOpen / hipBLASLt underneath).  It exists to compare numerics and
-    accuracy with the reference, not for speed."""
+    """``--dtype``: 'bf16' (default; bf16 storage with fp32 accumulation) or 'fp32' (the
+    reference's precision, SURVEY §0.1 / §5.6: another_neural_net.py:95-115 and nb :655-702 run
+    fp32 everywhere).  Both stay on the HIP kernels: fp32 activations select the fp32 kernels of
+    ``csrc/f32.hip`` (convolutions / Linear on v_mfma_f32_16x16x4_f32, BatchNorm, pooling, dropout,
+    losses).  The text encoders' bf16-only kernels (LayerNorm, GELU, tanh, attention, embedding,
+    LSTM) have no fp32 twin; in fp32 mode those ops run the PyTorch reference (``kernels.FP32_REF_OPS``,
+    listed in the JSON record of the text entry point)."""
     global _compute_dtype
     assert name in ("bf16", "fp32"), name
-    if name == "fp32":
-        _compute_dtype = torch.float32
-        set_backend("torch")
-    else:
-        _compute_dtype = None
+    _compute_dtype = torch.float32 if name == "fp32" else None
+
+
+def precision() -> str:
+    return "fp32" if _compute_dtype == torch.float32 else "bf16"
 
 
 def default_compute_dtype(device: torch.device) -> torch.dtype:

@@ -20,7 +20,7 @@ OP_NAMES = (
     "bn_partials", "bn_finalize", "bn_eval_coeff", "bn_apply", "bn_bwd_reduce", "bn_bwd_finalize",
     "bn_bwd_apply",
     "maxpool_fwd", "maxpool_bwd", "maxpool_bwd_bnr", "gap_fwd", "gap_bwd", "softmax_xent", "loss_mean", "xent_grad_scale", "log_softmax_bwd", "dropout", "relu_bwd", "colsum",
-    "nchw_to_nhwc", "image_to_s2d",
+    "nchw_to_nhwc", "nchw_to_nhwc_f32", "image_to_s2d", "resize_image",
     "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16", "wt_transpose_multi",
     "embedding_fwd", "embedding_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
     "masked_mean_fwd", "masked_mean_bwd",
@@ -28,6 +28,16 @@ OP_NAMES = (
     "attention_fwd", "attention_bwd", "tanh_fwd", "tanh_bwd", "add_bf16",
     "topk_rows", "synth_images",
 )
+
+
+# Ops whose HIP kernels are bf16-only (the text encoders').  In the fp32 precision mode
+# (``--dtype fp32``) they run the PyTorch reference implementation -- an explicit, documented list,
+# not a silent fallback; every other op has an fp32 HIP kernel (csrc/f32.hip).
+FP32_REF_OPS = frozenset({
+    "layernorm_fwd", "layernorm_bwd", "gelu_fwd", "gelu_bwd", "tanh_fwd", "tanh_bwd",
+    "attention_fwd", "attention_bwd", "add_bf16", "embedding_fwd", "embedding_bwd",
+    "lstm_seq_fwd", "lstm_seq_bwd", "masked_mean_fwd", "masked_mean_bwd",
+})
 
 
 def _first_tensor(args):
@@ -45,7 +55,7 @@ class _Dispatch:
             t = _first_tensor(args)
             if TRACE is not None:
                 TRACE.append((name, [tuple(a.shape) if isinstance(a, torch.Tensor) else a for a in args]))
-            if _lib.use_native(t):
+            if _lib.use_native(t) and not (name in FP32_REF_OPS and _lib.precision() == "fp32"):
                 return getattr(torch.ops.pcmp, name)(*args)
             if refimpl is None:
                 raise NotImplementedError(f"no reference implementation for {name}")

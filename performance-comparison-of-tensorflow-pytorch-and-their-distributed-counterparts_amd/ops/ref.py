@@ -220,6 +220,31 @@ def gap_bwd(dy, H, W):
     return (dy.float() / (H * W)).view(N, 1, 1, C).expand(N, H, W, C).to(dy.dtype).contiguous()
 
 
+def nchw_to_nhwc_f32(x, cpad, scale):
+    h = x.float().permute(0, 2, 3, 1) * scale
+    return F.pad(h, (0, cpad - h.shape[-1])).contiguous()
+
+
+def resize_image(x, Ho, Wo, mode, cpad, scale, mean=None, stdv=None):
+    """PIL bilinear resize of uint8 [N,H,W,C] images (the device kernel's reference)."""
+    import numpy as np
+    from PIL import Image
+    outs = []
+    for im in x.cpu().numpy():
+        pim = Image.fromarray(im[..., 0] if im.shape[-1] == 1 else im)
+        r = np.asarray(pim.resize((int(Wo), int(Ho)), Image.BILINEAR), dtype=np.uint8)
+        outs.append(torch.from_numpy(r.reshape(int(Ho), int(Wo), -1).copy()))
+    u = torch.stack(outs).to(x.device)                       # [N, Ho, Wo, C]
+    if mode == 0:
+        return u.permute(0, 3, 1, 2).contiguous()
+    v = u.float() * scale
+    if mean is not None:
+        C = v.shape[-1]
+        v = (v - mean[:C].float().to(v.device)) / stdv[:C].float().to(v.device)
+    v = F.pad(v, (0, cpad - v.shape[-1]))
+    return v.to(torch.bfloat16 if mode == 1 else torch.float32).contiguous()
+
+
 # ------------------------------------------------------------------------------ loss
 def softmax_xent(logits, labels, want_logp, want_grad, grad_scale, ignore_index):
     z = logits.float()

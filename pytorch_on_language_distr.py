@@ -23,7 +23,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import torch  # noqa: E402
 
 import pcmp  # noqa: E402,F401
-from pcmp.engine import cli  # noqa: E402
+from pcmp.engine import cli
+from pcmp.ops.kernels import FP32_REF_OPS  # noqa: E402
 
 
 def main(argv=None):
@@ -92,7 +93,9 @@ def main(argv=None):
     cli.write_json(args, {"script": "pytorch_on_language_distr", "model": args.model, "world_size": env.world_size,
                           "epoch_seconds": times, "train_loss": state.history["train_loss"], "test_accuracy": acc,
                           "samples_per_sec": len(train_ds) * args.epochs / max(1e-9, sum(times)),
-                          "total_seconds": time.time() - t0, "data": "real" if args.csv else "synthetic"})
+                          "total_seconds": time.time() - t0, "data": "real" if args.csv else "synthetic",
+                          "dtype": args.dtype,
+                          "fp32_reference_ops": sorted(FP32_REF_OPS) if args.dtype == "fp32" else []})
     if model.__class__.__name__ == "BiLSTMClassifier":
         from pcmp.ops.rnn import check_errors
         check_errors()

@@ -209,11 +209,15 @@ def test_mlp_cpu_reports_held_out_metrics():
     assert out.count("Epoch ") == 2
 
 
-def test_dtype_fp32_parity_mode_selects_reference_backend():
+def test_dtype_fp32_stays_on_hip_backend():
+    """--dtype fp32 (the reference's precision) keeps the HIP backend (fp32 kernels of csrc/f32.hip);
+    only the listed bf16-only text ops run the reference in that mode."""
     from pcmp.ops import _lib
+    from pcmp.ops.kernels import FP32_REF_OPS
+    assert "conv_fwd" not in FP32_REF_OPS and "layernorm_fwd" in FP32_REF_OPS
     try:
         _lib.set_precision("fp32")
-        assert _lib.backend() == "torch"
+        assert _lib.backend() == "hip" and _lib.precision() == "fp32"
         assert _lib.default_compute_dtype(torch.device("cuda", 0)) == torch.float32
         from pcmp.models.resnet import resnet18
         m = resnet18(num_classes=10)

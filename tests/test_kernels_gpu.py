@@ -799,3 +799,109 @@ def test_halo_conv_dgrad_matches_igemm(gpu, bnr):
         close(got[0], outr[0])
     else:
         close(got[0], ref.conv_dgrad(dy, w, H, H, 1, 1, None))
+
+
+@pytest.mark.parametrize("mode", ["fwd_stats", "dgrad_bnr", "plain_gemm"])
+def test_dma8_staggered_schedule_bitwise(gpu, mode):
+    """The 8-wave LDS-DMA kernel's wave-row-staggered READ / MFMA schedule (knob dma8_stag) gives the
+    lock-step schedule's outputs bitwise (same MFMA order per accumulator) and matches the fp32
+    reference, on shapes that select the 256x256 kernel (>= 160 tiles, >= 8 K-tiles)."""
+    torch.manual_seed(11)
+    ops = _ops()
+    N, H, C, K, R = 210, 14, 256, 256, 3          # 41,160 rows x 256: 161 tiles, 36 K-tiles
+    x = rnd(N, H, H, C, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+    dy = rnd(N, H, H, K, dev=gpu)
+    xb = rnd(N, H, H, C, dev=gpu)
+    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    msc, msh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
+    A = (torch.rand(40960, 2048, device=gpu) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(256, 2048, device=gpu) * 2 - 1).to(torch.bfloat16)
+
+    def run():
+        if mode == "fwd_stats":
+            return [t.clone() for t in ops.conv_fwd(x, w, 1, 1, None, None, False, True)]
+        if mode == "dgrad_bnr":
+            return [t.clone() for t in ops.conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, xb, mean, istd,
+                                                          None, None, None, msc, msh)]
+        return [ops.conv_fwd(A.view(40960, 1, 1, 2048), B.view(256, 1, 1, 2048), 1, 0, None, None, False,
+                             False)[0].clone()]
+    outs = []
+    if mode == "plain_gemm":
+        ops.set_knob("plan_force", 2)             # the 8-wave 256x256 DMA kernel
+    old = {k.split("=")[0]: int(k.split("=")[1]) for k in ops.list_knobs()}
+    try:
+        # lock-step, staggered, early-prefetch (8-wave and 4-wave kernels)
+        for stag, pf2 in ((0, 0), (1, 0), (0, 3)):
+            ops.set_knob("dma8_stag", stag)
+            ops.set_knob("dma_pf2", pf2)
+            outs.append(run())
+    finally:
+        ops.set_knob("dma8_stag", old["dma8_stag"])
+        ops.set_knob("dma_pf2", old["dma_pf2"])
+        ops.set_knob("plan_force", -1)
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        for pa, pb in zip(outs[0][1:], o[1:]):
+            assert torch.equal(pa, pb)
+    if mode == "fwd_stats":
+        yr = ref.conv_fwd(x, w, 1, 1, None, None, False, True)[0]
+        close(outs[1][0], yr)
+        close_el(outs[1][0], yr)
+    elif mode == "dgrad_bnr":
+        gr = ref.conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, xb, mean, istd, None, None, None, msc, msh)[0]
+        close(outs[1][0], gr)
+    else:
+        refm = (A.float() @ B.float().t())
+        close(outs[1][0].view(40960, 256), refm, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("shape", [(16, 28, 28, 128, 128, 3), (8, 28, 28, 512, 128, 1), (8, 56, 56, 64, 64, 3)])
+def test_dma4_early_prefetch_bitwise(gpu, shape):
+    """Early-prefetch schedule (knob dma_pf2 bit 0) of the 4-wave LDS-DMA kernels (128x128, 128x64):
+    FWD+stats and DGRAD+BN-reduce outputs bitwise equal to the lock-step schedule."""
+    torch.manual_seed(12)
+    ops = _ops()
+    N, H, W, C, K, R = shape
+    x = rnd(N, H, W, C, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+    dy = rnd(N, H, W, K, dev=gpu)
+    xb = rnd(N, H, W, C, dev=gpu)
+    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    msc, msh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
+    outs = []
+    old = ops.set_knob("dma_pf2", 0)
+    try:
+        for v in (0, 1):
+            ops.set_knob("dma_pf2", v)
+            f = [t.clone() for t in ops.conv_fwd(x, w, 1, R // 2, None, None, False, True)]
+            d = [t.clone() for t in ops.conv_dgrad_bnr(dy, w, H, W, 1, R // 2, None, None, xb, mean, istd,
+                                                       None, None, None, msc, msh)]
+            outs.append(f + d)
+    finally:
+        ops.set_knob("dma_pf2", old)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    close(outs[1][0], ref.conv_fwd(x, w, 1, R // 2, None, None, False, True)[0])
+
+
+@pytest.mark.parametrize("hw,out", [((375, 500), (224, 224)), ((224, 224), (224, 224)), ((100, 77), (224, 224)),
+                                    ((1000, 333), (224, 160)), ((31, 900), (256, 256))])
+def test_resize_image_matches_pil_bit_exact(gpu, hw, out):
+    """Device bilinear resize (the reference's per-image Resize((224,224)) + ToTensor)
+    is bit-identical to PIL.Image.resize(BILINEAR) for downscales, upscales and the identity; the
+    fused NHWC bf16 / fp32 model-input forms equal the same values scaled and normalised."""
+    g = torch.Generator().manual_seed(hw[0] * 7 + hw[1])
+    x = torch.randint(0, 256, (2, hw[0], hw[1], 3), dtype=torch.uint8, generator=g)
+    xd = x.to(gpu)
+    y = _ops().resize_image(xd, out[0], out[1], 0, 0, 1.0, None, None)
+    yr = ref.resize_image(x, out[0], out[1], 0, 0, 1.0)
+    assert y.shape == (2, 3, out[0], out[1])
+    assert torch.equal(y.cpu(), yr.cpu()), (y.int() - yr.to(gpu).int()).abs().max().item()
+    mean = torch.tensor([0.485, 0.456, 0.406], device=gpu)
+    std = torch.tensor([0.229, 0.224, 0.225], device=gpu)
+    for mode, dt in ((1, torch.bfloat16), (2, torch.float32)):
+        z = _ops().resize_image(xd, out[0], out[1], mode, 8, 1 / 255.0, mean, std)
+        zr = ref.resize_image(x, out[0], out[1], mode, 8, 1 / 255.0, mean, std)
+        assert z.dtype == dt and z.shape == (2, out[0], out[1], 8)
+        close(z, zr, 1e-6, 1e-6)
