@@ -87,6 +87,18 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
   return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
 }
 
+// Dropout seed with an optional device-side salt: a captured hipGraph replays its kernels with the
+// arguments of the capture, so a training step replayed from a graph reads a per-replay counter
+// (incremented by the step itself) to draw a new mask every step; eager launches pass no salt.
+__device__ __forceinline__ uint64_t dropout_seed(uint64_t seed, const int64_t* salt) {
+  return salt ? seed + (uint64_t)salt[0] * 0x9E3779B97F4A7C15ull : seed;
+}
+inline const int64_t* salt_ptr(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->numel() >= 1, "dropout salt: int64 GPU tensor");
+  return t->data_ptr<int64_t>();
+}
+
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }

@@ -436,8 +436,9 @@ __global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const T* __restric
 // ---------------------------------------------------------------- dropout ----------------------
 // y = x * keep / (1-p), keep = uniform(seed, offset+i) >= p ; same call in backward on dy.
 __global__ void dropout_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y, int64_t n, float p,
-                               uint64_t seed, uint64_t offset) {
+                               uint64_t seed0, uint64_t offset, const int64_t* __restrict__ salt) {
   const float scale = 1.f / (1.f - p);
+  const uint64_t seed = dropout_seed(seed0, salt);
   const int64_t nv = n / 8;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -920,13 +921,13 @@ at::Tensor log_softmax_bwd(const at::Tensor& g, const at::Tensor& logp) {
   return dz;
 }
 
-at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
-  if (x.scalar_type() == at::kFloat) return f32::dropout(x, p, seed, offset);
+at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt) {
+  if (x.scalar_type() == at::kFloat) return f32::dropout(x, p, seed, offset, salt);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   TORCH_CHECK(x.numel() % 8 == 0, "dropout: numel % 8");
   auto y = at::empty_like(x);
   hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(x.numel() / 8)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
-                     ptr<__bf16>(y), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset);
+                     ptr<__bf16>(y), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset, salt_ptr(salt));
   PCMP_LAUNCH_CHECK();
   return y;
 }
@@ -1259,7 +1260,7 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("loss_mean(Tensor loss_rows, Tensor labels, int V, int ignore_index) -> Tensor", &pcmp::loss_mean);
   m.def("xent_grad_scale(Tensor dl, Tensor gout, Tensor valid) -> Tensor", &pcmp::xent_grad_scale);
   m.def("log_softmax_bwd(Tensor g, Tensor logp) -> Tensor", &pcmp::log_softmax_bwd);
-  m.def("dropout(Tensor x, float p, int seed, int offset) -> Tensor", &pcmp::dropout);
+  m.def("dropout(Tensor x, float p, int seed, int offset, Tensor? salt=None) -> Tensor", &pcmp::dropout);
   m.def("relu_bwd(Tensor dy, Tensor y) -> Tensor", &pcmp::relu_bwd);
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()", &pcmp::colsum);
   m.def("nchw_to_nhwc(Tensor x, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor", &pcmp::nchw_to_nhwc);

@@ -47,7 +47,7 @@ std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& 
                                         const at::Tensor& shift, int64_t k, int64_t s, int64_t pad);
 at::Tensor gap_fwd(const at::Tensor& x);
 at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W);
-at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset);
+at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt);
 at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y);
 void colsum(const at::Tensor& x, at::Tensor out, bool accumulate);
 

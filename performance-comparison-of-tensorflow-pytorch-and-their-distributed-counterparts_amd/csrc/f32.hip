@@ -816,18 +816,20 @@ at::Tensor gap_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
 
 // dropout with the bf16 kernel's counter RNG (same keep mask for the same seed / offset / index)
 __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
-                                                      float p, uint64_t seed, uint64_t offset) {
+                                                      float p, uint64_t seed0, uint64_t offset,
+                                                      const int64_t* __restrict__ salt) {
   const float scale = 1.f / (1.f - p);
+  const uint64_t seed = dropout_seed(seed0, salt);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     y[i] = uniform01(seed, offset + i) >= p ? x[i] * scale : 0.f;
 }
 
-at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset) {
+at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt) {
   check_f32(x, "dropout(fp32)");
   auto y = at::empty_like(x);
   if (x.numel())
     hipLaunchKernelGGL(dropout_kernel, dim3(grid_n(x.numel())), dim3(256), 0, cur_stream(), ptr<float>(x),
-                       ptr<float>(y), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset);
+                       ptr<float>(y), x.numel(), (float)p, (uint64_t)seed, (uint64_t)offset, salt_ptr(salt));
   PCMP_LAUNCH_CHECK();
   return y;
 }

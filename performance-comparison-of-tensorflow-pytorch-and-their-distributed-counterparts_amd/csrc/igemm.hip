@@ -97,6 +97,10 @@ struct IgemmParams {
   int* grp_cnt;
   double* grp_red;
   double* grp_red2;
+  // coalesced epilogue (4-wave kernels, BM = 128, no split-K, no in-kernel group reduction): the
+  // fp32 accumulator tile is re-laid out through LDS so every epilogue load / store moves whole
+  // cache lines (igemm_epilogue_coal); set by the host when the launch's LDS allocation covers it
+  int coal;
 };
 
 constexpr int BK = 64;
@@ -200,6 +204,202 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+
+// Coalesced epilogue for the 4-wave FWD / DGRAD kernels (BM = 128, BN = 64 / 128, 256 threads).
+// The MFMA accumulator layout gives each lane 8 channels of one pixel row, so the fragment-shaped
+// epilogue moves 16 rows x 64 B per wave instruction: every 128-B line of the residual, the BN
+// input(s), the ReLU mask and the output is requested twice, and the texture path, not HBM, sets
+// the rate (cdna_hip_programming.md §5, "fragment-shaped x costs +18-45 %, TA_BUSY 2x").  Here the
+// fp32 tile is staged in LDS (the stage buffers are dead) and re-read row-major: thread t keeps the
+// 8-channel chunk (t % (BN/8)) and walks rows t / (BN/8), + NTHR/(BN/8), ...; a wave instruction then
+// covers 4 (BN = 128) or 8 (BN = 64) rows x BN channels of whole lines.  Per-element math is that of
+// igemm_epilogue_fd (fp32 sum, one bf16 rounding, mask on the rounded value), so outputs are bitwise
+// equal; the BN partial sums are reduced in another (fixed) order.
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int NTHR, int EPD>
+__device__ __forceinline__ void igemm_epilogue_coal(const IgemmParams& p, f32x4 (&acc)[BN / WN / 16][BM / WM / 16],
+                                                    char* smem, int tid, int m0, int n0, int tile_m) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr bool PAIR = (TN % 2 == 0);
+  constexpr int LDT = BN + 4;              // fp32 row stride of the staged tile
+  constexpr int CPR = BN / 8;              // 8-channel chunks per row
+  constexpr int RSTEP = NTHR / CPR;        // rows between a thread's chunks
+  constexpr int NCH = BM / RSTEP;          // chunks per thread
+  static_assert(NTHR % CPR == 0 && BM % RSTEP == 0, "coalesced epilogue geometry");
+  constexpr bool stats = EPI == EPI_STATS;
+  constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
+  constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
+  constexpr int NS = bnr2 ? 3 : 2;
+  constexpr int D = EPD < NCH ? EPD : NCH;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  float* T = reinterpret_cast<float*>(smem);
+  float* ctab = T + BM * LDT;
+  auto chan = [&](int j) {
+    return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
+  };
+  lds_sync();   // every wave is past its last operand read of the stage buffers
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      *reinterpret_cast<f32x4*>(T + (wr * WTM + i * 16 + fr) * LDT + chan(j)) = acc[j][i];
+  const bool has_bias = MODE == MODE_FWD && p.bias != nullptr;
+  const bool has_res = p.resid != nullptr;
+  const bool has_mb = bnr && p.bn_mbits != nullptr;
+  const bool has_mk = bnr && !has_mb && p.bn_mask != nullptr;
+  const bool mfx = bnr && !has_mb && !has_mk && p.bn_msc != nullptr;
+  for (int idx = tid; idx < BN; idx += NTHR) {
+    const int c = min(n0 + idx, p.gn - 1);
+    ctab[idx] = has_bias ? p.bias[c] : 0.f;
+    if constexpr (bnr) {
+      const float is = p.bn_istd[c];
+      ctab[1 * BN + idx] = is;
+      ctab[2 * BN + idx] = -p.bn_mean[c] * is;
+      ctab[3 * BN + idx] = mfx ? p.bn_msc[c] : 0.f;
+      ctab[4 * BN + idx] = mfx ? p.bn_msh[c] : 0.f;
+      if constexpr (bnr2) {
+        const float is2 = p.bn_istd2[c];
+        ctab[5 * BN + idx] = is2;
+        ctab[6 * BN + idx] = -p.bn_mean2[c] * is2;
+      }
+    }
+  }
+  __syncthreads();
+  const int c8 = (tid % CPR) * 8, rbase = tid / CPR;
+  const int n = n0 + c8;
+  const bool nok = n < p.gn;   // gn % 8 == 0: a chunk is wholly in or out
+  float bias[8], ka[8], kb[8], msc[8], msh[8], ka2[8], kb2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    bias[e] = ctab[c8 + e];
+    if constexpr (bnr) {
+      ka[e] = ctab[1 * BN + c8 + e]; kb[e] = ctab[2 * BN + c8 + e];
+      msc[e] = ctab[3 * BN + c8 + e]; msh[e] = ctab[4 * BN + c8 + e];
+      if constexpr (bnr2) { ka2[e] = ctab[5 * BN + c8 + e]; kb2[e] = ctab[6 * BN + c8 + e]; }
+    }
+  }
+  float sm[NS][8];
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm[k][e] = 0.f;
+  auto out_off = [&](int row, bool& ok) -> size_t {
+    const int m = m0 + row;
+    ok = nok && m < p.gm;
+    size_t orow = ok ? m : 0;
+    if constexpr (MODE == MODE_DGRAD) {
+      if (p.sub && ok) {
+        const int nn = fdiv(m, p.fd_HW);
+        const int rem = m - nn * p.dH * p.dW;
+        const int hh = fdiv(rem, p.fd_W);
+        const int ww = rem - hh * p.dW;
+        orow = ((size_t)nn * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
+      }
+    }
+    return orow * p.gn + (ok ? n : 0);
+  };
+  uint4 rv[D], xv[D], xv2[D], mk[D];
+  unsigned mb[D];
+  auto issue = [&](int k, int b) {
+    bool ok;
+    const size_t o = out_off(rbase + k * RSTEP, ok);
+    const uint4 z = uint4{0, 0, 0, 0};
+    if (has_res) rv[b] = ok ? *reinterpret_cast<const uint4*>(p.resid + o) : z;
+    if constexpr (bnr) {
+      if (has_mb) mb[b] = ok ? (unsigned)p.bn_mbits[o >> 3] : 0u;
+      if (has_mk) mk[b] = ok ? *reinterpret_cast<const uint4*>(p.bn_mask + o) : z;
+      xv[b] = ok ? *reinterpret_cast<const uint4*>(p.bn_x + o) : z;
+      if constexpr (bnr2) xv2[b] = ok ? *reinterpret_cast<const uint4*>(p.bn_x2 + o) : z;
+    }
+  };
+  __bf16* out = reinterpret_cast<__bf16*>(p.out);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d) issue(d, d);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int b = k % D;
+    if (k + D - 1 < NCH) issue(k + D - 1, (k + D - 1) % D);
+    const int row = rbase + k * RSTEP;
+    bool ok;
+    const size_t o = out_off(row, ok);
+    if (!ok) continue;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(T + row * LDT + c8);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(T + row * LDT + c8 + 4);
+    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const unsigned rw[4] = {rv[b].x, rv[b].y, rv[b].z, rv[b].w};
+    const unsigned xw[4] = {xv[b].x, xv[b].y, xv[b].z, xv[b].w};
+    const unsigned xw2[4] = {xv2[b].x, xv2[b].y, xv2[b].z, xv2[b].w};
+    const unsigned mw[4] = {mk[b].x, mk[b].y, mk[b].z, mk[b].w};
+    unsigned ov[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ce = 2 * q;
+      float x0 = av[ce] + bias[ce], x1 = av[ce + 1] + bias[ce + 1];
+      if (has_res) {
+        x0 += __uint_as_float(rw[q] << 16);
+        x1 += __uint_as_float(rw[q] & 0xffff0000u);
+      }
+      if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+      unsigned u = f2bf2(x0, x1);
+      if constexpr (bnr) {
+        const float xa = __uint_as_float(xw[q] << 16), xb = __uint_as_float(xw[q] & 0xffff0000u);
+        if (has_mb) {
+          const unsigned bits = mb[b] >> ce;
+          u &= ((bits & 1u) ? 0x0000ffffu : 0u) | ((bits & 2u) ? 0xffff0000u : 0u);
+        } else if (has_mk) {
+          const unsigned y = mw[q];
+          u &= (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
+               (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
+        } else if (mfx) {
+          const float z0 = fmaf(xa, msc[ce], msh[ce]);
+          const float z1 = fmaf(xb, msc[ce + 1], msh[ce + 1]);
+          u &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
+        }
+        const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+        sm[0][ce] += r0; sm[0][ce + 1] += r1;
+        sm[1][ce] += r0 * fmaf(xa, ka[ce], kb[ce]);
+        sm[1][ce + 1] += r1 * fmaf(xb, ka[ce + 1], kb[ce + 1]);
+        if constexpr (bnr2) {
+          sm[2][ce] += r0 * fmaf(__uint_as_float(xw2[q] << 16), ka2[ce], kb2[ce]);
+          sm[2][ce + 1] += r1 * fmaf(__uint_as_float(xw2[q] & 0xffff0000u), ka2[ce + 1], kb2[ce + 1]);
+        }
+      } else if constexpr (stats) {
+        const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
+        sm[0][ce] += r0; sm[0][ce + 1] += r1;
+        sm[1][ce] += r0 * r0; sm[1][ce + 1] += r1 * r1;
+      }
+      ov[q] = u;
+    }
+    *reinterpret_cast<uint4*>(out + o) = uint4{ov[0], ov[1], ov[2], ov[3]};
+  }
+  if constexpr (stats || bnr) {
+    // column sums: the RSTEP threads of a chunk column combine through LDS (T is dead now), then one
+    // thread per channel sums the RSTEP rows in order
+    float* red = T;   // [RSTEP][NS][BN]
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      *reinterpret_cast<f32x4*>(red + (rbase * NS + k) * BN + c8) = f32x4{sm[k][0], sm[k][1], sm[k][2], sm[k][3]};
+      *reinterpret_cast<f32x4*>(red + (rbase * NS + k) * BN + c8 + 4) = f32x4{sm[k][4], sm[k][5], sm[k][6], sm[k][7]};
+    }
+    __syncthreads();
+    float* st = p.stats + (size_t)tile_m * 2 * p.gn;
+    float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
+    for (int i = tid; i < NS * BN; i += NTHR) {
+      const int k = i / BN, ci = i - k * BN, c = n0 + ci;
+      if (c >= p.gn) continue;
+      float t = 0.f;
+#pragma unroll 4
+      for (int r = 0; r < RSTEP; ++r) t += red[(r * NS + k) * BN + ci];
+      if (k == 0) { st[c] = t; if (bnr2) st2[c] = t; }
+      else if (k == 1) st[p.gn + c] = t;
+      else st2[p.gn + c] = t;
+    }
+  }
+}
+
 // SHRED: column sums reduced across the 16 pixel lanes with DPP instead of an LDS transpose, so
 // the epilogue's LDS scratch is only [6][BN] coefficient rows + [WM][NS][BN] partials (smem must
 // then point at a region that no stage buffer uses: the persistent streaming kernel keeps
@@ -218,6 +418,12 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     auto chan = [&](int j) {   // channel offset inside the BN tile of acc[j][*][0]
       return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
     };
+    if constexpr (NTHR == NT && BM == 128 && (BN == 128 || BN == 64) && !SHRED && MODE != MODE_WGRAD) {
+      if (p.coal && p.nsplit == 1 && p.grp == 0) {
+        igemm_epilogue_coal<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m);
+        return;
+      }
+    }
     if (p.nsplit > 1) {
       // split-K forward (small-M inference shapes): raw fp32 partials, epilogue in the reduction
       float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
@@ -1905,6 +2111,20 @@ __global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src
 
 // ------------------------------------------------------------------------------------------------
 // host side
+// coalesced epilogue (igemm_epilogue_coal) for the 4-wave BM = 128 FWD / DGRAD kernels: A/B knob
+static Knob kn_epi_coal("epi_coal", 1);
+template <int MODE, int BM, int BN, int NTHR>
+static size_t coal_setup(IgemmParams& p, size_t smem) {
+  p.coal = 0;
+  if constexpr (MODE != MODE_WGRAD && NTHR == NT && BM == 128 && (BN == 128 || BN == 64)) {
+    if (kn_epi_coal.get() && p.nsplit == 1 && p.grp == 0 && p.gn % 8 == 0) {
+      p.coal = 1;
+      smem = std::max(smem, (size_t)(BM * (BN + 4) + 7 * BN) * sizeof(float));
+    }
+  }
+  return smem;
+}
+
 template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
@@ -1919,13 +2139,23 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
     const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
     smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
   }
+  smem = coal_setup<MODE, BM, BN, NT>(p, smem);
   const int cin = MODE == MODE_FWD ? p.C : p.K;
   const bool unif = MODE != MODE_WGRAD && cin % BK == 0 && p.ksplit % BK == 0;
   int epi = EPI_PLAIN;
   if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
-#define PCMP_IGEMM_LAUNCH(U, E) \
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, U, E>), dim3(grid), dim3(NT), smem, st, p)
+#define PCMP_IGEMM_LAUNCH(U, E)                                                                       \
+  do {                                                                                              \
+    auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, U, E>;                                            \
+    static bool attr_ = false;                                                                      \
+    if (!attr_) {                                                                                   \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf_),                        \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
+      attr_ = true;                                                                                 \
+    }                                                                                               \
+    hipLaunchKernelGGL(kf_, dim3(grid), dim3(NT), smem, st, p);                                     \
+  } while (0)
   if constexpr (MODE == MODE_FWD) {
     if (epi == EPI_STATS) {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_STATS); else PCMP_IGEMM_LAUNCH(false, EPI_STATS);
@@ -1934,8 +2164,17 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
     }
   } else if constexpr (MODE == MODE_DGRAD) {
     const bool deep = kn_epi_depth.get() >= 4;
-#define PCMP_IGEMM_LAUNCH_D(U, E) \
-  hipLaunchKernelGGL((igemm_kernel<MODE, BM, BN, WM, WN, U, E, 4>), dim3(grid), dim3(NT), smem, st, p)
+#define PCMP_IGEMM_LAUNCH_D(U, E)                                                                     \
+  do {                                                                                              \
+    auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, U, E, 4>;                                         \
+    static bool attr_ = false;                                                                      \
+    if (!attr_) {                                                                                   \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf_),                        \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
+      attr_ = true;                                                                                 \
+    }                                                                                               \
+    hipLaunchKernelGGL(kf_, dim3(grid), dim3(NT), smem, st, p);                                     \
+  } while (0)
     if (epi == EPI_BNR) {
       if (deep) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR); }
       else if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR); else PCMP_IGEMM_LAUNCH(false, EPI_BNR);
@@ -2009,8 +2248,9 @@ static int igemm8_min_tiles() {
 
 // 8-wave LDS-DMA kernel with the wave-row-staggered READ / MFMA schedule (STAG): A/B knob
 static Knob kn_dma8_stag("dma8_stag", 0);   // measured null (profiles/r3_stagger_ab.txt)
-// early-prefetch schedule (SCHED 2): bit 0 the 4-wave kernels, bit 1 the 8-wave kernel
-static Knob kn_dma_pf2("dma_pf2", 0);
+// early-prefetch schedule (SCHED 2): bit 0 the 4-wave kernels, bit 1 the 8-wave kernel.  Whole-step
+// A/B (profiles/r3_prio_pf2_ab.txt, 3 interleaved rounds): 12,213-12,283 -> 12,346-12,360 img/s
+static Knob kn_dma_pf2("dma_pf2", 3);
 
 template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB>
 static void launch_dma(IgemmParams& p, hipStream_t st) {
@@ -2027,6 +2267,7 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
     const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
     smem = std::max(smem, (size_t)((NTHR / 64) * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
   }
+  smem = coal_setup<MODE, BM, BN, NTHR>(p, smem);
   int epi = EPI_PLAIN;
   if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
@@ -2647,7 +2888,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.bn_mbits = nullptr;
   p.stats_cap = 0;
   p.grp = 0; p.grp_cnt = nullptr; p.grp_red = nullptr; p.grp_red2 = nullptr;
-  p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
+  p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1; p.coal = 0;
 }
 
 // x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual

@@ -216,6 +216,7 @@ struct AttnParams {
   int B, S, H, D;
   float scale, p_drop;
   uint64_t seed, offset;
+  const int64_t* salt;   // optional per-replay RNG salt (hipGraph-captured steps), see dropout_seed()
 };
 
 // bf16 fragment (8 consecutive k) from an LDS row-major tile: X[row][k0..k0+7]
@@ -240,7 +241,7 @@ __device__ __forceinline__ bf16x8 frag_tr(const __bf16* X, int ld, int k0, int m
 __device__ __forceinline__ float drop_scale(const AttnParams& p, int bh, int q, int k) {
   if (p.p_drop <= 0.f) return 1.f;
   const uint64_t idx = ((uint64_t)bh * p.S + q) * p.S + k;
-  return uniform01(p.seed, p.offset + idx) >= p.p_drop ? 1.f / (1.f - p.p_drop) : 0.f;
+  return uniform01(dropout_seed(p.seed, p.salt), p.offset + idx) >= p.p_drop ? 1.f / (1.f - p.p_drop) : 0.f;
 }
 
 // stage rows [S][64] of a qkv section into LDS (row-major, padded) and optionally transposed
@@ -628,7 +629,8 @@ static size_t attn_bwd_smem() { return ((size_t)4 * AS * ADP + AS * ASP) * 2 + 3
 
 // qkv [B*S][3D] bf16 -> [ctx [B*S][D] bf16, lse [B*H][S] f32]
 std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& ids, int64_t B,
-                                      int64_t S, int64_t H, double p_drop, int64_t seed, int64_t offset) {
+                                      int64_t S, int64_t H, double p_drop, int64_t seed, int64_t offset,
+                                      const c10::optional<at::Tensor>& salt) {
   PCMP_CHECK_BF16(qkv); PCMP_CHECK_CONTIG(qkv);
   const int D3 = qkv.size(-1), D = D3 / 3;
   TORCH_CHECK(D == H * AD, "attention: head dim must be 64");
@@ -640,7 +642,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional
   if (ids.has_value() && ids->defined()) idc = ids->contiguous();
   AttnParams p{ptr<__bf16>(qkv), idc.defined() ? idc.data_ptr<int64_t>() : nullptr, ptr<__bf16>(ctx), ptr<float>(lse),
                nullptr, nullptr, nullptr, (int)B, (int)S, (int)H, D, 0.125f, (float)p_drop, (uint64_t)seed,
-               (uint64_t)offset};
+               (uint64_t)offset, salt_ptr(salt)};
   hipLaunchKernelGGL(attention_fwd_kernel, dim3(B * H), dim3(256), attn_fwd_smem(), cur_stream(), p);
   PCMP_LAUNCH_CHECK();
   return {ctx, lse};
@@ -648,7 +650,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional
 
 at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at::Tensor& ctx, const at::Tensor& lse,
                          const c10::optional<at::Tensor>& ids, int64_t B, int64_t S, int64_t H, double p_drop,
-                         int64_t seed, int64_t offset) {
+                         int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt) {
   PCMP_CHECK_BF16(qkv);
   auto dc = dctx.contiguous();
   const int D3 = qkv.size(-1), D = D3 / 3;
@@ -657,7 +659,7 @@ at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at
   if (ids.has_value() && ids->defined()) idc = ids->contiguous();
   AttnParams p{ptr<__bf16>(qkv), idc.defined() ? idc.data_ptr<int64_t>() : nullptr, nullptr, ptr<float>(lse),
                ptr<__bf16>(dc), ptr<__bf16>(ctx), ptr<__bf16>(dqkv), (int)B, (int)S, (int)H, D, 0.125f,
-               (float)p_drop, (uint64_t)seed, (uint64_t)offset};
+               (float)p_drop, (uint64_t)seed, (uint64_t)offset, salt_ptr(salt)};
   hipLaunchKernelGGL(attention_bwd_kernel, dim3(B * H), dim3(256), attn_bwd_smem(), cur_stream(), p);
   PCMP_LAUNCH_CHECK();
   return dqkv;
@@ -675,9 +677,10 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("tanh_fwd(Tensor x) -> Tensor", &pcmp::tanh_fwd);
   m.def("tanh_bwd(Tensor dy, Tensor y) -> Tensor", &pcmp::tanh_bwd);
   m.def("add_bf16(Tensor a, Tensor b) -> Tensor", &pcmp::add_bf16);
-  m.def("attention_fwd(Tensor qkv, Tensor? ids, int B, int S, int H, float p_drop, int seed, int offset) -> Tensor[]",
+  m.def("attention_fwd(Tensor qkv, Tensor? ids, int B, int S, int H, float p_drop, int seed, int offset, "
+        "Tensor? salt=None) -> Tensor[]",
         &pcmp::attention_fwd);
   m.def("attention_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor? ids, int B, int S, int H, float p_drop, "
-        "int seed, int offset) -> Tensor",
+        "int seed, int offset, Tensor? salt=None) -> Tensor",
         &pcmp::attention_bwd);
 }

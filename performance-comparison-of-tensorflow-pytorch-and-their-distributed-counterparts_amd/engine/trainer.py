@@ -35,7 +35,7 @@ from ..parallel.metrics import all_reduce_max, all_reduce_sum
 from ..utils import report as R
 from ..utils.checkpoint import BestCheckpoint
 from ..utils.flat import FlatParams
-from ..utils.misc import StepThrottle, roctx_range, watchdog_kick
+from ..utils.misc import PriorityStream, StepThrottle, roctx_range, watchdog_kick
 from ..utils.timer import PhaseTimer
 
 
@@ -50,6 +50,7 @@ class TrainState:
     history: dict = field(default_factory=lambda: {"train_loss": [], "test_loss": [], "test_acc": []})
     timer: PhaseTimer | None = None   # per-phase device time, PCMP_PHASE_TIMES=1
     throttle: StepThrottle | None = None   # host run-ahead bound (allocator footprint)
+    prio: PriorityStream | None = None     # high-priority compute stream for the step
 
     def phase(self, name):
         """Phase bracket: HIP-event device time + a roctx range for rocprofv3 (when timing)."""
@@ -108,7 +109,8 @@ def make_state(model, optimizer="sgd", lr=0.1, distributed=False, clip=None, sha
     ddp = DistributedDataParallel(model, flat) if distributed else None
     timer = PhaseTimer(warmup_steps=int(os.environ.get("PCMP_PHASE_WARMUP", "2"))) \
         if os.environ.get("PCMP_PHASE_TIMES") == "1" else None
-    return TrainState(model, flat, opt, ddp, clip=clip, timer=timer, throttle=StepThrottle(dev))
+    return TrainState(model, flat, opt, ddp, clip=clip, timer=timer, throttle=StepThrottle(dev),
+                      prio=PriorityStream(dev))
 
 
 def _logits(model, x):
@@ -163,11 +165,12 @@ def train_image_classifier(state: TrainState, trainloader, testloader, epochs=1,
             steps += 1
             if verbose_steps:
                 printer(steps)
-            state.zero_grad()
-            with state.phase("forward"):
-                loss = cross_entropy(_logits(model, x), y)
-            state.backward_step(loss)
-            running += loss.detach().double()
+            with (state.prio.step(x, y) if state.prio is not None else contextlib.nullcontext()):
+                state.zero_grad()
+                with state.phase("forward"):
+                    loss = cross_entropy(_logits(model, x), y)
+                state.backward_step(loss)
+                running += loss.detach().double()
             n_in_window += 1
         printer(R.TRAINLOADER_DONE)
         if (epoch % print_every) == 0 or epoch == epochs - 1:
@@ -203,9 +206,18 @@ def train_image_classifier(state: TrainState, trainloader, testloader, epochs=1,
 
 # ---------------------------------------------------------------------------------- text
 def train_text_classifier(state: TrainState, train_loader, val_loader=None, epochs=3, print_batches=False,
-                          progress_every=40, printer=R.rprint):
+                          progress_every=40, printer=R.rprint, graph=False):
+    """The reference's BERT / text training loop (pytorch_on_language_distr.py:219-335).  ``graph``:
+    replay each full-size batch's step from one captured hipGraph (:class:`pcmp.engine.graph.
+    GraphedStep`; single process, GPU); other batch shapes run eagerly."""
     model = state.model
     times = []
+    graphed = None
+    use_graph = bool(graph) and state.ddp is None and state.flat.device.type == "cuda"
+
+    def loss_of(ids, mask, labels):
+        return model(ids, None, mask, labels)[0] if _is_bert(model) else cross_entropy(
+            model.forward_logits(ids, mask), labels)
     for epoch_i in range(epochs):
         printer("")
         printer(R.text_epoch_header(epoch_i, epochs))
@@ -224,10 +236,18 @@ def train_text_classifier(state: TrainState, train_loader, val_loader=None, epoc
             if step % progress_every == 0 and not step == 0:
                 printer(R.batch_progress_line(step, nsteps, R.format_time(time.time() - t0)))
             ids, mask, labels = batch
+            if use_graph and graphed is None:
+                from .graph import GraphedStep
+                graphed = GraphedStep(state, loss_of, [ids, mask, labels])
+            if graphed is not None and graphed.matches(ids, mask, labels):
+                loss = graphed(ids, mask, labels)
+                total += loss.double()
+                n += 1
+                watchdog_kick("train_step")
+                continue
             state.zero_grad()
             with state.phase("forward"):
-                loss = model(ids, None, mask, labels)[0] if _is_bert(model) else cross_entropy(
-                    model.forward_logits(ids, mask), labels)
+                loss = loss_of(ids, mask, labels)
             total += loss.detach().double()
             n += 1
             state.backward_step(loss)

@@ -17,11 +17,17 @@ from .params import compute_weight, compute_weight_t, emit_grad
 
 
 class _RNG:
-    """Dropout seed/offset stream: deterministic given ``torch.initial_seed()``."""
+    """Dropout seed/offset stream: deterministic given ``torch.initial_seed()``.
+
+    ``salt`` (set by :class:`pcmp.engine.graph.GraphedStep` while it captures a training step) is
+    a device int64 counter that the dropout / attention kernels mix into the seed; the captured step
+    increments it, so every replay of the graph draws new masks although the kernels' arguments
+    are frozen at capture time.  Eager steps leave it None."""
 
     def __init__(self):
         self.seed = None
         self.counter = itertools.count()
+        self.salt = None
 
     def next(self, n: int):
         if self.seed is None:
@@ -83,13 +89,13 @@ class DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p):
         seed, off = dropout_rng.next(x.numel())
-        ctx.cfg = (p, seed, off)
-        return K.dropout(x.contiguous(), p, seed, off)
+        ctx.cfg = (p, seed, off, dropout_rng.salt)
+        return K.dropout(x.contiguous(), p, seed, off, dropout_rng.salt)
 
     @staticmethod
     def backward(ctx, dy):
-        p, seed, off = ctx.cfg
-        return K.dropout(dy.contiguous(), p, seed, off), None
+        p, seed, off, salt = ctx.cfg
+        return K.dropout(dy.contiguous(), p, seed, off, salt), None
 
 
 class SoftmaxXentFn(torch.autograd.Function):

@@ -309,7 +309,14 @@ def hash_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
     return (u32 >> 8).float() * (1.0 / 16777216.0)
 
 
-def dropout(x, p, seed, offset):
+def _salted(seed, salt):
+    if salt is None:
+        return seed
+    return (seed + int(salt.reshape(-1)[0].item()) * 0x9E3779B97F4A7C15) & _M64
+
+
+def dropout(x, p, seed, offset, salt=None):
+    seed = _salted(seed, salt)
     idx = torch.arange(x.numel(), device=x.device, dtype=torch.int64) + offset
     keep = hash_uniform(seed, idx).view(x.shape) >= p
     return torch.where(keep, x.float() / (1.0 - p), torch.zeros((), device=x.device)).to(x.dtype)
@@ -576,7 +583,8 @@ def _attn_drop(B, H, S, p, seed, offset, device):
     return keep.float() / (1.0 - p)
 
 
-def attention_fwd(qkv, ids, B, S, H, p_drop, seed, offset):
+def attention_fwd(qkv, ids, B, S, H, p_drop, seed, offset, salt=None):
+    seed = _salted(seed, salt)
     q, k, v, bias, D = _attn_prep(qkv, ids, B, S, H)
     s = q @ k.transpose(-1, -2) * 0.125 + bias
     lse = torch.logsumexp(s, -1)
@@ -589,7 +597,8 @@ def attention_fwd(qkv, ids, B, S, H, p_drop, seed, offset):
     return [ctx.to(qkv.dtype), lse.reshape(B * H, S)]
 
 
-def attention_bwd(dctx, qkv, ctx, lse, ids, B, S, H, p_drop, seed, offset):
+def attention_bwd(dctx, qkv, ctx, lse, ids, B, S, H, p_drop, seed, offset, salt=None):
+    seed = _salted(seed, salt)
     q, k, v, bias, D = _attn_prep(qkv, ids, B, S, H)
     d = D // H
     dO = dctx.float().view(B, S, H, d).transpose(1, 2)

@@ -60,16 +60,18 @@ class AttentionFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, ids, B, S, H, p_drop):
         seed, off = dropout_rng.next(B * H * S * S) if p_drop > 0 else (0, 0)
-        out, lse = K.attention_fwd(qkv.contiguous(), ids, B, S, H, p_drop, seed, off)
+        salt = dropout_rng.salt if p_drop > 0 else None
+        out, lse = K.attention_fwd(qkv.contiguous(), ids, B, S, H, p_drop, seed, off, salt)
         ctx.save_for_backward(qkv, out, lse, ids if ids is not None else torch.empty(0))
-        ctx.cfg = (B, S, H, p_drop, seed, off, ids is not None)
+        ctx.cfg = (B, S, H, p_drop, seed, off, ids is not None, salt)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse, ids = ctx.saved_tensors
-        B, S, H, p, seed, off, has_ids = ctx.cfg
-        dqkv = K.attention_bwd(dout.contiguous(), qkv, out, lse, ids if has_ids else None, B, S, H, p, seed, off)
+        B, S, H, p, seed, off, has_ids, salt = ctx.cfg
+        dqkv = K.attention_bwd(dout.contiguous(), qkv, out, lse, ids if has_ids else None, B, S, H, p, seed, off,
+                               salt)
         return dqkv, None, None, None, None, None
 
 

@@ -37,6 +37,8 @@ def main(argv=None):
     ap.add_argument("--test-size", type=int, default=2500)
     ap.add_argument("--layers", type=int, default=None, help="override encoder depth (tests)")
     ap.add_argument("--print-batches", action="store_true", help="reference's per-step print(batch)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each training step from one captured hipGraph (single GPU process)")
     args = ap.parse_args(argv)
     cli.apply_preset(args, dict(model="bilstm", epochs=3, batch_size=32))
     env = cli.setup(args)
@@ -88,7 +90,8 @@ def main(argv=None):
     state.sched = linear_schedule_with_warmup(state.opt, 0, total_steps)
     t0 = time.time()
     with cli.run_context(args, env):
-        times = train_text_classifier(state, train_loader, val_loader, args.epochs, print_batches=args.print_batches)
+        times = train_text_classifier(state, train_loader, val_loader, args.epochs, print_batches=args.print_batches,
+                                      graph=args.graph and not env.distributed)
         acc = test_text(model, test_loader)
     cli.write_json(args, {"script": "pytorch_on_language_distr", "model": args.model, "world_size": env.world_size,
                           "epoch_seconds": times, "train_loss": state.history["train_loss"], "test_accuracy": acc,

@@ -904,4 +904,4 @@ def test_resize_image_matches_pil_bit_exact(gpu, hw, out):
         z = _ops().resize_image(xd, out[0], out[1], mode, 8, 1 / 255.0, mean, std)
         zr = ref.resize_image(x, out[0], out[1], mode, 8, 1 / 255.0, mean, std)
         assert z.dtype == dt and z.shape == (2, out[0], out[1], 8)
-        close(z, zr, 1e-6, 1e-6)
+        close(z.cpu(), zr.cpu(), 1e-6, 1e-6)

@@ -174,3 +174,48 @@ def test_vgg16_step(gpu):
             a, b = a[:, None], b[:, None]
         row_err = (a - b).norm(dim=1) / (b.norm(dim=1) + 1e-3 * b.norm() + 1e-12)
         assert int((row_err > 0.05).sum()) <= 4, (n, row_err.max().item())
+
+
+def test_graphed_bert_step_matches_eager_without_dropout(gpu):
+    """GraphedStep (whole training step as one hipGraph) == eager steps bitwise-close when dropout is
+    off: same losses over 4 steps with AdamW + clipping + a linear LR schedule run between replays;
+    with dropout on, replays draw a new mask every step (device salt) and training still decreases."""
+    from pcmp.engine.graph import GraphedStep
+    from pcmp.engine.trainer import make_state
+    from pcmp.models.bert import BertConfig, BertForSequenceClassification
+    from pcmp.optim import linear_schedule_with_warmup
+    torch.manual_seed(0)
+    cfg = BertConfig(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    ids = torch.randint(1, 30522, (8, 128), device=gpu)
+    ids[:, 100:] = 0
+    mask = (ids > 0).long()
+    y = torch.randint(0, 2, (8,), device=gpu)
+    losses = {}
+    for mode in ("eager", "graph"):
+        torch.manual_seed(1)
+        m = BertForSequenceClassification(cfg).to(gpu)
+        st = make_state(m, "adamw", lr=1e-4, eps=1e-8, clip=1.0)
+        st.sched = linear_schedule_with_warmup(st.opt, 0, 8)
+        fn = lambda a, b, c, m=m: m(a, None, b, c)[0]   # noqa: E731
+        out = []
+        if mode == "graph":
+            g = GraphedStep(st, fn, [ids, mask, y])
+            for _ in range(4):
+                out.append(float(g(ids, mask, y)))
+        else:
+            for _ in range(4):
+                st.zero_grad()
+                loss = fn(ids, mask, y)
+                st.backward_step(loss)
+                out.append(float(loss))
+        losses[mode] = out
+    for a, b in zip(losses["eager"], losses["graph"]):
+        assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), losses
+    # dropout on: masks differ per replay (device salt), loss goes down on a fixed batch
+    torch.manual_seed(2)
+    m = BertForSequenceClassification(BertConfig(num_hidden_layers=2)).to(gpu)
+    st = make_state(m, "adamw", lr=3e-4, eps=1e-8, clip=1.0)
+    g = GraphedStep(st, lambda a, b, c: m(a, None, b, c)[0], [ids, mask, y])
+    seq = [float(g(ids, mask, y)) for _ in range(12)]
+    assert int(g.salt.item()) == 12
+    assert min(seq[-3:]) < seq[0], seq

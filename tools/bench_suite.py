@@ -166,6 +166,14 @@ def bert_train():
     m = bert_base().to(dev)
     t = timeit(hip_train_step(m, lambda: m(ids, None, mask, y)[0], "adamw", 2e-5, eps=1e-8, clip=1.0))
     emit(bench="bert_train", impl="hip", samples_s=32 / t, ms=t * 1e3, batch=32)
+    # the same step replayed from one captured hipGraph (pcmp.engine.graph.GraphedStep)
+    from pcmp.engine.graph import GraphedStep
+    from pcmp.engine.trainer import make_state
+    m2 = bert_base().to(dev)
+    st = make_state(m2, "adamw", lr=2e-5, eps=1e-8, clip=1.0)
+    g = GraphedStep(st, lambda a, b, c: m2(a, None, b, c)[0], [ids, mask, y])
+    t = timeit(lambda: g(ids, mask, y))
+    emit(bench="bert_train", impl="hip+hipgraph", samples_s=32 / t, ms=t * 1e3, batch=32)
     if HIP_ONLY:
         return
     hf = transformers.BertForSequenceClassification(transformers.BertConfig(num_labels=2)).to(dev)
