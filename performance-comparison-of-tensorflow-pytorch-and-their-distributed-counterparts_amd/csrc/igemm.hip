@@ -2112,7 +2112,7 @@ __global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src
 // ------------------------------------------------------------------------------------------------
 // host side
 // coalesced epilogue (igemm_epilogue_coal) for the 4-wave BM = 128 FWD / DGRAD kernels: A/B knob
-static Knob kn_epi_coal("epi_coal", 1);
+static Knob kn_epi_coal("epi_coal", 0);   // measured slower: profiles/r3_epi_coal_*.txt
 template <int MODE, int BM, int BN, int NTHR>
 static size_t coal_setup(IgemmParams& p, size_t smem) {
   p.coal = 0;
