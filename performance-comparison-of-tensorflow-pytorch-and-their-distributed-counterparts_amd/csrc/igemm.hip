@@ -55,14 +55,16 @@ struct IgemmParams {
   const __bf16* b;    // FWD: w[K][R][S][C]; DGRAD: wt[C][R][S][K]; WGRAD: x[N,H,W,C]
   void* out;          // FWD/DGRAD: bf16 [gm][gn]; WGRAD: f32 [split][gm][gn]
   const float* bias;  // FWD: [gn] (optional)
-  const __bf16* resid;  // FWD/DGRAD: bf16 [gm][gn] added before activation (optional)
+  const __bf16* resid;  // FWD/DGRAD: bf16 [gm][gn] added before activation (optional); act 3: u
+  __bf16* aux;          // act 2: bf16 [gm][gn] pre-activation output u (GELU's backward operand)
   float* stats;       // FWD/DGRAD: [gridM][2][gn] per-block column sum / sum of squares (optional)
   int gm, gn, gk;
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   FastDiv fd_PQ, fd_Q, fd_HW, fd_W;
   // DGRAD decode: rows m -> (n, hh, ww) over [N][dH][dW]; h = hh*ostep + oph (sub-pixel class)
   int dH, dW, offy, offx, sub, oph, opw;
-  int relu;
+  int relu;         // epilogue activation: 0 none, 1 ReLU, 2 GELU (u = acc + bias -> aux, out = gelu(u)),
+                    // 3 GELU backward (out = acc * gelu'(u), u read through resid; BERT FFN)
   unsigned a_bytes, b_bytes;   // buffer-resource extents of a / b (hardware OOB -> zero)
   int ksplit;       // K elements per split (multiple of BK)
   int nsplit;
@@ -419,7 +421,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
     };
     if constexpr (NTHR == NT && BM == 128 && (BN == 128 || BN == 64) && !SHRED && MODE != MODE_WGRAD) {
-      if (p.coal && p.nsplit == 1 && p.grp == 0) {
+      if (p.coal && p.nsplit == 1 && p.grp == 0 && p.relu < 2) {
         igemm_epilogue_coal<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m);
         return;
       }
@@ -563,17 +565,24 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           if (mfx) { ldt(msc, 2, j0); ldt(msh, 3, j0); }
           if constexpr (bnr2) { ldt(ka2, 4, j0); ldt(kb2, 5, j0); }
         }
-        unsigned ov[NP];
+        unsigned ov[NP], av[NP];
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
           const int j = j0 + (q >> 1), e0 = (q & 1) * 2, ce = 2 * q;   // ce: channel within the store
           float x0 = acc[j][i][e0] + bias[ce];
           float x1 = acc[j][i][e0 + 1] + bias[ce + 1];
           if (has_res) {
-            x0 += __uint_as_float(rvA[b][q] << 16);
-            x1 += __uint_as_float(rvA[b][q] & 0xffff0000u);
+            const float r0 = __uint_as_float(rvA[b][q] << 16), r1 = __uint_as_float(rvA[b][q] & 0xffff0000u);
+            if (p.relu == 3) { x0 *= dgelu_erf(r0); x1 *= dgelu_erf(r1); }
+            else { x0 += r0; x1 += r1; }
           }
-          if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+          if (p.relu == 1) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+          else if (p.relu == 2) {   // u (bf16) -> aux; out = gelu(u) as the separate kernel would
+            const unsigned uu = f2bf2(x0, x1);
+            av[q] = uu;
+            x0 = gelu_erf(__uint_as_float(uu << 16));
+            x1 = gelu_erf(__uint_as_float(uu & 0xffff0000u));
+          }
           unsigned u = f2bf2(x0, x1);
           if constexpr (bnr) {
             const float xa = __uint_as_float(xvA[b][q] << 16), xb = __uint_as_float(xvA[b][q] & 0xffff0000u);
@@ -608,6 +617,10 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
         }
         if constexpr (VW == 8) *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(ov);
         else *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<const uint2*>(ov);
+        if (p.relu == 2) {
+          if constexpr (VW == 8) *reinterpret_cast<uint4*>(p.aux + o) = *reinterpret_cast<const uint4*>(av);
+          else *reinterpret_cast<uint2*>(p.aux + o) = *reinterpret_cast<const uint2*>(av);
+        }
       }
     }
     if constexpr (stats || bnr) {
@@ -1947,6 +1960,7 @@ static void launch_skinny(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, 64);
   p.tiles_n = ceil_div(p.gn, 64);
   TORCH_CHECK(p.C % 32 == 0 && p.ksplit % 32 == 0 && p.gn % 4 == 0, "skinny_fwd: C, ksplit multiples of 32");
+  TORCH_CHECK(p.relu < 2, "skinny_fwd: ReLU / plain epilogue only");
   const int grid = p.tiles_m * p.tiles_n * p.nsplit;
   hipLaunchKernelGGL(skinny_fwd_kernel<8>, dim3(grid), dim3(NT), 0, st, p);
   PCMP_LAUNCH_CHECK();
@@ -2021,7 +2035,7 @@ __global__ void __launch_bounds__(256) splitk_reduce2_kernel(const float* __rest
 __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float* __restrict__ ws, __bf16* __restrict__ out,
                                                               const float* __restrict__ bias,
                                                               const __bf16* __restrict__ resid, int64_t n, int gn,
-                                                              int nsplit, int relu) {
+                                                              int nsplit, int relu, __bf16* __restrict__ aux) {
   // one float4 column per thread over a grid that covers the output (the layout of the BN apply
   // kernels, profiles/r2_ew_apply_ab.txt); the split slabs are read four at a time
   const int64_t n4 = n >> 2;
@@ -2037,16 +2051,18 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float* __res
   }
   for (; k < nsplit; ++k) s += w4[(size_t)k * n4 + i];
   const int c = (int)((i * 4) % gn);
-  u16x4 rv, ov;
+  u16x4 rv, ov, av;
   if (resid) rv = reinterpret_cast<const u16x4*>(resid)[i];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float x = s[e] + (bias ? bias[c + e] : 0.f);
-    if (resid) x += bf2f(rv[e]);
-    if (relu) x = fmaxf(x, 0.f);
+    if (resid) x = relu == 3 ? x * dgelu_erf(bf2f(rv[e])) : x + bf2f(rv[e]);
+    if (relu == 1) x = fmaxf(x, 0.f);
+    else if (relu == 2) { av[e] = f2bf(x); x = gelu_erf(bf2f(av[e])); }
     ov[e] = f2bf(x);
   }
   reinterpret_cast<u16x4*>(out)[i] = ov;
+  if (relu == 2) reinterpret_cast<u16x4*>(aux)[i] = av;
 }
 
 // weight transpose for DGRAD: wt[c][t][k] = w[k][r(t)][s(t)][c]  (bf16), taps t over a
@@ -2117,7 +2133,7 @@ template <int MODE, int BM, int BN, int NTHR>
 static size_t coal_setup(IgemmParams& p, size_t smem) {
   p.coal = 0;
   if constexpr (MODE != MODE_WGRAD && NTHR == NT && BM == 128 && (BN == 128 || BN == 64)) {
-    if (kn_epi_coal.get() && p.nsplit == 1 && p.grp == 0 && p.gn % 8 == 0) {
+    if (kn_epi_coal.get() && p.nsplit == 1 && p.grp == 0 && p.gn % 8 == 0 && p.relu < 2) {
       p.coal = 1;
       smem = std::max(smem, (size_t)(BM * (BN + 4) + 7 * BN) * sizeof(float));
     }
@@ -2676,7 +2692,7 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
     const int64_t n = (int64_t)p.gm * p.gn;
     const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out,
-                       MODE == MODE_FWD ? p.bias : nullptr, resid, n, p.gn, nsplit, p.relu);
+                       MODE == MODE_FWD ? p.bias : nullptr, resid, n, p.gn, nsplit, p.relu, p.aux);
     PCMP_LAUNCH_CHECK();
   }
 }
@@ -2739,7 +2755,7 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
         if (kind == 5 && p.gn > 1024) continue;
         cands.push_back({kind, ns});
       }
-      if (MODE == MODE_FWD && p.C % 32 == 0 && p.gk % 32 == 0 && p.gn % 4 == 0 && p.gm <= 1024 &&
+      if (MODE == MODE_FWD && p.relu < 2 && p.C % 32 == 0 && p.gk % 32 == 0 && p.gn % 4 == 0 && p.gm <= 1024 &&
           p.gk / 32 / ns >= 2)
         cands.push_back({6, ns});
     }
@@ -2882,7 +2898,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.fd_HW = make_fastdiv(H * W);
   p.fd_W = make_fastdiv(W);
   p.dH = H; p.dW = W; p.offy = pad; p.offx = pad; p.sub = 0; p.oph = 0; p.opw = 0;
-  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.stats2 = nullptr;
+  p.bias = nullptr; p.resid = nullptr; p.aux = nullptr; p.stats = nullptr; p.stats2 = nullptr;
   p.bn_mask = nullptr; p.bn_x = nullptr; p.bn_mean = nullptr; p.bn_istd = nullptr;
   p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr; p.bn_msc = nullptr; p.bn_msh = nullptr;
   p.bn_mbits = nullptr;
@@ -2892,11 +2908,11 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
 }
 
 // x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
-// (bf16 [N,P,Q,K]) and ReLU fused; optional stats output [tiles_m,2,K] f32 (returned).
-std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
-                                 const c10::optional<at::Tensor>& bias,
-                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats) {
-  if (x.scalar_type() == at::kFloat) return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats);
+// (bf16 [N,P,Q,K]) and activation (act: IgemmParams::relu) fused; optional stats output
+// [tiles_m,2,K] f32 (returned).  act 2 (GELU) also returns the pre-activation u.
+static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                             const c10::optional<at::Tensor>& bias,
+                                             const c10::optional<at::Tensor>& resid, int act, bool want_stats) {
   PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(x); PCMP_CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: NHWC x and KRSC w expected");
@@ -2917,7 +2933,13 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
     TORCH_CHECK(resid->numel() == y.numel(), "conv_fwd: residual shape");
     p.resid = ptr<__bf16>(*resid);
   }
-  p.relu = relu;
+  p.relu = act;
+  at::Tensor u;
+  if (act == 2) {
+    TORCH_CHECK(!want_stats, "conv_fwd: GELU epilogue without statistics");
+    u = at::empty_like(y);
+    p.aux = ptr<__bf16>(u);
+  }
   p.ksplit = p.gk; p.nsplit = 1;
   const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
   const int BNsel = p.gn <= 64 ? 64 : 128;
@@ -2932,7 +2954,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   if (plain_gemm_eligible<MODE_FWD>(p)) {
     const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
     run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
-    return {y};
+    return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
   }
   // Small-M shapes (batch-1 inference: 49..3136 pixels) leave most of the 256 CUs idle; split the
   // reduction so the grid reaches ~256 workgroups, then reduce + epilogue in one pass.
@@ -2948,7 +2970,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   if (!want_stats && tiles < 128 && ksteps >= 8 && kn_gemm_plan.get()) {
     const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st, true, nsplit);
     run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
-    return {y};
+    return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
   }
   if (nsplit > 1) {
     const int steps_per = ceil_div(ksteps, nsplit);
@@ -2961,13 +2983,31 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
     dispatch<MODE_FWD>(p, st);
     const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<__bf16>(y),
-                       p.bias, p.resid, n, p.gn, nsplit, (int)relu);
+                       p.bias, p.resid, n, p.gn, nsplit, p.relu, p.aux);
     PCMP_LAUNCH_CHECK();
-    return {y};
+    return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
   }
   dispatch<MODE_FWD>(p, st);
   if (want_stats) return {y, stats_red.defined() ? stats_red : stats};
-  return {y};
+  return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
+}
+
+
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias,
+                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats) {
+  if (x.scalar_type() == at::kFloat) return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats);
+  return conv_fwd_impl(x, w, stride, pad, bias, resid, relu ? 1 : 0, want_stats);
+}
+
+// Linear y = gelu(x W^T + b) with the GELU fused into the GEMM epilogue: x [M, C], w [N, C] bf16
+// -> [gelu(u), u] (u = x W^T + b, kept for the backward).  BERT's FFN up-projection
+// (pytorch_on_language_distr.py:151-161 via BertIntermediate).
+std::vector<at::Tensor> linear_gelu_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "linear_gelu_fwd: x [M, C], w [N, C]");
+  const int64_t M = x.size(0), C = x.size(1), N = w.size(0);
+  auto r = conv_fwd_impl(x.view({M, 1, 1, C}), w.view({N, 1, 1, C}), 1, 0, bias, c10::nullopt, 2, false);
+  return {r[0].view({M, N}), r[1].view({M, N})};
 }
 
 static at::Tensor transpose_taps(const at::Tensor& w, int r0, int s0, int rstep, int subR, int subS,
@@ -3000,7 +3040,8 @@ struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (s
 
 static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
                                           int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
-                                          const BnrArgs* bn, const c10::optional<at::Tensor>& wt_given) {
+                                          const BnrArgs* bn, const c10::optional<at::Tensor>& wt_given,
+                                          const at::Tensor* dgelu_u = nullptr) {
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(w);
   const int N = dy.size(0), K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
@@ -3126,6 +3167,13 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(wt); p.out = dx.data_ptr();
   p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(wt);
   if (has_res) p.resid = ptr<__bf16>(*resid);
+  if (dgelu_u) {   // dx = dgrad * gelu'(u): the GELU backward of the layer that produced dy's input
+    TORCH_CHECK(!has_res && !bn && stride == 1 && R == 1 && S == 1, "linear_dgrad_gelu: plain 1x1 GEMM only");
+    PCMP_CHECK_BF16(*dgelu_u); PCMP_CHECK_CONTIG(*dgelu_u);
+    TORCH_CHECK(dgelu_u->numel() == (int64_t)N * H * W * C, "linear_dgrad_gelu: u shape");
+    p.resid = ptr<__bf16>(*dgelu_u);
+    p.relu = 3;
+  }
   p.ksplit = p.gk;
   if (!bn && plain_gemm_eligible<MODE_DGRAD>(p)) {
     const GemmPlan pl = plan_gemm<MODE_DGRAD>(p, ptr<__bf16>(dx), fopts, st);
@@ -3160,6 +3208,18 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
                       int64_t pad, const c10::optional<at::Tensor>& resid, const c10::optional<at::Tensor>& wt) {
   if (dy.scalar_type() == at::kFloat) return f32::conv_dgrad(dy, w, H, W, stride, pad, resid);
   return dgrad_impl(dy, w, H, W, stride, pad, resid, nullptr, wt)[0];
+}
+
+// Linear input gradient through a GELU: dy [M, N], w [N, C] -> du = (dy W) * gelu'(u), u [M, C] the
+// pre-activation saved by linear_gelu_fwd (the GELU backward fused into the DGRAD epilogue).
+at::Tensor linear_dgrad_gelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& u,
+                             const c10::optional<at::Tensor>& wt) {
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && u.dim() == 2 && dy.size(1) == w.size(0) && u.size(1) == w.size(1) &&
+              u.size(0) == dy.size(0), "linear_dgrad_gelu: dy [M, N], w [N, C], u [M, C]");
+  const int64_t M = dy.size(0), N = w.size(0), C = w.size(1);
+  const at::Tensor u4 = u.view({M, 1, 1, C});
+  auto dx = dgrad_impl(dy.view({M, 1, 1, N}), w.view({N, 1, 1, C}), 1, 1, 1, 0, c10::nullopt, nullptr, wt, &u4)[0];
+  return dx.view({M, C});
 }
 
 // conv_dgrad with the BatchNorm-backward reduction of the layer(s) whose output gradient this is
@@ -3359,4 +3419,6 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
         &pcmp::conv_wgrad);
+  m.def("linear_gelu_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor[]", &pcmp::linear_gelu_fwd);
+  m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor? wt=None) -> Tensor", &pcmp::linear_dgrad_gelu);
 }

@@ -15,6 +15,7 @@ Pretrained weights are not downloadable here (no network); ``load_hf`` maps a HF
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -23,8 +24,12 @@ from torch import nn
 from ..ops import _lib
 from ..ops.functions import cross_entropy
 from ..ops.rnn import EmbeddingFn
-from ..ops.transformer import attention, gelu, layer_norm, tanh
+from ..ops.transformer import BertAttentionBlockFn, BertFFNBlockFn, attention, gelu, layer_norm, tanh
 from .layers import Dropout, Linear
+
+# PCMP_BERT_FUSED=0: the op-by-op layer (separate dropout / GELU / LayerNorm-backward / bias-grad
+# launches and the autograd add of h's two gradients) -- for A/B runs and parity tests
+_FUSED = os.environ.get("PCMP_BERT_FUSED", "1") != "0"
 
 
 @dataclass
@@ -79,12 +84,24 @@ class BertLayer(nn.Module):
             _init_linear(lin, c.initializer_range)
 
     def forward(self, h, ids, B, S):
+        if _FUSED:
+            return self.forward_fused(h, ids, B, S)
         qkv = self.qkv(h)
         ctx = attention(qkv, ids, B, S, self.heads, self.p_attn if self.training else 0.0)
         a = self.drop(self.attn_out(ctx))
         h1 = self.ln1(a, h)
         f = self.drop(self.ffn2(gelu(self.ffn1(h1))))
         return self.ln2(f, h1)
+
+    def forward_fused(self, h, ids, B, S):
+        """Same math as the op-by-op path, as two fused autograd nodes (ops/transformer.py)."""
+        p_attn = self.p_attn if self.training else 0.0
+        p_hid = self.drop.p if self.training else 0.0
+        h1 = BertAttentionBlockFn.apply(h, ids, self.qkv.weight, self.qkv.bias, self.attn_out.weight,
+                                        self.attn_out.bias, self.ln1.weight, self.ln1.bias, B, S, self.heads,
+                                        p_attn, p_hid, self.ln1.eps)
+        return BertFFNBlockFn.apply(h1, self.ffn1.weight, self.ffn1.bias, self.ffn2.weight, self.ffn2.bias,
+                                    self.ln2.weight, self.ln2.bias, p_hid, self.ln2.eps)
 
 
 class BertForSequenceClassification(nn.Module):

@@ -517,9 +517,14 @@ def lstm_seq_bwd(dhout, gates, cst, whh, ids):
 
 
 # ------------------------------------------------------------------------------ transformer
-def layernorm_fwd(x, r, g, b, eps):
-    xs = x.float() + r.float() if r is not None else x.float()
-    if r is not None:
+def layernorm_fwd(x, r, g, b, eps, p=0.0, seed=0, offset=0, salt=None):
+    xf = x.float()
+    if p > 0:
+        idx = torch.arange(x.numel(), device=x.device, dtype=torch.int64) + offset
+        keep = hash_uniform(_salted(seed, salt), idx).view(x.shape) >= p
+        xf = torch.where(keep, xf / (1.0 - p), torch.zeros((), device=x.device))
+    xs = xf + r.float() if r is not None else xf
+    if r is not None or p > 0:
         xs = xs.to(x.dtype).float()
     mean = xs.mean(-1)
     var = ((xs - mean.unsqueeze(-1)) ** 2).mean(-1)
@@ -540,6 +545,36 @@ def layernorm_bwd(dy, xs, mean, rstd, g, dg, db, accumulate):
     if db is not None:
         (db.add_ if accumulate else db.copy_)(dyf.sum(0))
     return dx.reshape(xs.shape).to(dy.dtype)
+
+
+def layernorm_bwd_fused(dy, xs, mean, rstd, g, dg, db, dbias, accmask, p, seed, offset, salt=None):
+    """Reference of csrc/transformer.hip ln_bwd_fused_kernel: [dx, dxd] plus dgamma / dbeta /
+    dbias (column sums of dy*xhat, dy, dxd) written or accumulated (bit w of accmask)."""
+    D = xs.shape[-1]
+    dyf = dy.float().reshape(-1, D)
+    xh = (xs.float().reshape(-1, D) - mean.view(-1, 1)) * rstd.view(-1, 1)
+    gy = dyf * g
+    dx = (rstd.view(-1, 1) * (gy - gy.mean(-1, keepdim=True) - xh * (gy * xh).mean(-1, keepdim=True))).to(dy.dtype)
+    dxd = dropout(dx, p, seed, offset, salt) if p > 0 else dx
+    for w, (out, val) in enumerate(((dg, (dyf * xh).sum(0)), (db, dyf.sum(0)), (dbias, dxd.float().sum(0)))):
+        if out is not None:
+            (out.add_ if (accmask >> w) & 1 else out.copy_)(val)
+    return [dx.reshape(xs.shape), dxd.reshape(xs.shape)]
+
+
+def linear_gelu_fwd(x, w, bias=None):
+    u = x.float() @ w.float().t()
+    if bias is not None:
+        u = u + bias.float()
+    u = u.to(x.dtype)
+    return [F.gelu(u.float()).to(x.dtype), u]
+
+
+def linear_dgrad_gelu(dy, w, u, wt=None):
+    uf = u.float()
+    cdf = 0.5 * (1 + torch.erf(uf * 0.7071067811865476))
+    pdf = 0.3989422804014327 * torch.exp(-0.5 * uf * uf)
+    return ((dy.float() @ w.float()) * (cdf + uf * pdf)).to(dy.dtype)
 
 
 def gelu_fwd(x):

@@ -5,7 +5,7 @@ import torch
 
 from .functions import dropout_rng
 from .kernels import K
-from .params import sink_or_temp
+from .params import compute_weight, compute_weight_t, emit_grad, sink_or_temp
 
 
 class LayerNormFn(torch.autograd.Function):
@@ -89,3 +89,124 @@ def tanh(x):
 
 def attention(qkv, ids, B, S, H, p_drop=0.0):
     return AttentionFn.apply(qkv, ids, B, S, H, p_drop)
+
+
+# ------------------------------------------------------------------------------------------------
+# Fused BERT sublayers.  Each post-LN sublayer of BertLayer is ONE autograd node whose backward
+# issues the kernels itself, so that the fusions that cross op boundaries are possible:
+#   * dropout(sublayer output) + residual add + LayerNorm: one forward kernel (layernorm_fwd with
+#     p), one backward kernel (layernorm_bwd_fused) that also emits the dropped branch's gradient and
+#     the bias gradient of the projection that produced it (no dropout / colsum launches);
+#   * the residual gradient is added in the epilogue of the sublayer input's DGRAD GEMM (no
+#     autograd-engine at::add of the two gradients of h);
+#   * GELU: in the epilogue of the FFN up-projection (forward: out = gelu(u), u kept) and of the
+#     down-projection's DGRAD (backward: du = (df W2) * gelu'(u)).
+# Reference: BertLayer = BertAttention(BertSelfAttention + BertSelfOutput) + BertIntermediate +
+# BertOutput of the HF model the reference fine-tunes (pytorch_on_language_distr.py:151-161).
+
+def _gemm(x, w, bias):
+    M, C = x.shape
+    N = w.shape[0]
+    return K.conv_fwd(x.reshape(M, 1, 1, C), w.reshape(N, 1, 1, C), 1, 0, bias, None, False, False)[0].reshape(M, N)
+
+
+def _dgrad(dy, w, wt, resid=None):
+    M, N = dy.shape
+    C = w.shape[1]
+    return K.conv_dgrad(dy.reshape(M, 1, 1, N), w.reshape(N, 1, 1, C), 1, 1, 1, 0,
+                        None if resid is None else resid.reshape(M, 1, 1, C), wt).reshape(M, C)
+
+
+def _wgrad(p, dy, x):
+    M, N = dy.shape
+    C = x.shape[1]
+    return emit_grad(p, lambda out, acc: K.conv_wgrad(dy.reshape(M, 1, 1, N), x.reshape(M, 1, 1, C), out, 1, 1, 1, 0,
+                                                        acc))
+
+
+def _ln_fwd(ctx, a, resid, gamma, beta, eps, p):
+    seed, off = dropout_rng.next(a.numel()) if p > 0 else (0, 0)
+    salt = dropout_rng.salt if p > 0 else None
+    y, xs, mean, rstd = K.layernorm_fwd(a, resid, gamma.detach(), beta.detach(), eps, p, seed, off, salt)
+    ctx.ln = (p, seed, off, salt)
+    return y, xs, mean, rstd
+
+
+def _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, bias):
+    """-> (dresid, dbranch); gamma / beta / the branch bias gradients emitted."""
+    p, seed, off, salt = ctx.ln
+    outs, fins, accmask = [], [], 0
+    for w, prm in enumerate((gamma, beta, bias)):
+        out, acc, fin = sink_or_temp(prm)
+        outs.append(out)
+        fins.append(fin)
+        accmask |= int(bool(acc)) << w
+    dx, dxd = K.layernorm_bwd_fused(dy.contiguous(), xs, mean, rstd, gamma.detach(), outs[0], outs[1], outs[2],
+                                    accmask, p, seed, off, salt)
+    return dx, dxd, [fin() for fin in fins]
+
+
+class BertAttentionBlockFn(torch.autograd.Function):
+    """h1 = LayerNorm(h + dropout(attn_out(attention(qkv(h)))))."""
+
+    @staticmethod
+    def forward(ctx, h, ids, wqkv, bqkv, wo, bo, gamma, beta, B, S, H, p_attn, p_hid, eps):
+        dt = h.dtype
+        wq, wo_c = compute_weight(wqkv, dt), compute_weight(wo, dt)
+        qkv = _gemm(h, wq, bqkv.detach().float())
+        seed, off = dropout_rng.next(B * H * S * S) if p_attn > 0 else (0, 0)
+        salt = dropout_rng.salt if p_attn > 0 else None
+        out, lse = K.attention_fwd(qkv, ids, B, S, H, p_attn, seed, off, salt)
+        a = _gemm(out, wo_c, bo.detach().float())
+        y, xs, mean, rstd = _ln_fwd(ctx, a, h, gamma, beta, eps, p_hid)
+        ctx.save_for_backward(h, qkv, out, lse, ids if ids is not None else torch.empty(0), xs, mean, rstd)
+        ctx.attn = (B, S, H, p_attn, seed, off, ids is not None, salt)
+        ctx.params = (wqkv, bqkv, wo, bo, gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, qkv, out, lse, ids, xs, mean, rstd = ctx.saved_tensors
+        wqkv, bqkv, wo, bo, gamma, beta = ctx.params
+        B, S, H, p, seed, off, has_ids, salt = ctx.attn
+        dt = h.dtype
+        if dy.dtype != dt:
+            dy = dy.to(dt)
+        dres, da, (gg, gb, gbo) = _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, bo)
+        gwo = _wgrad(wo, da, out)
+        dctx = _dgrad(da, compute_weight(wo, dt), compute_weight_t(wo, dt))
+        dqkv = K.attention_bwd(dctx, qkv, out, lse, ids if has_ids else None, B, S, H, p, seed, off, salt)
+        gwq = _wgrad(wqkv, dqkv, h)
+        gbq = emit_grad(bqkv, lambda o, acc: K.colsum(dqkv, o, acc))
+        dh = _dgrad(dqkv, compute_weight(wqkv, dt), compute_weight_t(wqkv, dt), dres) if ctx.needs_input_grad[0] else None
+        return dh, None, gwq, gbq, gwo, gbo, gg, gb, None, None, None, None, None, None
+
+
+class BertFFNBlockFn(torch.autograd.Function):
+    """h2 = LayerNorm(h1 + dropout(ffn2(gelu(ffn1(h1)))))."""
+
+    @staticmethod
+    def forward(ctx, h1, w1, b1, w2, b2, gamma, beta, p_hid, eps):
+        dt = h1.dtype
+        w1c, w2c = compute_weight(w1, dt), compute_weight(w2, dt)
+        g, u = K.linear_gelu_fwd(h1, w1c, b1.detach().float())
+        f = _gemm(g, w2c, b2.detach().float())
+        y, xs, mean, rstd = _ln_fwd(ctx, f, h1, gamma, beta, eps, p_hid)
+        ctx.save_for_backward(h1, g, u, xs, mean, rstd)
+        ctx.params = (w1, b1, w2, b2, gamma, beta)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h1, g, u, xs, mean, rstd = ctx.saved_tensors
+        w1, b1, w2, b2, gamma, beta = ctx.params
+        dt = h1.dtype
+        if dy.dtype != dt:
+            dy = dy.to(dt)
+        dres, df, (gg, gb, gb2) = _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, b2)
+        gw2 = _wgrad(w2, df, g)
+        du = K.linear_dgrad_gelu(df, compute_weight(w2, dt), u, compute_weight_t(w2, dt))
+        gw1 = _wgrad(w1, du, h1)
+        gb1 = emit_grad(b1, lambda o, acc: K.colsum(du, o, acc))
+        dh1 = _dgrad(du, compute_weight(w1, dt), compute_weight_t(w1, dt), dres) if ctx.needs_input_grad[0] else None
+        return dh1, gw1, gb1, gw2, gb2, gg, gb, None, None

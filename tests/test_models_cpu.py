@@ -104,6 +104,30 @@ def test_bert_matches_hf():
     assert _rel(m.layers[1].ffn1.weight.grad, sd["bert.encoder.layer.1.intermediate.dense.weight"].grad) < 1e-4
 
 
+def test_bert_fused_sublayers_match_op_by_op(monkeypatch):
+    """The fused sublayer nodes (dropout+residual+LayerNorm fwd/bwd kernels, GELU and residual-grad
+    GEMM epilogues) give the op-by-op layer's loss and gradients, dropout ON (same RNG stream)."""
+    import pcmp.models.bert as bert
+    from pcmp.ops.functions import dropout_rng
+    kw = dict(num_hidden_layers=2, hidden_size=256, num_attention_heads=4, intermediate_size=512)
+    ids = torch.randint(1, 30522, (2, 32))
+    ids[1, 20:] = 0
+    y = torch.tensor([0, 1])
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(bert, "_FUSED", fused)
+        torch.manual_seed(0)
+        m = bert.BertForSequenceClassification(bert.BertConfig(**kw)).train()
+        dropout_rng.reseed(123)
+        loss, _ = m(ids, None, (ids > 0).long(), y)
+        loss.backward()
+        res[fused] = (loss.item(), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert abs(res[True][0] - res[False][0]) < 1e-5
+    assert set(res[True][1]) == set(res[False][1])
+    for n, g in res[False][1].items():
+        assert _rel(res[True][1][n], g) < 1e-4, n
+
+
 def test_bert_base_param_count():
     from pcmp.models.bert import bert_base
     from pcmp.models.resnet import count_params

@@ -88,6 +88,60 @@ def test_layernorm_act(gpu):
     close(ops().tanh_bwd(z, t), ref.tanh_bwd(z, t))
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_dropout_fused(gpu, p):
+    """LayerNorm(drop(x) + r) forward and the fused backward (dx, dropped-branch grad, dgamma,
+    dbeta, bias grad) against the fp32 reference with the same counter-based mask."""
+    M, D = 1000, 768
+    x = torch.randn(M, D, device=gpu).to(torch.bfloat16)
+    r = torch.randn(M, D, device=gpu).to(torch.bfloat16)
+    g = torch.rand(D, device=gpu) + 0.5
+    b = torch.randn(D, device=gpu)
+    salt = torch.tensor([3], device=gpu, dtype=torch.int64)
+    y, xs, m, s = ops().layernorm_fwd(x, r, g, b, 1e-12, p, 77, 1 << 32, salt)
+    yr, xsr, mr, sr = ref.layernorm_fwd(x, r, g, b, 1e-12, p, 77, 1 << 32, salt)
+    close(xs, xsr, 0, 1e-2)
+    close(y, yr)
+    dy = torch.randn(M, D, device=gpu).to(torch.bfloat16)
+    outs = [torch.full((D,), 0.5, device=gpu) for _ in range(6)]
+    dx, dxd = ops().layernorm_bwd_fused(dy, xs, m, s, g, outs[0], outs[1], outs[2], 0b100, p, 77, 1 << 32, salt)
+    dxr, dxdr = ref.layernorm_bwd_fused(dy, xs, m, s, g, outs[3], outs[4], outs[5], 0b100, p, 77, 1 << 32, salt)
+    close(dx, dxr)
+    close(dxd, dxdr)
+    if p == 0:
+        assert dxd.data_ptr() == dx.data_ptr()
+    else:
+        frac = (dxd == 0).float().mean().item()
+        assert abs(frac - p) < 0.02, frac
+    for a, c in zip(outs[:3], outs[3:]):
+        close(a, c, 1e-3, 1e-2)
+    # two outputs only (no bias gradient) and accumulate bits on gamma / beta
+    dg, db = torch.ones(D, device=gpu), torch.ones(D, device=gpu)
+    ops().layernorm_bwd_fused(dy, xs, m, s, g, dg, db, None, 0b011, p, 77, 1 << 32, salt)
+    close(dg, outs[3] + 1, 1e-3, 1e-2)
+    close(db, outs[4] + 1, 1e-3, 1e-2)
+
+
+@pytest.mark.parametrize("M", [4096, 300])
+def test_linear_gelu_epilogues(gpu, M):
+    """GELU fused into the up-projection's epilogue (out = gelu(u), u kept) and into the
+    down-projection's DGRAD epilogue (du = (dy W) * gelu'(u)), planner-chosen kernels / splits."""
+    torch.manual_seed(0)
+    C, N = 768, 3072
+    x = (torch.randn(M, C, device=gpu) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, C, device=gpu) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(N, device=gpu) * 0.1
+    gl, u = ops().linear_gelu_fwd(x, w, bias)
+    glr, ur = ref.linear_gelu_fwd(x, w, bias)
+    close(u, ur, 2e-2, 2e-2)
+    close(gl, glr, 2e-2, 2e-2)
+    w2 = (torch.randn(C, N, device=gpu) * 0.03).to(torch.bfloat16)
+    dy = torch.randn(M, C, device=gpu).to(torch.bfloat16)
+    du = ops().linear_dgrad_gelu(dy, w2, u)
+    dur = ref.linear_dgrad_gelu(dy, w2, u)
+    close(du, dur, 2e-2, 2e-2)
+
+
 @pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (64, 0.1), (96, 0.0), (32, 0.1)])
 def test_attention(gpu, S, p):
     torch.manual_seed(1)
@@ -174,6 +228,27 @@ def test_vgg16_step(gpu):
             a, b = a[:, None], b[:, None]
         row_err = (a - b).norm(dim=1) / (b.norm(dim=1) + 1e-3 * b.norm() + 1e-12)
         assert int((row_err > 0.05).sum()) <= 4, (n, row_err.max().item())
+
+
+def test_bert_fused_sublayers_native(gpu, monkeypatch):
+    """Fused sublayer nodes on the HIP kernels vs the op-by-op layer on the HIP kernels, dropout on
+    (same RNG stream): bf16-close loss and gradients."""
+    import pcmp.models.bert as bert
+    from pcmp.ops.functions import dropout_rng
+    ids = _ids(4, 128, 30522, gpu, lens=[128, 100, 50, 7])
+    y = torch.randint(0, 2, (4,), device=gpu)
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(bert, "_FUSED", fused)
+        torch.manual_seed(0)
+        m = bert.BertForSequenceClassification(bert.BertConfig(num_hidden_layers=2)).to(gpu).train()
+        dropout_rng.reseed(5)
+        loss, _ = m(ids, None, (ids > 0).long(), y)
+        loss.backward()
+        res[fused] = (loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert abs(res[True][0] - res[False][0]) < 2e-2
+    bad = [(n, _rel(res[True][1][n], g)) for n, g in res[False][1].items() if _rel(res[True][1][n], g) > 0.05]
+    assert not bad, bad
 
 
 def test_graphed_bert_step_matches_eager_without_dropout(gpu):
