@@ -449,6 +449,10 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
     constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
     constexpr int NS = bnr2 ? 3 : 2;          // per-channel sums kept
+    // GELU forward / backward epilogues (act 2 / 3) exist only in the plain-epilogue, non-persistent
+    // instantiations (the Linear GEMMs); compiling them out elsewhere keeps the register budget of
+    // the BN-epilogue and halo / streaming kernels untouched
+    constexpr bool GELU = EPI == EPI_PLAIN && !SHRED;
     float sm[NS][TN][4];
 #pragma unroll
     for (int k = 0; k < NS; ++k)
@@ -573,16 +577,18 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           float x1 = acc[j][i][e0 + 1] + bias[ce + 1];
           if (has_res) {
             const float r0 = __uint_as_float(rvA[b][q] << 16), r1 = __uint_as_float(rvA[b][q] & 0xffff0000u);
-            if (p.relu == 3) { x0 *= dgelu_erf(r0); x1 *= dgelu_erf(r1); }
+            if (GELU && p.relu == 3) { x0 *= dgelu_erf(r0); x1 *= dgelu_erf(r1); }
             else { x0 += r0; x1 += r1; }
           }
-          if (p.relu == 1) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
-          else if (p.relu == 2) {   // u (bf16) -> aux; out = gelu(u) as the separate kernel would
-            const unsigned uu = f2bf2(x0, x1);
-            av[q] = uu;
-            x0 = gelu_erf(__uint_as_float(uu << 16));
-            x1 = gelu_erf(__uint_as_float(uu & 0xffff0000u));
-          }
+          if constexpr (GELU) {
+            if (p.relu == 1) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
+            else if (p.relu == 2) {   // u (bf16) -> aux; out = gelu(u) as the separate kernel would
+              const unsigned uu = f2bf2(x0, x1);
+              av[q] = uu;
+              x0 = gelu_erf(__uint_as_float(uu << 16));
+              x1 = gelu_erf(__uint_as_float(uu & 0xffff0000u));
+            }
+          } else if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
           unsigned u = f2bf2(x0, x1);
           if constexpr (bnr) {
             const float xa = __uint_as_float(xvA[b][q] << 16), xb = __uint_as_float(xvA[b][q] & 0xffff0000u);
@@ -617,9 +623,11 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
         }
         if constexpr (VW == 8) *reinterpret_cast<uint4*>(out + o) = *reinterpret_cast<const uint4*>(ov);
         else *reinterpret_cast<uint2*>(out + o) = *reinterpret_cast<const uint2*>(ov);
-        if (p.relu == 2) {
-          if constexpr (VW == 8) *reinterpret_cast<uint4*>(p.aux + o) = *reinterpret_cast<const uint4*>(av);
-          else *reinterpret_cast<uint2*>(p.aux + o) = *reinterpret_cast<const uint2*>(av);
+        if constexpr (GELU) {
+          if (p.relu == 2) {
+            if constexpr (VW == 8) *reinterpret_cast<uint4*>(p.aux + o) = *reinterpret_cast<const uint4*>(av);
+            else *reinterpret_cast<uint2*>(p.aux + o) = *reinterpret_cast<const uint2*>(av);
+          }
         }
       }
     }
@@ -1074,6 +1082,196 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   } else {
     igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// LDS-DMA WGRAD kernel: dW[co][j] (+)= sum_m dy[m][co] * im2col(x)[m][j] with both operand tiles
+// moved global -> LDS by buffer_load ... lds (no VGPR round trip, no ds_write, no loader VALU on
+// the critical path) into the transposed-read images of the register-staged WGRAD kernel
+// (tr_off: [BK reduction rows][cols], read with ds_read_b64_tr_b16).  A DMA instruction writes
+// 1 KB of consecutive LDS (64 lanes x 16 B), so lane -> (row, chunk) is the INVERSE of the
+// image's swizzle: lane l of wave w, instruction i fills LDS chunk position P = (i*NW + w)*64 + l,
+// i.e. row P / CPR and logical chunk (P % CPR) ^ 2f(row), and fetches that chunk from global
+// (dy row for A; the im2col gather of x for B, whose per-row (n, p, q) walk advances by BK rows
+// per stage without divisions).  Double-buffered: the DMA of stage t+1 is in flight while stage t
+// is multiplied; one counted vmcnt + barrier before and one LDS barrier after each stage.
+// Epilogue and split-K semantics are those of igemm_kernel<MODE_WGRAD>.
+template <int COLS>
+__device__ __forceinline__ int tr_chunk_of_pos(int row, int pos) {   // inverse of tr_off's chunk swizzle
+  constexpr int RB = COLS * 2;
+  int f;
+  if constexpr (RB >= 256) f = (row & 3) | (((row >> 3) & 1) << 2);
+  else if constexpr (RB == 128) f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  else f = 0;
+  return pos ^ (2 * f);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(NT, 2) igemm_wgrad_dma_kernel(const IgemmParams p) {
+  constexpr int NW = NT / 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int RBA = BM * 2, RBB = BN * 2;
+  constexpr int A_BYTES = BK * RBA, B_BYTES = BK * RBB, STAGE = A_BYTES + B_BYTES;
+  constexpr int NIA = A_BYTES / 1024 / NW, NIB = B_BYTES / 1024 / NW;
+  constexpr int CPR_A = RBA / 16, CPR_B = RBB / 16;
+  static_assert(WM * WN == NW && NIA >= 1 && NIB >= 1 && NIA * NW * 1024 == A_BYTES && NIB * NW * 1024 == B_BYTES,
+                "wgrad_dma geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = lin / tiles_mn;
+  const int tl = lin - split * tiles_mn;
+  const int tile_n = tl % p.tiles_n, tile_m = tl / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = split * p.ksplit;
+  const int kend = min(p.gk, kbeg + p.ksplit);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+
+  // ---- A slots: dy rows (reduction index m), output-channel chunk
+  int a_off[NIA], a_row[NIA];
+  bool a_cok[NIA];
+#pragma unroll
+  for (int i = 0; i < NIA; ++i) {
+    const int P = (i * NW + wid) * 64 + lane;
+    const int row = P / CPR_A;
+    const int col = tr_chunk_of_pos<BM>(row, P % CPR_A) * 8;
+    a_row[i] = row;
+    a_cok[i] = m0 + col < p.gm;
+    a_off[i] = (kbeg + row) * p.K + m0 + col;
+  }
+  // ---- B slots: im2col rows, column chunk j = (r, s, c)
+  const int st = p.stride;
+  const int dq = BK % p.Q, dp = (BK / p.Q) % p.P, dn = BK / (p.P * p.Q);
+  const int WC = p.W * p.C;
+  const int g_dqs = dq * st, g_Qs = p.Q * st, g_dps = dp * st, g_Ps = p.P * st;
+  const int g_A0 = dq * st * p.C + dp * st * WC + dn * p.H * WC;
+  const int g_A1 = st * WC - p.Q * st * p.C;
+  const int g_A2 = p.H * WC - p.P * st * WC;
+  int b_off[NIB], b_ps[NIB], b_qs[NIB], b_row[NIB], b_r[NIB], b_s[NIB], b_col[NIB];
+  bool b_cok[NIB];
+#pragma unroll
+  for (int i = 0; i < NIB; ++i) {
+    const int P = (i * NW + wid) * 64 + lane;
+    const int row = P / CPR_B;
+    const int j = n0 + tr_chunk_of_pos<BN>(row, P % CPR_B) * 8;
+    b_row[i] = row;
+    b_cok[i] = j < p.gn;
+    const int jj = b_cok[i] ? j : 0;
+    const int c = jj % p.C, rs = jj / p.C;
+    b_s[i] = rs % p.S - p.pad;
+    b_r[i] = rs / p.S - p.pad;
+    b_col[i] = (b_r[i] * p.W + b_s[i]) * p.C + c;
+    const int m = min(kbeg + row, p.gk);
+    const int n = fdiv(m, p.fd_PQ);
+    const int rem = m - n * p.P * p.Q;
+    const int pp = fdiv(rem, p.fd_Q);
+    const int qq = rem - pp * p.Q;
+    b_ps[i] = pp * st;
+    b_qs[i] = qq * st;
+    b_off[i] = ((n * p.H + pp * st) * p.W + qq * st) * p.C;
+  }
+  int k0 = kbeg;
+  auto issue = [&](int buf) {
+    char* sA = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < NIA; ++i) {
+      const bool ok = a_cok[i] && k0 + a_row[i] < kend;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(sA + (i * NW + wid) * 1024),
+                                               16, ok ? (unsigned)a_off[i] * 2u : kOOB, 0, 0, 0);
+      a_off[i] += BK * p.K;
+    }
+#pragma unroll
+    for (int i = 0; i < NIB; ++i) {
+      const int yy = b_ps[i] + b_r[i], xx = b_qs[i] + b_s[i];
+      const bool ok = b_cok[i] && k0 + b_row[i] < kend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB,
+                                               (__attribute__((address_space(3))) void*)(sA + A_BYTES + (i * NW + wid) * 1024),
+                                               16, ok ? (unsigned)(b_off[i] + b_col[i]) * 2u : kOOB, 0, 0, 0);
+      int qs = b_qs[i] + g_dqs;
+      const bool c1 = qs >= g_Qs;
+      qs -= c1 ? g_Qs : 0;
+      int ps = b_ps[i] + g_dps + (c1 ? st : 0);
+      const bool c2 = ps >= g_Ps;
+      ps -= c2 ? g_Ps : 0;
+      b_qs[i] = qs;
+      b_ps[i] = ps;
+      b_off[i] += g_A0 + (c1 ? g_A1 : 0) + (c2 ? g_A2 : 0);
+    }
+    k0 += BK;
+  };
+
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
+  auto compute = [&](int buf) {
+    const char* sA = smem + buf * STAGE;
+    const char* sB = sA + A_BYTES;
+    const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int rowb = kk * 32 + 8 * g + q;
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wr * WTM + i * 16 + pc;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
+        fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wc * WTN + j * 16 + pc;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
+        fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    issue(0);
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < nk) { issue(buf ^ 1); wait_vm<NIA + NIB>(); } else wait_vm<0>();
+      lds_barrier();          // stage t landed in LDS for every wave
+      compute(buf);
+      lds_sync();             // WAR: every wave's ds_reads of buf retire before it is re-filled
+    }
+  }
+
+  const int fr = lane & 15, fq = lane >> 4;
+  float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc * WTN + j * 16 + fr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wr * WTM + i * 16 + fq * 4 + e;
+        if (row < p.gm && col < p.gn) {
+          float v = acc[i][j][e] * p.alpha;
+          float* dst = out + (size_t)row * p.gn + col;
+          if (p.accumulate) v += *dst;
+          *dst = v;
+        }
+      }
+    }
 }
 
 
@@ -2228,6 +2426,28 @@ static bool use_wgrad8(const IgemmParams& p) {
   return k == 2 || (p.R * p.S > 1 && p.gm <= 256);
 }
 
+// LDS-DMA WGRAD (igemm_wgrad_dma_kernel) for the 4-wave tiles; knob wgrad_dma: 0 = register-staged
+// igemm_kernel<MODE_WGRAD> (round 2), 1 = DMA kernel
+static Knob kn_wgrad_dma("wgrad_dma", 1);
+template <int BM, int BN>
+static bool launch_wgrad_dma(IgemmParams& p, hipStream_t st) {
+  if (!kn_wgrad_dma.get() || p.C % 8 != 0 || p.K % 8 != 0) return false;
+  p.tiles_m = ceil_div(p.gm, BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  const size_t smem = (size_t)2 * (BM + BN) * BK * 2;
+  auto kfn = &igemm_wgrad_dma_kernel<BM, BN, 2, 2>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p);
+  PCMP_LAUNCH_CHECK();
+  return true;
+}
+
 static void launch_wgrad8(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, 256);
   p.tiles_n = ceil_div(p.gn, 256);
@@ -2425,7 +2645,7 @@ static bool halo_dgrad_ovl(const IgemmParams& p) {
 static bool halo_geom(int mode, const IgemmParams& p, HaloGeom& g) {
   const int hk = kn_halo.get();
   if ((mode == MODE_FWD && !(hk & 1)) || (mode == MODE_DGRAD && !(hk & 6)) || mode == MODE_WGRAD || p.nsplit != 1 || p.stride != 1 || p.R != p.S || p.gn != 64 ||
-      p.grp != 0 || p.sub)
+      p.grp != 0 || p.sub || p.relu >= 2)
     return false;
   int CS, pad;
   if (mode == MODE_FWD) {
@@ -2518,7 +2738,7 @@ static void launch_halo(IgemmParams& p, hipStream_t st) {
 // 0: not used; 1: 128x128; 2: 128x64 (narrow outputs)
 static int use_stream(int mode, const IgemmParams& p) {
   const int mk = kn_stream_maxk.get();
-  if (mk <= 0 || mode == MODE_WGRAD || p.nsplit != 1) return 0;
+  if (mk <= 0 || mode == MODE_WGRAD || p.nsplit != 1 || p.relu >= 2) return 0;   // no GELU epilogue there
   if (mode == MODE_FWD && !kn_stream_fwd.get()) return 0;
   const int cin = mode == MODE_FWD ? p.C : p.K;
   if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK > mk || p.gm < 4096) return 0;
@@ -2617,6 +2837,14 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
       case 2: launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st); return;
       case 3: launch_dma<MODE, 256, 64, 4, 1, NT, 2>(p, st); return;
       default: break;
+    }
+  }
+  if constexpr (MODE == MODE_WGRAD) {
+    if (p.gm > 32) {
+      bool done;
+      if (p.gm <= 64) done = p.gn <= 64 ? launch_wgrad_dma<64, 64>(p, st) : launch_wgrad_dma<64, 128>(p, st);
+      else done = p.gn <= 64 ? launch_wgrad_dma<128, 64>(p, st) : launch_wgrad_dma<128, 128>(p, st);
+      if (done) return;
     }
   }
   // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)

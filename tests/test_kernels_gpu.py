@@ -619,6 +619,33 @@ def test_bn_group_reduction_in_kernel(gpu, mode):
         torch.testing.assert_close(pa.sum(0), pc.double().sum(0), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 96, 3, 1, 1), (2, 28, 28, 128, 256, 1, 2, 0),
+                                   (8, 7, 7, 512, 2048, 1, 1, 0), (3, 9, 9, 40, 72, 3, 2, 1),
+                                   (16, 8, 8, 64, 48, 1, 1, 0)])
+def test_wgrad_dma_kernel_matches_register_kernel(gpu, shape):
+    """LDS-DMA WGRAD (knob wgrad_dma, default on) == register-staged WGRAD == fp32 reference,
+    including tile tails, stride 2, 3x3 padding, split-K and accumulate."""
+    N, H, W, C, K, R, s, p = shape
+    torch.manual_seed(11)
+    ops = _ops()
+    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
+    dy = rnd(N, P, Q, K, dev=gpu)
+    x = rnd(N, H, W, C, dev=gpu)
+    outs = {}
+    for v in (0, 1):
+        out = torch.full((K, R, R, C), 0.25, device=gpu)
+        prev = ops.set_knob("wgrad_dma", v)
+        try:
+            ops.conv_wgrad(dy, x, out, R, R, s, p, True)
+        finally:
+            ops.set_knob("wgrad_dma", prev)
+        outs[v] = out
+    outr = torch.full((K, R, R, C), 0.25, device=gpu)
+    ref.conv_wgrad(dy, x, outr, R, R, s, p, True)
+    close(outs[1], outr, rtol=1e-2, atol=5e-2)
+    close(outs[1], outs[0], rtol=1e-3, atol=1e-2)
+
+
 @pytest.mark.parametrize("v", [1, 2])
 def test_wgrad8_kernel_knob(gpu, v):
     """The 8-wave 256x256 WGRAD kernel (off by default, knob wgrad8) == the fp32 reference."""
