@@ -103,7 +103,38 @@ struct IgemmParams {
   // fp32 accumulator tile is re-laid out through LDS so every epilogue load / store moves whole
   // cache lines (igemm_epilogue_coal); set by the host when the launch's LDS allocation covers it
   int coal;
+  // in-kernel split-K fixup (sk_cnt != null, nsplit > 1): every split writes its fp32 partial tile
+  // to the workspace (out), then takes a ticket on sk_cnt[tile]; the LAST arriver of a tile sums the
+  // nsplit partials in split order (bitwise independent of arrival order) and runs the regular
+  // epilogue into sk_out (FWD/DGRAD: bf16 [gm][gn]; WGRAD: fp32 [gm][gn], accumulate honoured) --
+  // no separate reduction / epilogue launch.  Counters come from counter_slots (zero on entry, reset
+  // by the last arriver).
+  int* sk_cnt;
+  void* sk_out;
 };
+
+// split-K ticket: publish this block's partial tile (every thread's stores drained, one agent-scope
+// release), count the arrival; returns true in every thread of the tile's last-arriving block, which
+// has then acquired the other splits' partials (cdna_hip_programming.md split-K seam recipe)
+__device__ __forceinline__ bool splitk_ticket(const IgemmParams& p, int tile) {
+  __shared__ int sk_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(p.sk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == p.nsplit - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(p.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sk_last = last;
+  }
+  __syncthreads();
+  return sk_last != 0;
+}
 
 constexpr int BK = 64;
 constexpr int NT = 256;
@@ -427,7 +458,8 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       }
     }
     if (p.nsplit > 1) {
-      // split-K forward (small-M inference shapes): raw fp32 partials, epilogue in the reduction
+      // split-K: raw fp32 partials; the epilogue runs in the reduction kernel or, with the in-kernel
+      // fixup, in the tile's last-arriving split
       float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -439,9 +471,28 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           if (n < p.gn) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[j][i];
         }
       }
-      return;
+      if constexpr (SHRED) {
+        return;   // persistent kernels never split (host-checked)
+      } else {
+        if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + n0 / BN)) return;
+        const float* ws0 = reinterpret_cast<const float*>(p.out);
+        const size_t slab = (size_t)p.gm * p.gn;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wr * WTM + i * 16 + fr;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n = n0 + chan(j);
+            if (m >= p.gm || n >= p.gn) continue;
+            f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int sp = 0; sp < p.nsplit; ++sp)
+              t += sp == split ? acc[j][i] : *reinterpret_cast<const f32x4*>(ws0 + sp * slab + (size_t)m * p.gn + n);
+            acc[j][i] = t;
+          }
+        }
+      }
     }
-    __bf16* out = reinterpret_cast<__bf16*>(p.out);
+    __bf16* out = reinterpret_cast<__bf16*>(p.nsplit > 1 ? p.sk_out : p.out);
     constexpr int VW = PAIR ? 8 : 4;          // channels per store
     constexpr int NV = TN * 4 / VW;           // stores per pixel row
     constexpr int NP = VW / 2;                // packed bf16 pairs per store
@@ -2117,17 +2168,29 @@ __global__ void __launch_bounds__(NT, 2) skinny_fwd_kernel(const IgemmParams p) 
   }
   // epilogue: lane holds channels n0 + 4 fq .. +3 of pixels m0 + 16 i + fr
   const int n = n0 + 4 * fq;
-  if (n >= p.gn) return;
+  const bool nok = n < p.gn;
   if (p.nsplit > 1) {
     float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + 16 * i + fr;
-      if (m < p.gm) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[i];
+      if (nok && m < p.gm) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[i];
     }
-    return;
+    if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + tile_n)) return;
+    const float* ws0 = reinterpret_cast<const float*>(p.out);
+    const size_t slab = (size_t)p.gm * p.gn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + 16 * i + fr;
+      if (!nok || m >= p.gm) continue;
+      f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < p.nsplit; ++sp)
+        t += sp == split ? acc[i] : *reinterpret_cast<const f32x4*>(ws0 + sp * slab + (size_t)m * p.gn + n);
+      acc[i] = t;
+    }
   }
-  __bf16* out = reinterpret_cast<__bf16*>(p.out);
+  if (!nok) return;
+  __bf16* out = reinterpret_cast<__bf16*>(p.nsplit > 1 ? p.sk_out : p.out);
   float bias[4] = {0.f, 0.f, 0.f, 0.f};
   if (p.bias) {
 #pragma unroll
@@ -2890,6 +2953,22 @@ static const char* plan_kind_name(int k) {
   }
 }
 
+int* counter_slots(int n, int device);
+// in-kernel split-K fixup (IgemmParams::sk_cnt) instead of the splitk_epilogue launch: 1 = on
+static Knob kn_sk_fixup("sk_fixup", 1);
+
+// arm the fixup for a FWD/DGRAD split launch writing bf16 `out`; false: use splitk_epilogue_kernel
+static bool arm_splitk_fixup(IgemmParams& p, void* out, int device) {
+  if (!kn_sk_fixup.get() || p.nsplit <= 1) return false;
+  // counter index = tile_m * tiles_n + tile_n over the launched kernel's tiles; the smallest tiles
+  // any FWD/DGRAD kernel uses are 32 x 64
+  int* cnt = counter_slots(ceil_div(p.gm, 32) * ceil_div(p.gn, 64), device);
+  if (!cnt) return false;
+  p.sk_cnt = cnt;
+  p.sk_out = out;
+  return true;
+}
+
 template <int MODE>
 static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
   const int kq = pl.kind == 6 ? 32 : BK;   // K granularity of the kernel
@@ -2901,9 +2980,11 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   p.ksplit = steps_per * kq;
   const __bf16* resid = p.resid;
   at::Tensor ws;
+  bool fixup = false;
   if (nsplit > 1) {
     ws = at::empty({(int64_t)nsplit, (int64_t)p.gm * p.gn}, fopts);
     p.out = ws.data_ptr();
+    fixup = arm_splitk_fixup(p, out, ws.get_device());
   } else {
     p.out = out;
   }
@@ -2916,7 +2997,7 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
     if constexpr (MODE == MODE_FWD) launch_skinny(p, st);
     else TORCH_CHECK(false, "skinny kernel is FWD only");
   } else dispatch<MODE>(p, st);
-  if (nsplit > 1) {
+  if (nsplit > 1 && !fixup) {
     const int64_t n = (int64_t)p.gm * p.gn;
     const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out,
@@ -3133,6 +3214,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.stats_cap = 0;
   p.grp = 0; p.grp_cnt = nullptr; p.grp_red = nullptr; p.grp_red2 = nullptr;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1; p.coal = 0;
+  p.sk_cnt = nullptr; p.sk_out = nullptr;
 }
 
 // x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
@@ -3208,7 +3290,9 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
     const int64_t n = (int64_t)p.gm * p.gn;
     auto ws = at::empty({(int64_t)nsplit, n}, x.options().dtype(at::kFloat));
     p.out = ws.data_ptr();
+    const bool fixup = arm_splitk_fixup(p, y.data_ptr(), x.get_device());
     dispatch<MODE_FWD>(p, st);
+    if (fixup) return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
     const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<__bf16>(y),
                        p.bias, p.resid, n, p.gn, nsplit, p.relu, p.aux);

@@ -95,6 +95,75 @@ __global__ void layernorm_fwd_kernel(const __bf16* __restrict__ x, const __bf16*
   if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
 }
 
+
+// LayerNorm forward for D = 256*KC (BERT: 768), the layout of ln_bwd_fused_kernel: lane owns
+// columns 256k + 4*lane (8-byte loads / stores, every lane busy), gamma / beta as float4, one row per
+// wave, 4 rows per block.  Same math and outputs as layernorm_fwd_kernel.
+template <int KC>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ r,
+                                                     const float* __restrict__ g, const float* __restrict__ b,
+                                                     __bf16* __restrict__ y, __bf16* __restrict__ xs,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out, int M,
+                                                     float eps, float p, uint64_t seed0, uint64_t off,
+                                                     const int64_t* __restrict__ salt) {
+  constexpr int D = 256 * KC;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[KC][4];
+  uint2 xv[KC], rv[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const size_t o = (size_t)row * D + 256 * k + 4 * lane;
+    xv[k] = *reinterpret_cast<const uint2*>(x + o);
+    if (r) rv[k] = *reinterpret_cast<const uint2*>(r + o);
+  }
+  const bool drop = p > 0.f;
+  const uint64_t seed = drop ? dropout_seed(seed0, salt) : 0;
+  const float scale = drop ? 1.f / (1.f - p) : 1.f;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    v[k][0] = __uint_as_float(xv[k].x << 16); v[k][1] = __uint_as_float(xv[k].x & 0xffff0000u);
+    v[k][2] = __uint_as_float(xv[k].y << 16); v[k][3] = __uint_as_float(xv[k].y & 0xffff0000u);
+    if (drop) {
+      const uint64_t i0 = off + (uint64_t)row * D + 256 * k + 4 * lane;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] = uniform01(seed, i0 + e) >= p ? v[k][e] * scale : 0.f;
+    }
+    if (xs) {
+      if (r) {
+        v[k][0] += __uint_as_float(rv[k].x << 16); v[k][1] += __uint_as_float(rv[k].x & 0xffff0000u);
+        v[k][2] += __uint_as_float(rv[k].y << 16); v[k][3] += __uint_as_float(rv[k].y & 0xffff0000u);
+      }
+      // keep the bf16-rounded sum so backward sees exactly the normalised values
+      const uint2 u = uint2{f2bf2(v[k][0], v[k][1]), f2bf2(v[k][2], v[k][3])};
+      *reinterpret_cast<uint2*>(xs + (size_t)row * D + 256 * k + 4 * lane) = u;
+      v[k][0] = __uint_as_float(u.x << 16); v[k][1] = __uint_as_float(u.x & 0xffff0000u);
+      v[k][2] = __uint_as_float(u.y << 16); v[k][3] = __uint_as_float(u.y & 0xffff0000u);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[k][e];
+  }
+  const float mu = warp_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < KC; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { const float d = v[k][e] - mu; q += d * d; }
+  const float rs = rsqrtf(warp_sum(q) * (1.f / D) + eps);
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const f32x4 g4 = *reinterpret_cast<const f32x4*>(g + 256 * k + 4 * lane);
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(b + 256 * k + 4 * lane);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[k][e] - mu) * rs * g4[e] + b4[e];
+    *reinterpret_cast<uint2*>(y + (size_t)row * D + 256 * k + 4 * lane) = uint2{f2bf2(o[0], o[1]), f2bf2(o[2], o[3])};
+  }
+  if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+}
+
 // dx = rstd * (gy - mean(gy) - xhat * mean(gy * xhat)), gy = dy * gamma; per-block partial
 // dgamma/dbeta into part[blockIdx][2][D]
 __global__ void layernorm_bwd_kernel(const __bf16* __restrict__ dy, const __bf16* __restrict__ xs,
@@ -923,6 +992,25 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<a
   at::Tensor xs = (hr || p > 0.0) ? at::empty_like(x) : x;
   auto f32 = x.options().dtype(at::kFloat);
   auto mean = at::empty({M}, f32), rstd = at::empty({M}, f32);
+  static const bool v1 = [] { const char* e = std::getenv("PCMP_LN_FWD_V1"); return e && e[0] == '1'; }();
+  if (!v1 && D % 256 == 0 && D <= 1024) {
+    const __bf16* rp = hr ? ptr<__bf16>(*r) : nullptr;
+    __bf16* xsp = (hr || p > 0.0) ? ptr<__bf16>(xs) : nullptr;
+    const int64_t* sp = p > 0.0 ? salt_ptr(salt) : nullptr;
+#define PCMP_LNF(KC)                                                                                            \
+  hipLaunchKernelGGL(ln_fwd_kernel<KC>, dim3(ceil_div(M, 4)), dim3(256), 0, cur_stream(), ptr<__bf16>(x), rp,   \
+                     ptr<float>(g), ptr<float>(b), ptr<__bf16>(y), xsp, ptr<float>(mean), ptr<float>(rstd), M,  \
+                     (float)eps, (float)p, (uint64_t)seed, (uint64_t)offset, sp)
+    switch (D / 256) {
+      case 1: PCMP_LNF(1); break;
+      case 2: PCMP_LNF(2); break;
+      case 3: PCMP_LNF(3); break;
+      default: PCMP_LNF(4); break;
+    }
+#undef PCMP_LNF
+    PCMP_LAUNCH_CHECK();
+    return {y, xs, mean, rstd};
+  }
   hipLaunchKernelGGL(layernorm_fwd_kernel, dim3(ceil_div(M, 4)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
                      hr ? ptr<__bf16>(*r) : nullptr, ptr<float>(g), ptr<float>(b), ptr<__bf16>(y),
                      (hr || p > 0.0) ? ptr<__bf16>(xs) : nullptr, ptr<float>(mean), ptr<float>(rstd), M, D, (float)eps,
@@ -932,11 +1020,21 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<a
 }
 
 // returns dx; dgamma/dbeta written (or accumulated) into the given fp32 tensors when defined
+std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tensor& xs, const at::Tensor& mean,
+                                            const at::Tensor& rstd, const at::Tensor& g,
+                                            const c10::optional<at::Tensor>& dg, const c10::optional<at::Tensor>& db,
+                                            const c10::optional<at::Tensor>& dbias, int64_t accmask, double p,
+                                            int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt);
+
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& xs, const at::Tensor& mean, const at::Tensor& rstd,
                          const at::Tensor& g, const c10::optional<at::Tensor>& dg, const c10::optional<at::Tensor>& db,
                          bool accumulate) {
-  auto dyc = dy.contiguous();
   const int D = xs.size(-1);
+  static const bool v1 = [] { const char* e = std::getenv("PCMP_LN_BWD_V1"); return e && e[0] == '1'; }();
+  if (!v1 && D % 256 == 0 && D <= 1024)   // the lane-dense kernel (no dropout, no bias output)
+    return layernorm_bwd_fused(dy, xs, mean, rstd, g, dg, db, c10::nullopt, accumulate ? 3 : 0, 0.0, 0, 0,
+                               c10::nullopt)[0];
+  auto dyc = dy.contiguous();
   const int M = xs.numel() / D;
   auto dx = at::empty_like(xs);
   static const int target_blocks = [] {   // PCMP_LN_BLOCKS overrides (A/B runs)

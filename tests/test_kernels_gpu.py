@@ -585,6 +585,46 @@ def test_small_m_plan_kinds_match_reference(gpu, kind):
         ops.set_knob("plan_force", -1)
 
 
+@pytest.mark.parametrize("kind", [1, 3, 4, 5, 6])
+def test_splitk_in_kernel_fixup(gpu, kind):
+    """Split-K GEMMs whose last-arriving split sums the partial tiles in split order and runs the
+    epilogue (knob sk_fixup=1, default) == the separate splitk_epilogue launch (sk_fixup=0) == the
+    fp32 reference, bitwise repeatable; FWD (bias / residual / ReLU) and a plain Linear DGRAD."""
+    torch.manual_seed(5)
+    ops = _ops()
+    prev_force = ops.set_knob("plan_force", kind)
+    try:
+        for (H, C, K, R, s, use_res) in [(7, 2048, 512, 1, 1, False), (7, 512, 2048, 1, 1, True),
+                                         (1, 2048, 1000, 1, 1, False), (14, 256, 256, 3, 1, False)]:
+            if kind in (1, 5) and R > 1:
+                continue
+            p = R // 2
+            x = rnd(1, H, H, C, dev=gpu)
+            w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+            bias = torch.randn(K, device=gpu)
+            Ho = (H + 2 * p - R) // s + 1
+            res = rnd(1, Ho, Ho, K, dev=gpu) if use_res else None
+            yr = ref.conv_fwd(x, w, s, p, bias, res, True, False)[0]
+            ys = {}
+            for fx in (0, 1):
+                prev = ops.set_knob("sk_fixup", fx)
+                try:
+                    ys[fx] = ops.conv_fwd(x, w, s, p, bias, res, True, False)[0]
+                    if fx:
+                        assert torch.equal(ys[fx], ops.conv_fwd(x, w, s, p, bias, res, True, False)[0])
+                finally:
+                    ops.set_knob("sk_fixup", prev)
+                close(ys[fx], yr)
+            close(ys[1], ys[0], 1e-2, 1e-2)
+    finally:
+        ops.set_knob("plan_force", prev_force)
+    # Linear DGRAD through the plain-GEMM planner (K-splits for the N = 768 outputs)
+    dy = rnd(4096, 1, 1, 768, dev=gpu)
+    wl = rnd(768, 1, 1, 3072, dev=gpu, scale=0.02)
+    dres = rnd(4096, 1, 1, 3072, dev=gpu)
+    close(ops.conv_dgrad(dy, wl, 1, 1, 1, 0, dres), ref.conv_dgrad(dy, wl, 1, 1, 1, 0, dres))
+
+
 @pytest.mark.parametrize("mode", ["fwd", "dgrad_bnr", "dgrad_bnr2"])
 def test_bn_group_reduction_in_kernel(gpu, mode):
     """The last-arriving block of each row-tile group sums the group's BN-statistics rows in fixed
