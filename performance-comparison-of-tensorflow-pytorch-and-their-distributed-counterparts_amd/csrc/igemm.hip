@@ -106,7 +106,8 @@ struct IgemmParams {
   // in-kernel split-K fixup (sk_cnt != null, nsplit > 1): every split writes its fp32 partial tile
   // to the workspace (out), then takes a ticket on sk_cnt[tile]; the LAST arriver of a tile sums the
   // nsplit partials in split order (bitwise independent of arrival order) and runs the regular
-  // epilogue into sk_out (FWD/DGRAD: bf16 [gm][gn]; WGRAD: fp32 [gm][gn], accumulate honoured) --
+  // epilogue into sk_out (FWD/DGRAD plain-epilogue launches, bf16 [gm][gn]; WGRAD keeps its separate
+  // deterministic split reduction) --
   // no separate reduction / epilogue launch.  Counters come from counter_slots (zero on entry, reset
   // by the last arriver).
   int* sk_cnt;
@@ -116,8 +117,13 @@ struct IgemmParams {
 // split-K ticket: publish this block's partial tile (every thread's stores drained, one agent-scope
 // release), count the arrival; returns true in every thread of the tile's last-arriving block, which
 // has then acquired the other splits' partials (cdna_hip_programming.md split-K seam recipe)
-__device__ __forceinline__ bool splitk_ticket(const IgemmParams& p, int tile) {
-  __shared__ int sk_last;
+// `flag` is one int of LDS: the kernel's dynamic LDS array (its stage buffers are dead here) or, in
+// a kernel without one, a static __shared__ int.  A static __shared__ object inside this inlined
+// helper would add static LDS to every kernel that calls it -- those kernels request the whole
+// 160 KB as dynamic LDS (hipFuncSetAttribute then fails) -- and a second __shared__ object beside
+// an LDS-DMA staging array can de-pipeline the K loop (cdna_hip_programming.md §5, item 4(a)).
+// The trailing barrier keeps every thread's read of the flag ahead of any later LDS reuse.
+__device__ __forceinline__ bool splitk_ticket(const IgemmParams& p, int tile, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -130,10 +136,12 @@ __device__ __forceinline__ bool splitk_ticket(const IgemmParams& p, int tile) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(p.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    sk_last = last;
+    *flag = last;
   }
   __syncthreads();
-  return sk_last != 0;
+  const bool last = *flag != 0;
+  __syncthreads();
+  return last;
 }
 
 constexpr int BK = 64;
@@ -474,7 +482,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
       if constexpr (SHRED) {
         return;   // persistent kernels never split (host-checked)
       } else {
-        if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + n0 / BN)) return;
+        if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + n0 / BN, reinterpret_cast<int*>(smem))) return;
         const float* ws0 = reinterpret_cast<const float*>(p.out);
         const size_t slab = (size_t)p.gm * p.gn;
 #pragma unroll
@@ -2176,7 +2184,8 @@ __global__ void __launch_bounds__(NT, 2) skinny_fwd_kernel(const IgemmParams p) 
       const int m = m0 + 16 * i + fr;
       if (nok && m < p.gm) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[i];
     }
-    if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + tile_n)) return;
+    __shared__ int sk_flag;   // this kernel has no dynamic LDS
+    if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + tile_n, &sk_flag)) return;
     const float* ws0 = reinterpret_cast<const float*>(p.out);
     const size_t slab = (size_t)p.gm * p.gn;
 #pragma unroll
@@ -2491,7 +2500,7 @@ static bool use_wgrad8(const IgemmParams& p) {
 
 // LDS-DMA WGRAD (igemm_wgrad_dma_kernel) for the 4-wave tiles; knob wgrad_dma: 0 = register-staged
 // igemm_kernel<MODE_WGRAD> (round 2), 1 = DMA kernel
-static Knob kn_wgrad_dma("wgrad_dma", 1);
+static Knob kn_wgrad_dma("wgrad_dma", 0);   // whole step: 0.1-0.3 % slower in 3/3 rounds (profiles/r3_wgrad_dma_step_ab.txt)
 template <int BM, int BN>
 static bool launch_wgrad_dma(IgemmParams& p, hipStream_t st) {
   if (!kn_wgrad_dma.get() || p.C % 8 != 0 || p.K % 8 != 0) return false;
@@ -2935,6 +2944,7 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
 // captured).  This replaces the round-1 hipBLASLt candidate for these GEMMs.
 static Knob kn_gemm_plan("gemm_plan", 1);   // 0 = default dispatch only, 1 = autotuned plan
 static Knob kn_plan_force("plan_force", -1); // tests: >= 0 restricts the candidates to that kind (uncached)
+static Knob kn_plan_nsplit("plan_nsplit", 0); // tests: >= 1 (with plan_force) also pins the split count
 
 struct GemmPlan {
   int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves),
@@ -2954,8 +2964,12 @@ static const char* plan_kind_name(int k) {
 }
 
 int* counter_slots(int n, int device);
-// in-kernel split-K fixup (IgemmParams::sk_cnt) instead of the splitk_epilogue launch: 1 = on
-static Knob kn_sk_fixup("sk_fixup", 1);
+// in-kernel split-K fixup (IgemmParams::sk_cnt) instead of the splitk_epilogue launch: 1 = on.
+// Measured off (profiles/r3_sk_fixup_ab.txt, 2 interleaved rounds): batch-1 inference p50 0.549-0.554
+// -> 0.659-0.672 ms, BERT-base 3,691-3,739 -> 3,615-3,644 samples/s, ResNet-50 unchanged.  The tile's
+// last arriver reads every other split's fp32 slab serially (up to 32 splits at batch 1), which the
+// separate epilogue launch spreads over the whole chip.
+static Knob kn_sk_fixup("sk_fixup", 0);
 
 // arm the fixup for a FWD/DGRAD split launch writing bf16 `out`; false: use splitk_epilogue_kernel
 static bool arm_splitk_fixup(IgemmParams& p, void* out, int device) {
@@ -3080,6 +3094,12 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
     for (const GemmPlan& c : cands)
       if (c.kind == force) f.push_back(c);
     if (!f.empty()) cands = f;
+    if (kn_plan_nsplit.get() > 0) {   // a pinned split count makes repeated forced calls bitwise comparable
+      f.clear();
+      for (const GemmPlan& c : cands)
+        if (c.nsplit == kn_plan_nsplit.get()) f.push_back(c);
+      if (!f.empty()) cands = f;
+    }
   }
   hipEvent_t e0, e1;
   PCMP_HIP_CHECK(hipEventCreate(&e0));
