@@ -112,7 +112,25 @@ struct IgemmParams {
   // by the last arriver).
   int* sk_cnt;
   void* sk_out;
+  // BatchNorm-backward fold (register-staged DGRAD / WGRAD of 1x1 stride-1 convs, fold_x != null):
+  // the dy operand is dz = k1*g + k2*x + k3, computed while the tile is staged from g (= a),
+  // x (= fold_x, same layout and extent as a) and per-channel coefficients fold_coef[3][K]
+  // (bn_bwd_finalize's k1 | k2 | k3), rounded to bf16 exactly as bn_bwd_apply rounds its output.
+  // The bn_bwd_apply pass that would write dz (and the two reads of it) never runs.
+  const __bf16* fold_x;
+  const float* fold_coef;
+  int fold_lds;   // DGRAD: byte offset of the block's LDS copy of fold_coef
 };
+
+// dz = k1*g + k2*x + k3 of one 16-B chunk (8 channels), bf16-rounded; 0 for an invalid row
+__device__ __forceinline__ uint4 fold_dz(uint4 g, uint4 x, const float* k1, const float* k2, const float* k3,
+                                         bool ok) {
+  const u16x8 gv = __builtin_bit_cast(u16x8, g), xv = __builtin_bit_cast(u16x8, x);
+  u16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = ok ? f2bf(k1[e] * bf2f(gv[e]) + k2[e] * bf2f(xv[e]) + k3[e]) : (unsigned short)0;
+  return __builtin_bit_cast(uint4, o);
+}
 
 // split-K ticket: publish this block's partial tile (every thread's stores drained, one agent-scope
 // release), count the arrival; returns true in every thread of the tile's last-arriving block, which
@@ -792,7 +810,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT>
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT, bool FOLD = false>
 __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -802,6 +820,8 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   constexpr int NVB = BN * BK / 8 / NTHR;
   static_assert(NVA >= 1 && NVB >= 1, "tile too small");
   static_assert(WM * WN == NTHR / 64, "one wave tile per wave");
+  static_assert(!FOLD || MODE == MODE_WGRAD || (MODE == MODE_DGRAD && UNIF), "fold: DGRAD (uniform walk) / WGRAD");
+  static_assert(!FOLD || NVA <= 32, "fold: row-valid bits");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -838,6 +858,11 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
 
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+  // BatchNorm-backward fold: x chunks beside the g chunks, row-valid bits, channel of the stage
+  uint4 rx[FOLD ? NVA : 1];
+  unsigned fold_ok = 0;
+  int fold_chan = 0;
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(FOLD ? p.fold_x : p.a, p.a_bytes);
 
   // ---- per-thread loader state ----------------------------------------------------------------
   const int lchunk = tid & 7;
@@ -941,6 +966,30 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
     }
   }
 
+  // fold coefficients: WGRAD -- the thread's 8 output channels m0 + wa_col .. +7 are fixed, so
+  // their k1/k2/k3 live in registers; DGRAD -- the stage's reduction channels change per K-step, so
+  // the block copies fold_coef [3][K] into LDS once (after every buffer the kernel uses)
+  float wk1[MODE == MODE_WGRAD && FOLD ? 8 : 1], wk2[MODE == MODE_WGRAD && FOLD ? 8 : 1],
+      wk3[MODE == MODE_WGRAD && FOLD ? 8 : 1];
+  if constexpr (FOLD) {
+    if constexpr (MODE == MODE_WGRAD) {
+      const int co = m0 + wa_col;
+      const bool cok = co < p.gm;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = cok ? *reinterpret_cast<const f32x4*>(p.fold_coef + co + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 b = cok ? *reinterpret_cast<const f32x4*>(p.fold_coef + p.gm + co + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 c = cok ? *reinterpret_cast<const f32x4*>(p.fold_coef + 2 * p.gm + co + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { wk1[4 * h + e] = a[e]; wk2[4 * h + e] = b[e]; wk3[4 * h + e] = c[e]; }
+      }
+    } else {
+      f32x4* dst = reinterpret_cast<f32x4*>(smem + p.fold_lds);
+      for (int i = tid; i < 3 * p.K / 4; i += NTHR) dst[i] = reinterpret_cast<const f32x4*>(p.fold_coef)[i];
+      __syncthreads();
+    }
+  }
+
   auto load_stage = [&](int kt) {
     const int k0 = kbeg + kt * BK;
     if constexpr (MODE != MODE_WGRAD) {
@@ -955,6 +1004,7 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         else tap = -(kr * p.Q + ks) * p.K;
       }
       const bool kok = UNIF ? true : (k0 + lchunk * 8 < kend);
+      if constexpr (FOLD) fold_chan = chan;   // 1x1: the reduction index is the channel
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
         bool ok;
@@ -973,6 +1023,10 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         ok = ok && kok;
         const unsigned voff = ok ? (unsigned)(a_off[i] + tap + chan) * 2u : kOOB;
         ra[i] = bload16(rsA, voff);
+        if constexpr (FOLD) {
+          rx[i] = bload16(rsX, voff);
+          fold_ok = ok ? (fold_ok | (1u << i)) : (fold_ok & ~(1u << i));
+        }
       }
       const int kk = k0 + lchunk * 8;
 #pragma unroll
@@ -1002,6 +1056,10 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         const int row = (tid + NTHR * i) / CPR_A;
         const bool ok = co_ok && k0 + row < kend;
         ra[i] = bload16(rsA, ok ? (unsigned)wa_off[i] * 2u : kOOB);
+        if constexpr (FOLD) {
+          rx[i] = bload16(rsX, ok ? (unsigned)wa_off[i] * 2u : kOOB);
+          fold_ok = ok ? (fold_ok | (1u << i)) : (fold_ok & ~(1u << i));
+        }
         wa_off[i] += BK * p.K;
       }
       // B': rows = m, cols = j=(r,s,c): im2col gather of x
@@ -1029,6 +1087,25 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   auto store_stage = [&](int buf) {
     char* sA = smem + buf * STAGE;
     char* sB = sA + A_BYTES;
+    if constexpr (FOLD) {
+      if constexpr (MODE == MODE_WGRAD) {
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) ra[i] = fold_dz(ra[i], rx[i], wk1, wk2, wk3, (fold_ok >> i) & 1u);
+      } else {
+        const float* cf = reinterpret_cast<const float*>(smem + p.fold_lds) + fold_chan;
+        float k1[8], k2[8], k3[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(cf + 4 * h);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(cf + p.K + 4 * h);
+          const f32x4 c = *reinterpret_cast<const f32x4*>(cf + 2 * p.K + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { k1[4 * h + e] = a[e]; k2[4 * h + e] = b[e]; k3[4 * h + e] = c[e]; }
+        }
+#pragma unroll
+        for (int i = 0; i < NVA; ++i) ra[i] = fold_dz(ra[i], rx[i], k1, k2, k3, (fold_ok >> i) & 1u);
+      }
+    }
     if constexpr (MODE != MODE_WGRAD) {
 #pragma unroll
       for (int i = 0; i < NVA; ++i)
@@ -2492,6 +2569,14 @@ static Knob kn_shortk_bm64("shortk_bm64", 0);   // FWD/DGRAD with gk <= N: 64x12
 // profiles/r2_knob_sweep.txt), so the 8-wave WGRAD is off by default.
 static Knob kn_wgrad8("wgrad8", 0);
 static Knob kn_wgrad_wgs("wgrad_wgs", 0);   // > 0: fixed split-K workgroup target (side-stream WGRADs)
+// dual BN-reduce DGRADs (EPI_BNR2) on the register-staged kernel: 128x128 tiles need 256 VGPRs and
+// spill 72 B per lane with that epilogue (48 B with the BatchNorm-backward fold); 128x64 tiles fit in
+// 192 VGPRs at the cost of one more read of the (short) A operand per extra column tile.  A/B knob.
+static Knob kn_bnr2_n64("bnr2_n64", 0);
+static bool use_bnr2_n64(int mode, const IgemmParams& p) {
+  return mode == MODE_DGRAD && p.bn_x2 && kn_bnr2_n64.get() && p.gm > 64 && p.gn > 64;
+}
+
 static bool use_wgrad8(const IgemmParams& p) {
   const int k = kn_wgrad8.get();
   if (!k || p.gm < 256 || p.gn < 256) return false;
@@ -2854,6 +2939,11 @@ static int wgrad_wide(const IgemmParams& p) {
 }
 
 static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
+  if (p.fold_x) {   // launch_fold's choice
+    BM = p.gm <= 64 ? 64 : 128;
+    BN = p.gn <= 64 ? 64 : 128;
+    return;
+  }
   if (use_wgrad8(p)) { BM = 256; BN = 256; return; }
   const int w = wgrad_wide(p);
   if (w == 1) { BM = 64; BN = 256; return; }
@@ -2877,6 +2967,7 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
 static int igemm_bm(int mode, const IgemmParams& p) {
+  if (p.fold_x) return 128;
   if (use_halo(mode, p)) return HALO_BM;
   if (use_stream(mode, p)) return 128;
   if (use_igemm8(mode, p)) return BM8;
@@ -2885,8 +2976,74 @@ static int igemm_bm(int mode, const IgemmParams& p) {
   return p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
 }
 
+// BatchNorm-backward fold launches (IgemmParams::fold_x): register-staged kernel only -- the LDS-DMA
+// kernels move operands straight into LDS with no register pass in which dz could be formed.
+template <int MODE, int BM, int BN, int WM, int WN>
+static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
+  static_assert(MODE != MODE_FWD, "fold: DGRAD / WGRAD");
+  p.tiles_m = ceil_div(p.gm, BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  p.coal = 0;
+  TORCH_CHECK(MODE == MODE_WGRAD || !p.stats || p.tiles_m <= p.stats_cap, "igemm fold: partial-stats buffer too small");
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
+  size_t smem = (size_t)(nk > 1 ? 2 : 1) * (BM + BN) * BK * 2;
+  if (MODE == MODE_DGRAD && p.bn_x) {
+    const int NS = p.bn_x2 ? 3 : 2;
+    smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
+  }
+  if (MODE == MODE_DGRAD) {   // the coefficient copy sits after every buffer the kernel uses
+    p.fold_lds = (int)((smem + 15) / 16 * 16);
+    smem = (size_t)p.fold_lds + (size_t)3 * p.K * sizeof(float);
+  }
+#define PCMP_FOLD_LAUNCH(U, E, D)                                                                     \
+  do {                                                                                              \
+    auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, U, E, D, NT, true>;                               \
+    static bool attr_ = false;                                                                      \
+    if (!attr_) {                                                                                   \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf_),                        \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
+      attr_ = true;                                                                                 \
+    }                                                                                               \
+    hipLaunchKernelGGL(kf_, dim3(grid), dim3(NT), smem, st, p);                                     \
+  } while (0)
+  if constexpr (MODE == MODE_DGRAD) {
+    TORCH_CHECK(p.bn_x, "igemm fold: DGRAD only with the fused BN-backward-reduce epilogue");
+    if (p.bn_x2) {
+      if (kn_epi_depth_bnr2.get() >= 4) PCMP_FOLD_LAUNCH(true, EPI_BNR2, 4); else PCMP_FOLD_LAUNCH(true, EPI_BNR2, 2);
+    } else {
+      if (kn_epi_depth.get() >= 4) PCMP_FOLD_LAUNCH(true, EPI_BNR, 4); else PCMP_FOLD_LAUNCH(true, EPI_BNR, 2);
+    }
+  } else {
+    PCMP_FOLD_LAUNCH(false, EPI_PLAIN, 2);
+  }
+#undef PCMP_FOLD_LAUNCH
+  PCMP_LAUNCH_CHECK();
+}
+
+template <int MODE>
+static void launch_fold(IgemmParams& p, hipStream_t st) {
+  if constexpr (MODE == MODE_DGRAD) {
+    TORCH_CHECK(p.R == 1 && p.S == 1 && p.stride == 1 && p.K % BK == 0 && p.nsplit == 1 && p.ksplit % BK == 0,
+                "igemm fold: DGRAD of a 1x1 stride-1 conv with K % 64 == 0, no split");
+    if (p.gn <= 64 || use_bnr2_n64(MODE, p)) launch_fold_cfg<MODE, 128, 64, 2, 2>(p, st);
+    else launch_fold_cfg<MODE, 128, 128, 2, 2>(p, st);
+  } else if constexpr (MODE == MODE_WGRAD) {
+    TORCH_CHECK(p.K % 8 == 0, "igemm fold: WGRAD needs K % 8 == 0");
+    // (no 256x64 wide tile here: with the fold's x chunks and coefficients it spills)
+    if (p.gm <= 64) {
+      if (p.gn <= 64) launch_fold_cfg<MODE, 64, 64, 2, 2>(p, st); else launch_fold_cfg<MODE, 64, 128, 2, 2>(p, st);
+    } else {
+      if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2>(p, st); else launch_fold_cfg<MODE, 128, 128, 2, 2>(p, st);
+    }
+  } else {
+    TORCH_CHECK(false, "igemm fold: FWD has no BatchNorm-backward operand");
+  }
+}
+
 template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
+  if (p.fold_x) { launch_fold<MODE>(p, st); return; }
   if constexpr (MODE != MODE_WGRAD) {
     if (use_halo(MODE, p)) { launch_halo<MODE>(p, st); return; }
     switch (use_stream(MODE, p)) {
@@ -2927,7 +3084,7 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
     if (p.gn <= 64) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
     else launch_cfg<MODE, 64, 128, 2, 2>(p, st);
   } else {
-    if (p.gn <= 64) launch_cfg<MODE, 128, 64, 2, 2>(p, st);
+    if (p.gn <= 64 || use_bnr2_n64(MODE, p)) launch_cfg<MODE, 128, 64, 2, 2>(p, st);
     else launch_cfg<MODE, 128, 128, 2, 2>(p, st);
   }
 }
@@ -3235,6 +3392,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.grp = 0; p.grp_cnt = nullptr; p.grp_red = nullptr; p.grp_red2 = nullptr;
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1; p.coal = 0;
   p.sk_cnt = nullptr; p.sk_out = nullptr;
+  p.fold_x = nullptr; p.fold_coef = nullptr; p.fold_lds = 0;
 }
 
 // x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
@@ -3358,6 +3516,8 @@ static at::Tensor transpose_taps(const at::Tensor& w, int r0, int s0, int rstep,
 // that class of output pixels (no MFMA work on structural zeros); their epilogues accumulate in
 // place into the residual buffer, which is CONSUMED (its memory becomes dx).
 struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (see IgemmParams)
+  const __bf16* fold_x = nullptr;     // BatchNorm-backward fold of dy (IgemmParams::fold_x)
+  const float* fold_coef = nullptr;
   const uint8_t* mbits = nullptr;
   const __bf16* mask = nullptr;
   const __bf16* x = nullptr;
@@ -3391,6 +3551,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     q.bn_x2 = bn->x2; q.bn_mean2 = bn->mean2; q.bn_istd2 = bn->istd2;
     q.bn_msc = bn->msc; q.bn_msh = bn->msh;
     q.bn_mbits = bn->mbits;
+    q.fold_x = bn->fold_x; q.fold_coef = bn->fold_coef;
   };
   auto fopts = dy.options().dtype(at::kFloat);
   const bool two = bn && bn->x2;
@@ -3412,6 +3573,8 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
       wt_full = *wt_given;
     }
   }
+  TORCH_CHECK(!bn || !bn->fold_x || (stride == 1 && R == 1 && S == 1 && K % BK == 0),
+              "conv_dgrad_bnr: the BatchNorm-backward fold needs a 1x1 stride-1 conv with K % 64 == 0");
   if (stride == 2) {
     struct Cls { int oph, opw, r0, s0, subR, subS, dH, dW; };
     std::vector<Cls> cls;
@@ -3566,7 +3729,11 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& mscale,
                                        const c10::optional<at::Tensor>& mshift,
                                        const c10::optional<at::Tensor>& wt,
-                                       const c10::optional<at::Tensor>& ymask_bits) {
+                                       const c10::optional<at::Tensor>& ymask_bits,
+                                       const c10::optional<at::Tensor>& fold_x,
+                                       const c10::optional<at::Tensor>& fold_coef) {
+  const bool fold = fold_x.has_value() && fold_x->defined();
+  TORCH_CHECK(!fold || dy.scalar_type() != at::kFloat, "conv_dgrad_bnr: the BatchNorm-backward fold is bf16 only");
   if (dy.scalar_type() == at::kFloat)
     return f32::conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2, mean2, invstd2, mscale,
                                mshift, ymask_bits);
@@ -3594,6 +3761,14 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
     TORCH_CHECK(mshift.has_value() && mshift->defined(), "conv_dgrad_bnr: mshift required with mscale");
     PCMP_CHECK_F32(*mscale); PCMP_CHECK_F32(*mshift);
     a.msc = ptr<float>(*mscale); a.msh = ptr<float>(*mshift);
+  }
+  if (fold) {
+    PCMP_CHECK_BF16(*fold_x); PCMP_CHECK_CONTIG(*fold_x);
+    TORCH_CHECK(fold_x->numel() == dy.numel(), "conv_dgrad_bnr: fold_x must have dy's shape");
+    TORCH_CHECK(fold_coef.has_value() && fold_coef->defined(), "conv_dgrad_bnr: fold_coef required with fold_x");
+    PCMP_CHECK_F32(*fold_coef); PCMP_CHECK_CONTIG(*fold_coef);
+    TORCH_CHECK(fold_coef->numel() == 3 * dy.size(-1), "conv_dgrad_bnr: fold_coef must be [3, K]");
+    a.fold_x = ptr<__bf16>(*fold_x); a.fold_coef = ptr<float>(*fold_coef);
   }
   return dgrad_impl(dy, w, H, W, stride, pad, resid, &a, wt);
 }
@@ -3702,7 +3877,10 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
 
 // dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
-                int64_t stride, int64_t pad, bool accumulate) {
+                int64_t stride, int64_t pad, bool accumulate, const c10::optional<at::Tensor>& fold_x,
+                const c10::optional<at::Tensor>& fold_coef) {
+  const bool fold = fold_x.has_value() && fold_x->defined();
+  TORCH_CHECK(!fold || dy.scalar_type() != at::kFloat, "conv_wgrad: the BatchNorm-backward fold is bf16 only");
   if (dy.scalar_type() == at::kFloat) return f32::conv_wgrad(dy, x, out, R, S, stride, pad, accumulate);
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(x);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
@@ -3714,6 +3892,14 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
   p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(x);
   p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(x);
+  if (fold) {   // dy operand = k1*g + k2*fold_x + k3 (dy passed as g)
+    PCMP_CHECK_BF16(*fold_x); PCMP_CHECK_CONTIG(*fold_x);
+    TORCH_CHECK(fold_x->numel() == dy.numel(), "conv_wgrad: fold_x must have dy's shape");
+    TORCH_CHECK(fold_coef.has_value() && fold_coef->defined(), "conv_wgrad: fold_coef required with fold_x");
+    PCMP_CHECK_F32(*fold_coef); PCMP_CHECK_CONTIG(*fold_coef);
+    TORCH_CHECK(fold_coef->numel() == 3 * (int64_t)K, "conv_wgrad: fold_coef must be [3, K]");
+    p.fold_x = ptr<__bf16>(*fold_x); p.fold_coef = ptr<float>(*fold_coef);
+  }
   int BM, BN;
   wgrad_tile(p, BM, BN);
   const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
@@ -3747,9 +3933,10 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::conv_dgrad);
   m.def("conv_dgrad_bnr(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? ymask, "
         "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2, Tensor? mscale, "
-        "Tensor? mshift, Tensor? wt=None, Tensor? ymask_bits=None) -> Tensor[]",
+        "Tensor? mshift, Tensor? wt=None, Tensor? ymask_bits=None, Tensor? fold_x=None, Tensor? fold_coef=None) -> Tensor[]",
         &pcmp::conv_dgrad_bnr);
-  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate) -> ()",
+  m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate, "
+        "Tensor? fold_x=None, Tensor? fold_coef=None) -> ()",
         &pcmp::conv_wgrad);
   m.def("linear_gelu_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor[]", &pcmp::linear_gelu_fwd);
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor? wt=None) -> Tensor", &pcmp::linear_dgrad_gelu);

@@ -89,12 +89,70 @@ def _conv_bn_eval(x, L, dtype, relu, resid=None):
     return K.conv_fwd(x, w, L.stride, L.pad, b, resid, relu, False)[0]
 
 
+class _Fold:
+    """The input gradient dz = k1*g + k2*x + k3 of a BatchNorm, left unmaterialised.
+
+    Its consumers -- the DGRAD and the WGRAD of the 1x1 stride-1 conv that produced the BN's input
+    -- form dz while they stage the operand (``fold_x`` / ``fold_coef`` of ``conv_dgrad_bnr`` and
+    ``conv_wgrad``), so the ``bn_bwd_apply`` pass (read g and x, write dz) and the two reads of dz
+    never run: on the DGRAD chain one extra read of x replaces three memory passes."""
+
+    __slots__ = ("g", "x", "coef")
+
+    def __init__(self, g, x, coef):
+        self.g, self.x, self.coef = g, x, coef
+
+
+def _fold_enabled() -> bool:
+    import os
+    return os.environ.get("PCMP_DZ_FOLD", "1") != "0"
+
+
+def _fold_min_rows() -> int:
+    import os
+    try:
+        return int(os.environ.get("PCMP_DZ_FOLD_MINROWS", "400000"))
+    except ValueError:
+        return 400000
+
+
+def _fold_ok(L, g) -> bool:
+    """Should the BN-backward output feeding conv ``L`` stay folded?  1x1 stride-1 convs whose channel
+    count fits the kernels' block-uniform tap walk; on the GPU only the bf16 HIP kernels fold, and
+    only for the memory-bound layer-1 shapes (>= PCMP_DZ_FOLD_MINROWS rows, default 400k: ResNet-50
+    layer 1 at B=256 has 802,816).  Per shape (tools/fold_micro.py, profiles/r3_fold_micro.txt) the
+    fold saves 33-107 us of the DGRAD chain there, and costs more than it saves from layer 2 on: the
+    folded GEMMs run on the register-staged kernel instead of the LDS-DMA ones, and the folded WGRAD
+    reads g and x (the side stream is not free: folding every shape cost 5 % of the step)."""
+    if not _fold_enabled() or not (L.R == 1 and L.S == 1 and L.stride == 1 and g.shape[-1] % 64 == 0):
+        return False
+    if g.is_cuda and (g.dtype != torch.bfloat16 or g.numel() // g.shape[-1] < _fold_min_rows()):
+        return False
+    return True
+
+
+def _mat(dh):
+    """Materialise a folded BN-backward output (paths whose kernel cannot fold)."""
+    if isinstance(dh, _Fold):
+        return K.bn_bwd_apply(dh.g, None, dh.x, dh.coef, None, None, False)[0]
+    return dh
+
+
+def _fold_args(dh):
+    """(dy, fold_x, fold_coef) for a DGRAD / WGRAD op."""
+    if isinstance(dh, _Fold):
+        return dh.g, dh.x, dh.coef
+    return dh, None, None
+
+
 def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=None, L2=None, want_g=False,
-                 parts=None):
+                 parts=None, fold=False):
     """Backward of one BN (or two BNs sharing the incoming gradient) -> list of dx (+g).
 
     ``parts`` = reduction partials already produced by a dgrad epilogue (``conv_dgrad_bnr``; then
-    ``dy`` is the masked gradient and ``ymask`` is None) -- skips the separate reduction pass."""
+    ``dy`` is the masked gradient and ``ymask`` is None) -- skips the separate reduction pass.
+    ``fold``: the first BN's dx is returned as a :class:`_Fold` (not applied); a second BN's dx is
+    still applied."""
     if parts is None:
         parts = K.bn_bwd_reduce(dy, ymask, x, mean, invstd, x2, mean2, invstd2)
     count = x.numel() // x.shape[-1]
@@ -120,6 +178,10 @@ def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=Non
         coef2 = finalize(parts[1], L2, mean2, invstd2, gout2, bout2, acc2 or bacc2)
         grads[L2.gamma] = fin2()
         grads[L2.beta] = bfin2()
+    if fold:
+        assert ymask is None and not want_g, "fold: dy must already be the masked gradient"
+        rest = list(K.bn_bwd_apply(dy, None, x2, coef2, None, None, False)) if x2 is not None else []
+        return [_Fold(dy, x, coef)] + rest, grads
     outs = K.bn_bwd_apply(dy, ymask, x, coef, x2, coef2, want_g)
     return outs, grads
 
@@ -133,12 +195,18 @@ def _bnr_ok(L):
 def _wgrad(L, dy, x, grads, fill=None):
     """Weight gradient of layer ``L`` (``fill(out, accumulate)`` overrides the plain conv WGRAD)."""
     w = L.weight
+    g, fx, fc = _fold_args(dy)
+    keep = (g, x) if fx is None else (g, x, fx, fc)
     if fill is None:
-        def fill(out, acc):
-            K.conv_wgrad(dy, x, out, L.R, L.S, L.stride, L.pad, acc)
-    if dy.is_cuda and w.requires_grad and getattr(w, "main_grad", None) is not None and _params.side_stream_enabled():
+        if fx is None:
+            def fill(out, acc):
+                K.conv_wgrad(g, x, out, L.R, L.S, L.stride, L.pad, acc)
+        else:
+            def fill(out, acc):
+                K.conv_wgrad(g, x, out, L.R, L.S, L.stride, L.pad, acc, fx, fc)
+    if g.is_cuda and w.requires_grad and getattr(w, "main_grad", None) is not None and _params.side_stream_enabled():
         # into the flat gradient buffer on the WGRAD stream, concurrent with this layer's DGRAD
-        _params.run_on_side(lambda: emit_grad(w, fill), (dy, x))
+        _params.run_on_side(lambda: emit_grad(w, fill), keep)
         grads[w] = None
         return
     grads[w] = emit_grad(w, fill)
@@ -226,9 +294,10 @@ def _link_prev_tail(x):
 def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
     """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue."""
     mask = None if prev.mbits is not None else x
-    r = K.conv_dgrad_bnr(dh, w, H, W, L.stride, L.pad, resid, mask, prev.c, prev.mean, prev.invstd,
-                         prev.cd, prev.meand, prev.invstdd, None, None, compute_weight_t(L.weight, dh.dtype),
-                         prev.mbits)
+    g, fx, fc = _fold_args(dh)
+    r = K.conv_dgrad_bnr(g, w, H, W, L.stride, L.pad, resid, mask, prev.c, prev.mean, prev.invstd,
+                         prev.cd, prev.meand, prev.invstdd, None, None, compute_weight_t(L.weight, g.dtype),
+                         prev.mbits, fx, fc)
     prev.parts = r[1:]
     prev.g_ptr = r[0].data_ptr()
     return r[0]
@@ -342,12 +411,15 @@ class ResidualBlockFn(torch.autograd.Function):
         parts = tail.parts if fused else None
         mask = None if fused else out          # a fused dout is already masked by out > 0
         tail.parts = None
+        # the last conv's dz stays folded into its DGRAD / WGRAD (needs the masked gradient dout)
+        fold_tail = fused and _fold_ok(Ll, dout)
         if down is not None:
-            outs, gr = _bn_backward(dout, mask, cs[-1], mean, invstd, Ll, cd, meand, invstdd, down, parts=parts)
+            outs, gr = _bn_backward(dout, mask, cs[-1], mean, invstd, Ll, cd, meand, invstdd, down, parts=parts,
+                                    fold=fold_tail)
             dh, dcd = outs[0], outs[1]
             gid = None
         elif fused:
-            outs, gr = _bn_backward(dout, None, cs[-1], mean, invstd, Ll, parts=parts)
+            outs, gr = _bn_backward(dout, None, cs[-1], mean, invstd, Ll, parts=parts, fold=fold_tail)
             dh, gid = outs[0], dout
             dcd = None
         else:
@@ -369,8 +441,9 @@ class ResidualBlockFn(torch.autograd.Function):
         for i in range(len(main) - 1, -1, -1):
             L = main[i]
             _wgrad(L, dh, acts[i], grads)
-            wcomp = compute_weight(L.weight, dh.dtype)
-            wt = compute_weight_t(L.weight, dh.dtype)
+            dtype = _fold_args(dh)[0].dtype
+            wcomp = compute_weight(L.weight, dtype)
+            wt = compute_weight_t(L.weight, dtype)
             if i > 0:
                 Hi, Wi = acts[i].shape[1], acts[i].shape[2]
                 m_prev, is_prev = stats[i - 1]
@@ -378,11 +451,16 @@ class ResidualBlockFn(torch.autograd.Function):
                     # dgrad epilogue applies the previous ReLU mask and emits that BN's reduction
                     # the ReLU mask of acts[i] = relu(cs[i-1] * scale + shift) is recomputed from cs[i-1]
                     sc_prev, sh_prev = ctx.coefs[i - 1]
-                    r = K.conv_dgrad_bnr(dh, wcomp, Hi, Wi, L.stride, L.pad, None, None, cs[i - 1],
-                                         m_prev, is_prev, None, None, None, sc_prev, sh_prev, wt)
-                    outs, gr = _bn_backward(r[0], None, cs[i - 1], m_prev, is_prev, main[i - 1], parts=r[1:])
+                    g, fx, fc = _fold_args(dh)
+                    r = K.conv_dgrad_bnr(g, wcomp, Hi, Wi, L.stride, L.pad, None, None, cs[i - 1],
+                                         m_prev, is_prev, None, None, None, sc_prev, sh_prev, wt, None, fx, fc)
+                    # conv1's dz folds when every consumer can: its WGRAD, and its DGRAD only on the
+                    # fused into-previous-block path
+                    fold = (i - 1 == 0 and _fold_ok(main[0], r[0]) and (not need_dx or prev0 is not None))
+                    outs, gr = _bn_backward(r[0], None, cs[i - 1], m_prev, is_prev, main[i - 1], parts=r[1:],
+                                            fold=fold)
                 else:
-                    da = K.conv_dgrad(dh, wcomp, Hi, Wi, L.stride, L.pad, None, wt)
+                    da = K.conv_dgrad(_mat(dh), wcomp, Hi, Wi, L.stride, L.pad, None, wt)
                     outs, gr = _bn_backward(da, acts[i], cs[i - 1], m_prev, is_prev, main[i - 1])
                 grads.update(gr)
                 dh = outs[0]
@@ -391,8 +469,8 @@ class ResidualBlockFn(torch.autograd.Function):
                 if down is not None:
                     _wgrad(down, dcd, acts[0], grads)
                     if need_dx:
-                        wd = compute_weight(down.weight, dh.dtype)
-                        wdt = compute_weight_t(down.weight, dh.dtype)
+                        wd = compute_weight(down.weight, dtype)
+                        wdt = compute_weight_t(down.weight, dtype)
                         if prev is not None:
                             if tfork is not None:
                                 t = _params.join_side(*tfork)
@@ -400,13 +478,13 @@ class ResidualBlockFn(torch.autograd.Function):
                                 t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt)
                             dx = _dgrad_into_prev(dh, wcomp, H, W, L, t, x, prev)
                         else:
-                            t = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, None, wt)
+                            t = K.conv_dgrad(_mat(dh), wcomp, H, W, L.stride, L.pad, None, wt)
                             dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t, wdt)
                 elif need_dx:
                     if prev is not None:
                         dx = _dgrad_into_prev(dh, wcomp, H, W, L, gid, x, prev)
                     else:
-                        dx = K.conv_dgrad(dh, wcomp, H, W, L.stride, L.pad, gid, wt)
+                        dx = K.conv_dgrad(_mat(dh), wcomp, H, W, L.stride, L.pad, gid, wt)
         # free saved activations early
         ctx.acts = ctx.cs = ctx.dstate = ctx.coefs = None
         ctx.prev_tail = ctx.tail = None

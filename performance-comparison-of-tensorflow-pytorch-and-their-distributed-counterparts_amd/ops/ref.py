@@ -49,8 +49,18 @@ def conv_dgrad(dy, w, H, W, stride, pad, resid=None, wt=None):
     return dx.to(dy.dtype).contiguous()
 
 
+def fold_dz(g, x, coef):
+    """dz = k1*g + k2*x + k3 per channel (bn_bwd_apply's output), rounded to g's dtype: the operand a
+    BatchNorm-backward fold (``fold_x`` / ``fold_coef``) forms while staging instead of reading it."""
+    C = g.shape[-1]
+    c = coef.float().reshape(3, C)
+    return (c[0] * g.float() + c[1] * x.float() + c[2]).to(g.dtype)
+
+
 def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None,
-                   mscale=None, mshift=None, wt=None, ymask_bits=None):
+                   mscale=None, mshift=None, wt=None, ymask_bits=None, fold_x=None, fold_coef=None):
+    if fold_x is not None:
+        dy = fold_dz(dy, fold_x, fold_coef)
     if ymask_bits is not None:                    # mask as bits (bn_apply mbits)
         ymask = unpack_mask_bits(ymask_bits, x.shape)
     elif ymask is None and mscale is not None:    # mask recomputed from x: relu(x * scale + shift) > 0
@@ -59,7 +69,9 @@ def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=N
     return [g] + bn_bwd_reduce(g, None, x, mean, invstd, x2, mean2, invstd2)
 
 
-def conv_wgrad(dy, x, out, R, S, stride, pad, accumulate):
+def conv_wgrad(dy, x, out, R, S, stride, pad, accumulate, fold_x=None, fold_coef=None):
+    if fold_x is not None:
+        dy = fold_dz(dy, fold_x, fold_coef)
     K, C = dy.shape[-1], x.shape[-1]
     dw = torch.nn.grad.conv2d_weight(_nchw(x), (K, C, R, S), _nchw(dy), stride=stride, padding=pad)
     dw = _nhwc(dw).reshape(out.shape).to(out.dtype)

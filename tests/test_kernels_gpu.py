@@ -976,3 +976,64 @@ def test_resize_image_matches_pil_bit_exact(gpu, hw, out):
         zr = ref.resize_image(x, out[0], out[1], mode, 8, 1 / 255.0, mean, std)
         assert z.dtype == dt and z.shape == (2, out[0], out[1], 8)
         close(z.cpu(), zr.cpu(), 1e-6, 1e-6)
+
+
+def _fold_operands(gpu, N, H, K, seed):
+    """g (masked BN-input gradient), x (BN input) and bn_bwd_finalize-style coefficients [3, K]."""
+    torch.manual_seed(seed)
+    g = rnd(N, H, H, K, dev=gpu)
+    x = rnd(N, H, H, K, dev=gpu, scale=2.0) + 0.5
+    coef = torch.stack([torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.05,
+                        torch.randn(K, device=gpu) * 0.1]).contiguous()
+    return g, x, coef
+
+
+@pytest.mark.parametrize("K,C,two", [(256, 64, False), (64, 256, False), (128, 512, True), (512, 128, False)])
+def test_dgrad_bnr_fold(gpu, K, C, two):
+    """BatchNorm-backward fold in the register-staged DGRAD: conv_dgrad_bnr(g, ..., fold_x=x,
+    fold_coef=coef) == conv_dgrad_bnr(bn_bwd_apply(g, x, coef), ...): the same bf16 operand dz is
+    formed while staging, so the masked gradient matches the unfolded path and the reference (1x1,
+    stride 1, odd row count for the tail tile)."""
+    ops = _ops()
+    N, H = 3, 29
+    g, x, coef = _fold_operands(gpu, N, H, K, 11)
+    w = rnd(K, 1, 1, C, dev=gpu, scale=(2.0 / K) ** 0.5)
+    xb, res = rnd(N, H, H, C, dev=gpu), rnd(N, H, H, C, dev=gpu)
+    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    x2 = mean2 = istd2 = None
+    if two:
+        x2, mean2, istd2 = rnd(N, H, H, C, dev=gpu), torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    bits = torch.randint(0, 256, (N * H * H * C // 8,), device=gpu, dtype=torch.uint8)
+    dz = ops.bn_bwd_apply(g, None, x, coef, None, None, False)[0]
+    close_el(dz, ref.fold_dz(g, x, coef), rel=1e-2, abs_frac=1e-3)   # fma contraction: 1-ulp bf16 differences
+    args = (w, H, H, 1, 0, res, None, xb, mean, istd, x2, mean2, istd2, None, None, None, bits)
+    rf = ops.conv_dgrad_bnr(g, *args, x, coef)
+    ru = ops.conv_dgrad_bnr(dz, *args)
+    rr = ref.conv_dgrad_bnr(g, *args, x, coef)
+    close_el(rf[0], ru[0])
+    close(rf[0], rr[0])
+    for pf, pu in zip(rf[1:], ru[1:]):
+        torch.testing.assert_close(pf.double().sum(0), pu.double().sum(0), rtol=2e-3, atol=2e-1)
+    rf2 = ops.conv_dgrad_bnr(g, *args, x, coef)
+    assert torch.equal(rf[0], rf2[0])
+
+
+@pytest.mark.parametrize("K,C", [(256, 64), (64, 256), (512, 128), (1024, 256)])
+def test_wgrad_fold(gpu, K, C):
+    """BatchNorm-backward fold in the WGRAD: conv_wgrad(g, x_in, ..., fold_x=x, fold_coef=coef) ==
+    conv_wgrad(bn_bwd_apply(g, x, coef), x_in, ...) (split-K and accumulate paths)."""
+    ops = _ops()
+    N, H = 8, 29
+    g, x, coef = _fold_operands(gpu, N, H, K, 12)
+    xin = rnd(N, H, H, C, dev=gpu)
+    dz = ops.bn_bwd_apply(g, None, x, coef, None, None, False)[0]
+    of = torch.empty(K, 1, 1, C, device=gpu)
+    ou = torch.empty_like(of)
+    orr = torch.empty_like(of)
+    ops.conv_wgrad(g, xin, of, 1, 1, 1, 0, False, x, coef)
+    ops.conv_wgrad(dz, xin, ou, 1, 1, 1, 0, False)
+    ref.conv_wgrad(g, xin, orr, 1, 1, 1, 0, False, x, coef)
+    close_el(of, ou, rel=1e-3, abs_frac=1e-4)
+    close(of, orr, rtol=1e-2, atol=1e-2)
+    ops.conv_wgrad(g, xin, of, 1, 1, 1, 0, True, x, coef)
+    close(of, 2 * ou, rtol=1e-2, atol=2e-2)
