@@ -2585,10 +2585,15 @@ static bool use_wgrad8(const IgemmParams& p) {
 
 // LDS-DMA WGRAD (igemm_wgrad_dma_kernel) for the 4-wave tiles; knob wgrad_dma: 0 = register-staged
 // igemm_kernel<MODE_WGRAD> (round 2), 1 = DMA kernel
-static Knob kn_wgrad_dma("wgrad_dma", 0);   // whole step: 0.1-0.3 % slower in 3/3 rounds (profiles/r3_wgrad_dma_step_ab.txt)
+// 2 = per-shape policy: the DMA kernel for the filters it wins in isolation (profiles/r3_wgrad_dma_shape_ab.txt:
+// every 3x3, 6-10 %, and the 1x1s with <= 64k reduction rows -- layers 3-4 at B=256 -- 4-8 %), the
+// register-staged one for the long-reduction 1x1s of layers 1-2 (1-6 % faster there)
+static Knob kn_wgrad_dma("wgrad_dma", 0);   // 1 (all) in the whole step: 0.1-0.3 % slower in 3/3 rounds (profiles/r3_wgrad_dma_step_ab.txt)
 template <int BM, int BN>
 static bool launch_wgrad_dma(IgemmParams& p, hipStream_t st) {
-  if (!kn_wgrad_dma.get() || p.C % 8 != 0 || p.K % 8 != 0) return false;
+  const int mode = kn_wgrad_dma.get();
+  if (!mode || p.C % 8 != 0 || p.K % 8 != 0) return false;
+  if (mode == 2 && p.R * p.S == 1 && p.gk > 65536) return false;
   p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
   const int grid = p.tiles_m * p.tiles_n * p.nsplit;
