@@ -2945,6 +2945,7 @@ static int wgrad_wide(const IgemmParams& p) {
 
 static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
   if (p.fold_x) {   // launch_fold's choice
+    if (wgrad_wide(p) == 1) { BM = 64; BN = 256; return; }
     BM = p.gm <= 64 ? 64 : 128;
     BN = p.gn <= 64 ? 64 : 128;
     return;
@@ -3035,8 +3036,10 @@ static void launch_fold(IgemmParams& p, hipStream_t st) {
     else launch_fold_cfg<MODE, 128, 128, 2, 2>(p, st);
   } else if constexpr (MODE == MODE_WGRAD) {
     TORCH_CHECK(p.K % 8 == 0, "igemm fold: WGRAD needs K % 8 == 0");
-    // (no 256x64 wide tile here: with the fold's x chunks and coefficients it spills)
-    if (p.gm <= 64) {
+    // (no 256x64 wide tile here: with the fold's x chunks and coefficients it spills; the 64x256
+    // stem tile reads the folded operand once instead of once per 128-column tile)
+    if (wgrad_wide(p) == 1) launch_fold_cfg<MODE, 64, 256, 1, 4>(p, st);
+    else if (p.gm <= 64) {
       if (p.gn <= 64) launch_fold_cfg<MODE, 64, 64, 2, 2>(p, st); else launch_fold_cfg<MODE, 64, 128, 2, 2>(p, st);
     } else {
       if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2>(p, st); else launch_fold_cfg<MODE, 128, 128, 2, 2>(p, st);

@@ -131,6 +131,11 @@ def _fold_ok(L, g) -> bool:
     return True
 
 
+def _stem_tail_mode(t) -> bool:
+    import os
+    return t.is_cuda and t.dtype == torch.bfloat16 and _fold_enabled() and os.environ.get("PCMP_STEM_TAIL", "1") != "0"
+
+
 def _mat(dh):
     """Materialise a folded BN-backward output (paths whose kernel cannot fold)."""
     if isinstance(dh, _Fold):
@@ -537,22 +542,37 @@ class StemFn(torch.autograd.Function):
         grads = {}
         # pooling backward + ReLU mask (recomputed from c) + BN-backward partials in one pass
         r = K.maxpool_bwd_bnr(dy.contiguous(), idx, c, mean, invstd, sc, sh, 3, 2, 1)
-        outs, gr = _bn_backward(r[0], None, c, mean, invstd, L, parts=r[1:])
+        # The stem's WGRAD is the last GEMM of the step: nothing on the compute stream can overlap it
+        # (profiles/r3_step_tail.txt: the compute stream idled ~315 us waiting for it on the side stream).
+        # Tail mode (PCMP_STEM_TAIL, default on, GPU): when the WGRAD is the BN gradient's only
+        # consumer (no input gradient), the BN-backward apply is folded into it, and it runs on the
+        # compute stream with its autotuned split count (a lone GEMM wants the whole chip, not the
+        # side stream's fixed 384-workgroup target).
+        tail = _stem_tail_mode(c) and not ctx.needs_input_grad[0] and c.shape[-1] % 8 == 0
+        outs, gr = _bn_backward(r[0], None, c, mean, invstd, L, parts=r[1:], fold=tail)
         grads.update(gr)
         dc = outs[0]
+        g_, fx, fc = _fold_args(dc)
         if ctx.s2d is False:
-            _wgrad(L, dc, x, grads)
+            if tail:
+                grads[L.weight] = emit_grad(L.weight, lambda out, acc: K.conv_wgrad(
+                    g_, x, out, L.R, L.S, L.stride, L.pad, acc, fx, fc))
+            else:
+                _wgrad(L, dc, x, grads)
         else:
             def fill(out, acc):
                 g4 = torch.empty(out.shape[0], 4, 4, S2D_CH, dtype=torch.float32, device=out.device)
-                K.conv_wgrad(dc, x, g4, 4, 4, 1, 0, False)
+                K.conv_wgrad(g_, x, g4, 4, 4, 1, 0, False, fx, fc)
                 g = s2d_weight_grad(g4)
                 if acc:
                     out[..., :4].add_(g)
                 else:
                     out[..., :4].copy_(g)
                     out[..., 4:].zero_()
-            _wgrad(L, dc, x, grads, fill)
+            if tail:
+                grads[L.weight] = emit_grad(L.weight, fill)
+            else:
+                _wgrad(L, dc, x, grads, fill)
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.s2d is False:

@@ -145,3 +145,59 @@ def test_training_is_bitwise_deterministic(gpu):
     a, b = run(), run()
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def test_stem_tail_mode_matches(gpu, monkeypatch):
+    """Stem backward tail mode (BN-backward apply folded into the stem WGRAD, run on the compute
+    stream with its autotuned split; PCMP_STEM_TAIL) changes only the stem conv's weight gradient,
+    and only by rounding; every other gradient and the loss are bitwise those of the default path."""
+    from pcmp.models.resnet import resnet50
+    torch.manual_seed(3)
+    m = resnet50(num_classes=10).to(gpu).train()
+    x = torch.rand(8, 3, 64, 64, device=gpu)
+    y = torch.randint(0, 10, (8,), device=gpu)
+    monkeypatch.setenv("PCMP_DZ_FOLD", "0")
+    res = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("PCMP_STEM_TAIL", v)
+        res[v] = _run(m, x, y, "hip")
+    (lb, gb), (lt, gt) = res["0"], res["1"]
+    assert torch.equal(lb, lt)
+    for n, g in gb.items():
+        if n == "stem.conv.weight":
+            assert _rel(gt[n], g) < 1e-2, (n, _rel(gt[n], g))
+        else:
+            assert torch.equal(gt[n], g), n
+
+
+@pytest.mark.parametrize("cfg", [(64, 64, 1), (256, 128, 2)])
+def test_bottleneck_dz_fold_matches(gpu, monkeypatch, cfg):
+    """BatchNorm-backward fold at every eligible conv (PCMP_DZ_FOLD_MINROWS=0) == the unfolded backward,
+    to bf16 rounding (the fold forms the same bf16 dz while staging; the folded GEMMs run on the
+    register-staged kernel).  Two chained bottlenecks exercise both folds: the second block's conv1
+    dz (its DGRAD goes into the first block's tail) and the first block's tail dz (its gradient
+    arrives masked from that fused DGRAD; with a downsample branch, the dual-BN case)."""
+    from pcmp.models.resnet import Bottleneck
+    torch.manual_seed(0)
+    cin, planes, stride = cfg
+    b1 = Bottleneck(cin, planes, stride).to(gpu).train()
+    b2 = Bottleneck(planes * 4, planes, 1).to(gpu).train()
+    x = (torch.randn(4, 28, 28, cin, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_(True)
+    g = torch.randn(4, 28 // stride, 28 // stride, planes * 4, device=gpu).to(torch.bfloat16)
+    params = list(b1.named_parameters()) + [("b2." + n, p) for n, p in b2.named_parameters()]
+    outs = {}
+    monkeypatch.setenv("PCMP_DZ_FOLD_MINROWS", "0")
+    for v in ("0", "1"):
+        monkeypatch.setenv("PCMP_DZ_FOLD", v)
+        for _, p in params:
+            p.grad = None
+        x.grad = None
+        y = b2(b1(x))
+        y.backward(g)
+        torch.cuda.synchronize()
+        outs[v] = (y.detach().clone(), x.grad.detach().clone(),
+                   {n: p.grad.detach().clone() for n, p in params if p.grad is not None})
+    assert torch.equal(outs["0"][0], outs["1"][0])
+    assert _rel(outs["1"][1], outs["0"][1]) < 2e-2
+    for n, gr in outs["0"][2].items():
+        assert _rel(outs["1"][2][n], gr) < 2e-2, (n, _rel(outs["1"][2][n], gr))
