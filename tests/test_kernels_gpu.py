@@ -1037,3 +1037,20 @@ def test_wgrad_fold(gpu, K, C):
     close(of, orr, rtol=1e-2, atol=1e-2)
     ops.conv_wgrad(g, xin, of, 1, 1, 1, 0, True, x, coef)
     close(of, 2 * ou, rtol=1e-2, atol=2e-2)
+
+
+def test_wgrad_fold_stem_tile(gpu):
+    """Folded WGRAD of the space-to-depth stem geometry (64 filters x 4x4 taps x 16 channels: the
+    64x256 tile) == WGRAD on the applied dz, and == the reference."""
+    ops = _ops()
+    N, P = 4, 28
+    g, x, coef = _fold_operands(gpu, N, P, 64, 13)
+    xin = rnd(N, P + 3, P + 3, 16, dev=gpu)
+    dz = ops.bn_bwd_apply(g, None, x, coef, None, None, False)[0]
+    of = torch.empty(64, 4, 4, 16, device=gpu)
+    ou, orr = torch.empty_like(of), torch.empty_like(of)
+    ops.conv_wgrad(g, xin, of, 4, 4, 1, 0, False, x, coef)
+    ops.conv_wgrad(dz, xin, ou, 4, 4, 1, 0, False)
+    ref.conv_wgrad(g, xin, orr, 4, 4, 1, 0, False, x, coef)
+    close_el(of, ou, rel=1e-3, abs_frac=1e-4)
+    close(of, orr, rtol=1e-2, atol=1e-2)
