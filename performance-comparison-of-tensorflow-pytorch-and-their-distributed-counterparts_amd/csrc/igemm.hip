@@ -119,8 +119,23 @@ struct IgemmParams {
   // The bn_bwd_apply pass that would write dz (and the two reads of it) never runs.
   const __bf16* fold_x;
   const float* fold_coef;
-  int fold_lds;   // DGRAD: byte offset of the block's LDS copy of fold_coef
+  int fold_lds;   // DGRAD / FWD: byte offset of the block's LDS copy of the fold coefficients
+  // BatchNorm-forward fold (act_sc != null): the activation operand -- FWD's A (x), WGRAD's B (x) --
+  // is y = relu(act_sc[c] * z + act_sh[c]) formed while staging from the pre-BN tensor z, instead
+  // of the bn_apply pass that would write y (register-staged kernel; FWD: 1x1 stride-1 convs)
+  const float* act_sc;
+  const float* act_sh;
 };
+
+// y = relu(a*z + b) of one 16-B chunk (8 channels), bf16-rounded as bn_apply rounds; 0 for an
+// invalid row / padding
+__device__ __forceinline__ uint4 fold_act(uint4 z, const float* a, const float* b, bool ok) {
+  const u16x8 zv = __builtin_bit_cast(u16x8, z);
+  u16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = ok ? f2bf(fmaxf(bf2f(zv[e]) * a[e] + b[e], 0.f)) : (unsigned short)0;
+  return __builtin_bit_cast(uint4, o);
+}
 
 // dz = k1*g + k2*x + k3 of one 16-B chunk (8 channels), bf16-rounded; 0 for an invalid row
 __device__ __forceinline__ uint4 fold_dz(uint4 g, uint4 x, const float* k1, const float* k2, const float* k3,
@@ -810,7 +825,10 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT, bool FOLD = false>
+// FOLD (bitmask): 1 = the A operand is formed while staging -- DGRAD / WGRAD: dz of the BatchNorm-
+// backward fold (fold_x, fold_coef); FWD: relu(a*z + b) of the BatchNorm-forward fold (act_sc/sh);
+// 2 = WGRAD's B operand (x) is relu(a*z + b) (act_sc / act_sh)
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT, int FOLD = 0>
 __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -820,8 +838,11 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   constexpr int NVB = BN * BK / 8 / NTHR;
   static_assert(NVA >= 1 && NVB >= 1, "tile too small");
   static_assert(WM * WN == NTHR / 64, "one wave tile per wave");
-  static_assert(!FOLD || MODE == MODE_WGRAD || (MODE == MODE_DGRAD && UNIF), "fold: DGRAD (uniform walk) / WGRAD");
-  static_assert(!FOLD || NVA <= 32, "fold: row-valid bits");
+  constexpr bool FA = (FOLD & 1) != 0, FB = (FOLD & 2) != 0;
+  constexpr bool FAX = FA && MODE != MODE_FWD;   // A fold reading a second tensor (dz = f(g, x))
+  static_assert(!FA || MODE == MODE_WGRAD || UNIF, "fold: FWD / DGRAD need the block-uniform walk");
+  static_assert(!FB || MODE == MODE_WGRAD, "fold: B-operand fold is WGRAD only");
+  static_assert(NVA <= 32 && NVB <= 32, "fold: row-valid bits");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -859,10 +880,10 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
   // BatchNorm-backward fold: x chunks beside the g chunks, row-valid bits, channel of the stage
-  uint4 rx[FOLD ? NVA : 1];
-  unsigned fold_ok = 0;
+  uint4 rx[FAX ? NVA : 1];
+  unsigned fold_ok = 0, fold_okb = 0;
   int fold_chan = 0;
-  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(FOLD ? p.fold_x : p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsX = make_rsrc(FAX ? p.fold_x : p.a, p.a_bytes);
 
   // ---- per-thread loader state ----------------------------------------------------------------
   const int lchunk = tid & 7;
@@ -969,9 +990,19 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   // fold coefficients: WGRAD -- the thread's 8 output channels m0 + wa_col .. +7 are fixed, so
   // their k1/k2/k3 live in registers; DGRAD -- the stage's reduction channels change per K-step, so
   // the block copies fold_coef [3][K] into LDS once (after every buffer the kernel uses)
-  float wk1[MODE == MODE_WGRAD && FOLD ? 8 : 1], wk2[MODE == MODE_WGRAD && FOLD ? 8 : 1],
-      wk3[MODE == MODE_WGRAD && FOLD ? 8 : 1];
-  if constexpr (FOLD) {
+  float wk1[MODE == MODE_WGRAD && FA ? 8 : 1], wk2[MODE == MODE_WGRAD && FA ? 8 : 1],
+      wk3[MODE == MODE_WGRAD && FA ? 8 : 1];
+  float bsc[FB ? 8 : 1], bsh[FB ? 8 : 1];   // WGRAD B fold: the thread's 8 input channels are fixed
+  if constexpr (FB) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 a = wb_ok ? *reinterpret_cast<const f32x4*>(p.act_sc + wb_c + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 b = wb_ok ? *reinterpret_cast<const f32x4*>(p.act_sh + wb_c + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bsc[4 * h + e] = a[e]; bsh[4 * h + e] = b[e]; }
+    }
+  }
+  if constexpr (FA) {
     if constexpr (MODE == MODE_WGRAD) {
       const int co = m0 + wa_col;
       const bool cok = co < p.gm;
@@ -983,9 +1014,15 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
 #pragma unroll
         for (int e = 0; e < 4; ++e) { wk1[4 * h + e] = a[e]; wk2[4 * h + e] = b[e]; wk3[4 * h + e] = c[e]; }
       }
-    } else {
+    } else if constexpr (MODE == MODE_DGRAD) {
       f32x4* dst = reinterpret_cast<f32x4*>(smem + p.fold_lds);
       for (int i = tid; i < 3 * p.K / 4; i += NTHR) dst[i] = reinterpret_cast<const f32x4*>(p.fold_coef)[i];
+      __syncthreads();
+    } else {   // FWD: [scale | shift] of the C input channels
+      f32x4* dst = reinterpret_cast<f32x4*>(smem + p.fold_lds);
+      const int nv = p.C / 4;
+      for (int i = tid; i < 2 * nv; i += NTHR)
+        dst[i] = i < nv ? reinterpret_cast<const f32x4*>(p.act_sc)[i] : reinterpret_cast<const f32x4*>(p.act_sh)[i - nv];
       __syncthreads();
     }
   }
@@ -1004,7 +1041,7 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         else tap = -(kr * p.Q + ks) * p.K;
       }
       const bool kok = UNIF ? true : (k0 + lchunk * 8 < kend);
-      if constexpr (FOLD) fold_chan = chan;   // 1x1: the reduction index is the channel
+      if constexpr (FA) fold_chan = chan;   // 1x1: the reduction index is the channel
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
         bool ok;
@@ -1023,8 +1060,8 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         ok = ok && kok;
         const unsigned voff = ok ? (unsigned)(a_off[i] + tap + chan) * 2u : kOOB;
         ra[i] = bload16(rsA, voff);
-        if constexpr (FOLD) {
-          rx[i] = bload16(rsX, voff);
+        if constexpr (FA) {
+          if constexpr (FAX) rx[i] = bload16(rsX, voff);
           fold_ok = ok ? (fold_ok | (1u << i)) : (fold_ok & ~(1u << i));
         }
       }
@@ -1056,7 +1093,7 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         const int row = (tid + NTHR * i) / CPR_A;
         const bool ok = co_ok && k0 + row < kend;
         ra[i] = bload16(rsA, ok ? (unsigned)wa_off[i] * 2u : kOOB);
-        if constexpr (FOLD) {
+        if constexpr (FA) {
           rx[i] = bload16(rsX, ok ? (unsigned)wa_off[i] * 2u : kOOB);
           fold_ok = ok ? (fold_ok | (1u << i)) : (fold_ok & ~(1u << i));
         }
@@ -1070,6 +1107,7 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         const int xx = wb_qs[i] - p.pad + wb_s;
         const bool ok = wb_ok && k0 + row < kend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
         rb[i] = bload16(rsB, ok ? (unsigned)(wb_off[i] + wb_coloff) * 2u : kOOB);
+        if constexpr (FB) fold_okb = ok ? (fold_okb | (1u << i)) : (fold_okb & ~(1u << i));
         // advance the walk by BK rows
         int qs = wb_qs[i] + wg_dqs;
         const bool c1 = qs >= wg_Qs;
@@ -1087,7 +1125,24 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   auto store_stage = [&](int buf) {
     char* sA = smem + buf * STAGE;
     char* sB = sA + A_BYTES;
-    if constexpr (FOLD) {
+    if constexpr (FB) {
+#pragma unroll
+      for (int i = 0; i < NVB; ++i) rb[i] = fold_act(rb[i], bsc, bsh, (fold_okb >> i) & 1u);
+    }
+    if constexpr (FA && MODE == MODE_FWD) {
+      const float* cf = reinterpret_cast<const float*>(smem + p.fold_lds) + fold_chan;
+      float a[8], b[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(cf + 4 * h);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(cf + p.C + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { a[4 * h + e] = u[e]; b[4 * h + e] = v[e]; }
+      }
+#pragma unroll
+      for (int i = 0; i < NVA; ++i) ra[i] = fold_act(ra[i], a, b, (fold_ok >> i) & 1u);
+    }
+    if constexpr (FAX) {
       if constexpr (MODE == MODE_WGRAD) {
 #pragma unroll
         for (int i = 0; i < NVA; ++i) ra[i] = fold_dz(ra[i], rx[i], wk1, wk2, wk3, (fold_ok >> i) & 1u);
@@ -2944,8 +2999,8 @@ static int wgrad_wide(const IgemmParams& p) {
 }
 
 static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
-  if (p.fold_x) {   // launch_fold's choice
-    if (wgrad_wide(p) == 1) { BM = 64; BN = 256; return; }
+  if (p.fold_x || p.act_sc) {   // launch_fold's choice
+    if (!p.act_sc && wgrad_wide(p) == 1) { BM = 64; BN = 256; return; }
     BM = p.gm <= 64 ? 64 : 128;
     BN = p.gn <= 64 ? 64 : 128;
     return;
@@ -2973,7 +3028,7 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)
 static int igemm_bm(int mode, const IgemmParams& p) {
-  if (p.fold_x) return 128;
+  if (p.fold_x || p.act_sc) return 128;
   if (use_halo(mode, p)) return HALO_BM;
   if (use_stream(mode, p)) return 128;
   if (use_igemm8(mode, p)) return BM8;
@@ -2982,11 +3037,10 @@ static int igemm_bm(int mode, const IgemmParams& p) {
   return p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
 }
 
-// BatchNorm-backward fold launches (IgemmParams::fold_x): register-staged kernel only -- the LDS-DMA
-// kernels move operands straight into LDS with no register pass in which dz could be formed.
-template <int MODE, int BM, int BN, int WM, int WN>
+// BatchNorm fold launches (IgemmParams::fold_x / act_sc): register-staged kernel only -- the LDS-DMA
+// kernels move operands straight into LDS with no register pass in which the operand could be formed.
+template <int MODE, int BM, int BN, int WM, int WN, int FOLD>
 static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
-  static_assert(MODE != MODE_FWD, "fold: DGRAD / WGRAD");
   p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
   p.coal = 0;
@@ -2994,17 +3048,18 @@ static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
   const int grid = p.tiles_m * p.tiles_n * p.nsplit;
   const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
   size_t smem = (size_t)(nk > 1 ? 2 : 1) * (BM + BN) * BK * 2;
-  if (MODE == MODE_DGRAD && p.bn_x) {
-    const int NS = p.bn_x2 ? 3 : 2;
+  const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
+  if (epi_red) {
+    const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
     smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
   }
-  if (MODE == MODE_DGRAD) {   // the coefficient copy sits after every buffer the kernel uses
+  if (MODE != MODE_WGRAD) {   // the coefficient copy sits after every buffer the kernel uses
     p.fold_lds = (int)((smem + 15) / 16 * 16);
-    smem = (size_t)p.fold_lds + (size_t)3 * p.K * sizeof(float);
+    smem = (size_t)p.fold_lds + (MODE == MODE_FWD ? (size_t)2 * p.C : (size_t)3 * p.K) * sizeof(float);
   }
 #define PCMP_FOLD_LAUNCH(U, E, D)                                                                     \
   do {                                                                                              \
-    auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, U, E, D, NT, true>;                               \
+    auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, U, E, D, NT, FOLD>;                               \
     static bool attr_ = false;                                                                      \
     if (!attr_) {                                                                                   \
       PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf_),                        \
@@ -3020,6 +3075,8 @@ static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
     } else {
       if (kn_epi_depth.get() >= 4) PCMP_FOLD_LAUNCH(true, EPI_BNR, 4); else PCMP_FOLD_LAUNCH(true, EPI_BNR, 2);
     }
+  } else if constexpr (MODE == MODE_FWD) {
+    if (p.stats) PCMP_FOLD_LAUNCH(true, EPI_STATS, 2); else PCMP_FOLD_LAUNCH(true, EPI_PLAIN, 2);
   } else {
     PCMP_FOLD_LAUNCH(false, EPI_PLAIN, 2);
   }
@@ -3030,28 +3087,42 @@ static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
 template <int MODE>
 static void launch_fold(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE == MODE_DGRAD) {
+    TORCH_CHECK(p.fold_x && !p.act_sc, "igemm fold: DGRAD folds only the BatchNorm-backward dz");
     TORCH_CHECK(p.R == 1 && p.S == 1 && p.stride == 1 && p.K % BK == 0 && p.nsplit == 1 && p.ksplit % BK == 0,
                 "igemm fold: DGRAD of a 1x1 stride-1 conv with K % 64 == 0, no split");
-    if (p.gn <= 64 || use_bnr2_n64(MODE, p)) launch_fold_cfg<MODE, 128, 64, 2, 2>(p, st);
-    else launch_fold_cfg<MODE, 128, 128, 2, 2>(p, st);
-  } else if constexpr (MODE == MODE_WGRAD) {
-    TORCH_CHECK(p.K % 8 == 0, "igemm fold: WGRAD needs K % 8 == 0");
+    if (p.gn <= 64 || use_bnr2_n64(MODE, p)) launch_fold_cfg<MODE, 128, 64, 2, 2, 1>(p, st);
+    else launch_fold_cfg<MODE, 128, 128, 2, 2, 1>(p, st);
+  } else if constexpr (MODE == MODE_FWD) {
+    TORCH_CHECK(p.act_sc && p.act_sh && !p.fold_x, "igemm fold: FWD folds only the BatchNorm-forward activation");
+    TORCH_CHECK(p.R == 1 && p.S == 1 && p.stride == 1 && p.C % BK == 0 && p.nsplit == 1 && p.ksplit % BK == 0,
+                "igemm fold: FWD of a 1x1 stride-1 conv with C % 64 == 0, no split");
+    if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2, 1>(p, st);
+    else launch_fold_cfg<MODE, 128, 128, 2, 2, 1>(p, st);
+  } else {
+    TORCH_CHECK(p.K % 8 == 0 && p.C % 8 == 0, "igemm fold: WGRAD needs K % 8 == 0 and C % 8 == 0");
+    if (p.act_sc) {   // B-operand fold (optionally with the A-operand dz fold): 128-row tiles
+      TORCH_CHECK(p.gm > 64, "igemm fold: WGRAD activation fold needs >= 65 output channels");
+      if (p.fold_x) {
+        if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2, 3>(p, st); else launch_fold_cfg<MODE, 128, 128, 2, 2, 3>(p, st);
+      } else {
+        if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2, 2>(p, st); else launch_fold_cfg<MODE, 128, 128, 2, 2, 2>(p, st);
+      }
+      return;
+    }
     // (no 256x64 wide tile here: with the fold's x chunks and coefficients it spills; the 64x256
     // stem tile reads the folded operand once instead of once per 128-column tile)
-    if (wgrad_wide(p) == 1) launch_fold_cfg<MODE, 64, 256, 1, 4>(p, st);
+    if (wgrad_wide(p) == 1) launch_fold_cfg<MODE, 64, 256, 1, 4, 1>(p, st);
     else if (p.gm <= 64) {
-      if (p.gn <= 64) launch_fold_cfg<MODE, 64, 64, 2, 2>(p, st); else launch_fold_cfg<MODE, 64, 128, 2, 2>(p, st);
+      if (p.gn <= 64) launch_fold_cfg<MODE, 64, 64, 2, 2, 1>(p, st); else launch_fold_cfg<MODE, 64, 128, 2, 2, 1>(p, st);
     } else {
-      if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2>(p, st); else launch_fold_cfg<MODE, 128, 128, 2, 2>(p, st);
+      if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2, 1>(p, st); else launch_fold_cfg<MODE, 128, 128, 2, 2, 1>(p, st);
     }
-  } else {
-    TORCH_CHECK(false, "igemm fold: FWD has no BatchNorm-backward operand");
   }
 }
 
 template <int MODE>
 static void dispatch(IgemmParams& p, hipStream_t st) {
-  if (p.fold_x) { launch_fold<MODE>(p, st); return; }
+  if (p.fold_x || p.act_sc) { launch_fold<MODE>(p, st); return; }
   if constexpr (MODE != MODE_WGRAD) {
     if (use_halo(MODE, p)) { launch_halo<MODE>(p, st); return; }
     switch (use_stream(MODE, p)) {
@@ -3353,7 +3424,8 @@ static void setup_bn_group(IgemmParams& p, int T, const at::Tensor& like, at::Te
 static unsigned tensor_bytes(const at::Tensor& t);
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  const c10::optional<at::Tensor>& bias,
-                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats);
+                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats,
+                                 const c10::optional<at::Tensor>& in_scale, const c10::optional<at::Tensor>& in_shift);
 
 // Timings of every planner candidate for one conv_fwd call (reports / kernel tuning): runs the
 // planner uncached with its log enabled.
@@ -3364,7 +3436,7 @@ std::vector<std::string> plan_candidates(const at::Tensor& x, const at::Tensor& 
   const int old = kn_plan_force.value.exchange(99);   // 99: no such kind -> every candidate, uncached
   g_plan_log = &log;
   try {
-    conv_fwd(x, w, stride, pad, bias, resid, relu, false);
+    conv_fwd(x, w, stride, pad, bias, resid, relu, false, c10::nullopt, c10::nullopt);
   } catch (...) {
     g_plan_log = nullptr;
     kn_plan_force.value.store(old);
@@ -3401,6 +3473,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1; p.coal = 0;
   p.sk_cnt = nullptr; p.sk_out = nullptr;
   p.fold_x = nullptr; p.fold_coef = nullptr; p.fold_lds = 0;
+  p.act_sc = nullptr; p.act_sh = nullptr;
 }
 
 // x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
@@ -3408,7 +3481,8 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
 // [tiles_m,2,K] f32 (returned).  act 2 (GELU) also returns the pre-activation u.
 static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                              const c10::optional<at::Tensor>& bias,
-                                             const c10::optional<at::Tensor>& resid, int act, bool want_stats) {
+                                             const c10::optional<at::Tensor>& resid, int act, bool want_stats,
+                                             const at::Tensor* in_scale = nullptr, const at::Tensor* in_shift = nullptr) {
   PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(x); PCMP_CHECK_CONTIG(w);
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: NHWC x and KRSC w expected");
@@ -3437,6 +3511,16 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
     p.aux = ptr<__bf16>(u);
   }
   p.ksplit = p.gk; p.nsplit = 1;
+  if (in_scale) {   // BatchNorm-forward fold: the operand is relu(in_scale * x + in_shift); set before
+                    // igemm_bm sizes the statistics rows (the fold picks its own tile)
+    TORCH_CHECK(in_shift && R == 1 && S == 1 && stride == 1 && C % BK == 0 && act != 2,
+                "conv_fwd: the input activation fold needs a 1x1 stride-1 conv with C % 64 == 0");
+    for (const at::Tensor* t : {in_scale, in_shift}) {
+      PCMP_CHECK_F32(*t); PCMP_CHECK_CONTIG(*t);
+      TORCH_CHECK(t->numel() == C, "conv_fwd: in_scale / in_shift must hold C values");
+    }
+    p.act_sc = ptr<float>(*in_scale); p.act_sh = ptr<float>(*in_shift);
+  }
   const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
   const int BNsel = p.gn <= 64 ? 64 : 128;
   at::Tensor stats, stats_red;
@@ -3447,6 +3531,11 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
     setup_bn_group(p, p.stats_cap, x, stats_red, nullptr);
   }
   auto st = cur_stream();
+  if (in_scale) {   // BatchNorm-forward fold (act_sc / act_sh set above)
+    dispatch<MODE_FWD>(p, st);
+    if (want_stats) return {y, stats_red.defined() ? stats_red : stats};
+    return {y};
+  }
   if (plain_gemm_eligible<MODE_FWD>(p)) {
     const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
     run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
@@ -3493,9 +3582,14 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
 
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  const c10::optional<at::Tensor>& bias,
-                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats) {
+                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats,
+                                 const c10::optional<at::Tensor>& in_scale, const c10::optional<at::Tensor>& in_shift) {
+  const bool fold = in_scale.has_value() && in_scale->defined();
+  TORCH_CHECK(!fold || (in_shift.has_value() && in_shift->defined()), "conv_fwd: in_shift required with in_scale");
+  TORCH_CHECK(!fold || x.scalar_type() != at::kFloat, "conv_fwd: the input activation fold is bf16 only");
   if (x.scalar_type() == at::kFloat) return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats);
-  return conv_fwd_impl(x, w, stride, pad, bias, resid, relu ? 1 : 0, want_stats);
+  return conv_fwd_impl(x, w, stride, pad, bias, resid, relu ? 1 : 0, want_stats, fold ? &*in_scale : nullptr,
+                       fold ? &*in_shift : nullptr);
 }
 
 // Linear y = gelu(x W^T + b) with the GELU fused into the GEMM epilogue: x [M, C], w [N, C] bf16
@@ -3886,8 +3980,11 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
 // dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
                 int64_t stride, int64_t pad, bool accumulate, const c10::optional<at::Tensor>& fold_x,
-                const c10::optional<at::Tensor>& fold_coef) {
+                const c10::optional<at::Tensor>& fold_coef, const c10::optional<at::Tensor>& in_scale,
+                const c10::optional<at::Tensor>& in_shift) {
   const bool fold = fold_x.has_value() && fold_x->defined();
+  const bool afold = in_scale.has_value() && in_scale->defined();
+  TORCH_CHECK(!afold || dy.scalar_type() != at::kFloat, "conv_wgrad: the input activation fold is bf16 only");
   TORCH_CHECK(!fold || dy.scalar_type() != at::kFloat, "conv_wgrad: the BatchNorm-backward fold is bf16 only");
   if (dy.scalar_type() == at::kFloat) return f32::conv_wgrad(dy, x, out, R, S, stride, pad, accumulate);
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(x);
@@ -3907,6 +4004,14 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
     PCMP_CHECK_F32(*fold_coef); PCMP_CHECK_CONTIG(*fold_coef);
     TORCH_CHECK(fold_coef->numel() == 3 * (int64_t)K, "conv_wgrad: fold_coef must be [3, K]");
     p.fold_x = ptr<__bf16>(*fold_x); p.fold_coef = ptr<float>(*fold_coef);
+  }
+  if (afold) {   // x operand = relu(in_scale * x + in_shift) (x passed as the pre-BN tensor)
+    TORCH_CHECK(in_shift.has_value() && in_shift->defined(), "conv_wgrad: in_shift required with in_scale");
+    for (const at::Tensor* t : {&*in_scale, &*in_shift}) {
+      PCMP_CHECK_F32(*t); PCMP_CHECK_CONTIG(*t);
+      TORCH_CHECK(t->numel() == C, "conv_wgrad: in_scale / in_shift must hold C values");
+    }
+    p.act_sc = ptr<float>(*in_scale); p.act_sh = ptr<float>(*in_shift);
   }
   int BM, BN;
   wgrad_tile(p, BM, BN);
@@ -3935,7 +4040,8 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("plan_candidates(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu) -> str[]",
         &pcmp::plan_candidates);
   m.def("wt_transpose_multi(Tensor src, Tensor(a!) dst, Tensor desc, int blocks) -> ()", &pcmp::wt_transpose_multi);
-  m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu, bool want_stats) -> Tensor[]",
+  m.def("conv_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu, bool want_stats, "
+        "Tensor? in_scale=None, Tensor? in_shift=None) -> Tensor[]",
         &pcmp::conv_fwd);
   m.def("conv_dgrad(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? wt=None) -> Tensor",
         &pcmp::conv_dgrad);
@@ -3944,7 +4050,7 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         "Tensor? mshift, Tensor? wt=None, Tensor? ymask_bits=None, Tensor? fold_x=None, Tensor? fold_coef=None) -> Tensor[]",
         &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate, "
-        "Tensor? fold_x=None, Tensor? fold_coef=None) -> ()",
+        "Tensor? fold_x=None, Tensor? fold_coef=None, Tensor? in_scale=None, Tensor? in_shift=None) -> ()",
         &pcmp::conv_wgrad);
   m.def("linear_gelu_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor[]", &pcmp::linear_gelu_fwd);
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor? wt=None) -> Tensor", &pcmp::linear_dgrad_gelu);

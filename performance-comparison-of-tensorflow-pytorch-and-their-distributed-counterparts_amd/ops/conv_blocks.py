@@ -45,13 +45,58 @@ def _global_sums(part, count, group):
     return s, count * dist.get_world_size(grp)
 
 
+class _Act:
+    """The activation y = relu(scale*z + shift) of a BatchNorm, left unmaterialised: the 1x1 conv that
+    consumes it forms y while staging its operand (``in_scale`` / ``in_shift`` of ``conv_fwd``, and
+    of that conv's ``conv_wgrad`` in backward), so the forward ``bn_apply`` pass (read z, write y)
+    never runs.  The ReLU mask the backward needs is recomputed from z already."""
+
+    __slots__ = ("z", "scale", "shift")
+
+    def __init__(self, z, scale, shift):
+        self.z, self.scale, self.shift = z, scale, shift
+
+    @property
+    def shape(self):
+        return self.z.shape
+
+
+def _act_fold_ok(L, z) -> bool:
+    """Should relu(BN(z)) feeding conv ``L`` stay folded?  GPU bf16, 1x1 stride-1 convs with C % 64 == 0,
+    and only the memory-bound shapes whose conv already runs on the register-staged kernel (short
+    reductions of layers 1-2: >= PCMP_ACT_FOLD_MINROWS rows, default 150k; ResNet-50 layer 2 at
+    B=256 has 200,704)."""
+    import os
+    if os.environ.get("PCMP_ACT_FOLD", "1") == "0" or not (z.is_cuda and z.dtype == torch.bfloat16):
+        return False
+    if not (L.R == 1 and L.S == 1 and L.stride == 1 and z.shape[-1] % 64 == 0 and z.shape[-1] <= 128):
+        return False
+    try:
+        minrows = int(os.environ.get("PCMP_ACT_FOLD_MINROWS", "150000"))
+    except ValueError:
+        minrows = 150000
+    return z.numel() // z.shape[-1] >= minrows
+
+
+def _act_args(x):
+    """(x, in_scale, in_shift) for a conv_fwd / conv_wgrad operand."""
+    if isinstance(x, _Act):
+        return x.z, x.scale, x.shift
+    return x, None, None
+
+
 def _conv_bn_train(x, L, dtype, w=None, stride=None, pad=None):
     """conv (+stats) -> finalize.  Returns c, mean, invstd, scale, shift.  (``w``/``stride``/``pad``
-    override the layer's: the space-to-depth stem.)"""
+    override the layer's: the space-to-depth stem; ``x`` may be an :class:`_Act`.)"""
     if w is None:
         w = compute_weight(L.weight, dtype)
-    c, part = K.conv_fwd(x, w, L.stride if stride is None else stride, L.pad if pad is None else pad, None, None,
-                         False, True)
+    xz, isc, ish = _act_args(x)
+    if isc is None:
+        c, part = K.conv_fwd(xz, w, L.stride if stride is None else stride, L.pad if pad is None else pad, None, None,
+                             False, True)
+    else:
+        c, part = K.conv_fwd(xz, w, L.stride if stride is None else stride, L.pad if pad is None else pad, None, None,
+                             False, True, isc, ish)
     count = c.numel() // c.shape[-1]
     grp = _sync_group(L)
     if grp is not None:   # SyncBN: batch statistics over all ranks
@@ -201,14 +246,15 @@ def _wgrad(L, dy, x, grads, fill=None):
     """Weight gradient of layer ``L`` (``fill(out, accumulate)`` overrides the plain conv WGRAD)."""
     w = L.weight
     g, fx, fc = _fold_args(dy)
-    keep = (g, x) if fx is None else (g, x, fx, fc)
+    xz, isc, ish = _act_args(x)
+    keep = tuple(t for t in (g, xz, fx, fc, isc, ish) if t is not None)
     if fill is None:
-        if fx is None:
+        if fx is None and isc is None:
             def fill(out, acc):
-                K.conv_wgrad(g, x, out, L.R, L.S, L.stride, L.pad, acc)
+                K.conv_wgrad(g, xz, out, L.R, L.S, L.stride, L.pad, acc)
         else:
             def fill(out, acc):
-                K.conv_wgrad(g, x, out, L.R, L.S, L.stride, L.pad, acc, fx, fc)
+                K.conv_wgrad(g, xz, out, L.R, L.S, L.stride, L.pad, acc, fx, fc, isc, ish)
     if g.is_cuda and w.requires_grad and getattr(w, "main_grad", None) is not None and _params.side_stream_enabled():
         # into the flat gradient buffer on the WGRAD stream, concurrent with this layer's DGRAD
         _params.run_on_side(lambda: emit_grad(w, fill), keep)
@@ -364,7 +410,10 @@ class ResidualBlockFn(torch.autograd.Function):
             stats.append((mean, invstd))
             coefs.append((sc, sh))
             if i < len(main) - 1:
-                h = K.bn_apply(c, sc, sh, None, None, None, True)
+                if _act_fold_ok(main[i + 1], c):   # the next (1x1) conv forms relu(BN(c)) itself
+                    h = _Act(c, sc, sh)
+                else:
+                    h = K.bn_apply(c, sc, sh, None, None, None, True)
                 acts.append(h)
             else:
                 last = (sc, sh)
@@ -466,7 +515,10 @@ class ResidualBlockFn(torch.autograd.Function):
                                             fold=fold)
                 else:
                     da = K.conv_dgrad(_mat(dh), wcomp, Hi, Wi, L.stride, L.pad, None, wt)
-                    outs, gr = _bn_backward(da, acts[i], cs[i - 1], m_prev, is_prev, main[i - 1])
+                    ai = acts[i]
+                    if isinstance(ai, _Act):   # (never for ResNet v1.5: folded inputs feed 1x1 stride-1 convs)
+                        ai = K.bn_apply(ai.z, ai.scale, ai.shift, None, None, None, True)
+                    outs, gr = _bn_backward(da, ai, cs[i - 1], m_prev, is_prev, main[i - 1])
                 grads.update(gr)
                 dh = outs[0]
             else:

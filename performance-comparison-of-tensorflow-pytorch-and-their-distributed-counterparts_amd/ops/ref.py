@@ -20,7 +20,15 @@ def _nhwc(x):
 
 
 # ------------------------------------------------------------------------------ convolution
-def conv_fwd(x, w, stride, pad, bias=None, resid=None, relu=False, want_stats=False):
+def fold_act(z, scale, shift):
+    """y = relu(scale*z + shift) per channel (bn_apply's output), rounded to z's dtype: the operand a
+    BatchNorm-forward fold (``in_scale`` / ``in_shift``) forms while staging instead of reading it."""
+    return torch.relu(z.float() * scale.float() + shift.float()).to(z.dtype)
+
+
+def conv_fwd(x, w, stride, pad, bias=None, resid=None, relu=False, want_stats=False, in_scale=None, in_shift=None):
+    if in_scale is not None:
+        x = fold_act(x, in_scale, in_shift)
     y = _nhwc(F.conv2d(_nchw(x), _nchw(w), None, stride, pad))
     if bias is not None:
         y = y + bias.float()
@@ -69,9 +77,11 @@ def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=N
     return [g] + bn_bwd_reduce(g, None, x, mean, invstd, x2, mean2, invstd2)
 
 
-def conv_wgrad(dy, x, out, R, S, stride, pad, accumulate, fold_x=None, fold_coef=None):
+def conv_wgrad(dy, x, out, R, S, stride, pad, accumulate, fold_x=None, fold_coef=None, in_scale=None, in_shift=None):
     if fold_x is not None:
         dy = fold_dz(dy, fold_x, fold_coef)
+    if in_scale is not None:
+        x = fold_act(x, in_scale, in_shift)
     K, C = dy.shape[-1], x.shape[-1]
     dw = torch.nn.grad.conv2d_weight(_nchw(x), (K, C, R, S), _nchw(dy), stride=stride, padding=pad)
     dw = _nhwc(dw).reshape(out.shape).to(out.dtype)

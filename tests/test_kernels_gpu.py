@@ -1054,3 +1054,45 @@ def test_wgrad_fold_stem_tile(gpu):
     ref.conv_wgrad(g, xin, orr, 4, 4, 1, 0, False, x, coef)
     close_el(of, ou, rel=1e-3, abs_frac=1e-4)
     close(of, orr, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("C,K", [(64, 256), (128, 512), (128, 64)])
+def test_conv_fwd_act_fold(gpu, C, K):
+    """BatchNorm-forward fold: conv_fwd(z, ..., in_scale, in_shift) == conv_fwd(bn_apply(z, relu)):
+    the same bf16 operand relu(scale*z + shift) is formed while staging; BN statistics too."""
+    torch.manual_seed(21)
+    ops = _ops()
+    N, H = 3, 29
+    z = rnd(N, H, H, C, dev=gpu, scale=2.0)
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.5
+    w = rnd(K, 1, 1, C, dev=gpu, scale=(2.0 / C) ** 0.5)
+    y = ops.bn_apply(z, sc, sh, None, None, None, True)
+    close_el(y, ref.fold_act(z, sc, sh), rel=1e-2, abs_frac=1e-3)
+    rf = ops.conv_fwd(z, w, 1, 0, None, None, False, True, sc, sh)
+    ru = ops.conv_fwd(y, w, 1, 0, None, None, False, True)
+    rr = ref.conv_fwd(z, w, 1, 0, None, None, False, True, sc, sh)
+    close_el(rf[0], ru[0])
+    close(rf[0], rr[0])
+    torch.testing.assert_close(rf[1].double().sum(0), ru[1].double().sum(0), rtol=2e-3, atol=5e-1)
+
+
+@pytest.mark.parametrize("dzfold", [False, True])
+@pytest.mark.parametrize("K,C", [(256, 64), (512, 128)])
+def test_wgrad_act_fold(gpu, K, C, dzfold):
+    """WGRAD with the x operand folded (relu(scale*z + shift)), alone and together with the dz fold of
+    the dy operand == WGRAD on the materialised operands."""
+    ops = _ops()
+    N, H = 8, 29
+    g, x, coef = _fold_operands(gpu, N, H, K, 14)
+    z = rnd(N, H, H, C, dev=gpu, scale=2.0)
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.5
+    y = ops.bn_apply(z, sc, sh, None, None, None, True)
+    dz = ops.bn_bwd_apply(g, None, x, coef, None, None, False)[0]
+    of = torch.empty(K, 1, 1, C, device=gpu)
+    ou = torch.empty_like(of)
+    if dzfold:
+        ops.conv_wgrad(g, z, of, 1, 1, 1, 0, False, x, coef, sc, sh)
+    else:
+        ops.conv_wgrad(dz, z, of, 1, 1, 1, 0, False, None, None, sc, sh)
+    ops.conv_wgrad(dz, y, ou, 1, 1, 1, 0, False)
+    close_el(of, ou, rel=1e-3, abs_frac=1e-4)

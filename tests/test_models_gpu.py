@@ -187,8 +187,10 @@ def test_bottleneck_dz_fold_matches(gpu, monkeypatch, cfg):
     params = list(b1.named_parameters()) + [("b2." + n, p) for n, p in b2.named_parameters()]
     outs = {}
     monkeypatch.setenv("PCMP_DZ_FOLD_MINROWS", "0")
-    for v in ("0", "1"):
+    monkeypatch.setenv("PCMP_ACT_FOLD_MINROWS", "0")
+    for v in ("0", "1"):   # both folds: backward dz and forward relu(BN(z)) into the 1x1 convs
         monkeypatch.setenv("PCMP_DZ_FOLD", v)
+        monkeypatch.setenv("PCMP_ACT_FOLD", v)
         for _, p in params:
             p.grad = None
         x.grad = None
@@ -197,7 +199,7 @@ def test_bottleneck_dz_fold_matches(gpu, monkeypatch, cfg):
         torch.cuda.synchronize()
         outs[v] = (y.detach().clone(), x.grad.detach().clone(),
                    {n: p.grad.detach().clone() for n, p in params if p.grad is not None})
-    assert torch.equal(outs["0"][0], outs["1"][0])
+    assert _rel(outs["1"][0], outs["0"][0]) < 1e-2
     assert _rel(outs["1"][1], outs["0"][1]) < 2e-2
     for n, gr in outs["0"][2].items():
         assert _rel(outs["1"][2][n], gr) < 2e-2, (n, _rel(outs["1"][2][n], gr))
