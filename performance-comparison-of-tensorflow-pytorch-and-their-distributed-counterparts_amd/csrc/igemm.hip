@@ -147,6 +147,14 @@ __device__ __forceinline__ uint4 fold_dz(uint4 g, uint4 x, const float* k1, cons
   return __builtin_bit_cast(uint4, o);
 }
 
+// The in-kernel split-K fixup is compiled in only with -DPCMP_SK_FIXUP=1: it measured slower than the
+// separate epilogue launch everywhere (profiles/r3_sk_fixup_ab.txt), and its code in the plain
+// epilogue slowed the small-M inference kernels that never take it.
+#ifndef PCMP_SK_FIXUP
+#define PCMP_SK_FIXUP 0
+#endif
+constexpr bool kSkFixup = PCMP_SK_FIXUP != 0;
+
 // split-K ticket: publish this block's partial tile (every thread's stores drained, one agent-scope
 // release), count the arrival; returns true in every thread of the tile's last-arriving block, which
 // has then acquired the other splits' partials (cdna_hip_programming.md split-K seam recipe)
@@ -244,7 +252,9 @@ __device__ __forceinline__ int chan_perm(int rho) {
 // the address update is one uniform scalar offset plus one add per row.
 // Epilogue variants (FWD/DGRAD): plain store, + BatchNorm partial statistics of the stored output
 // (FWD training), + fused BatchNorm-backward reduction (DGRAD; BNR2: two BNs share the gradient).
-enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNR = 2, EPI_BNR2 = 3 };
+// EPI_GELU: the plain epilogue plus the GELU forward / backward activations (act 2 / 3, the BERT FFN
+// Linear GEMMs) -- its own instantiations, so the conv kernels' plain epilogue carries no GELU code
+enum { EPI_PLAIN = 0, EPI_STATS = 1, EPI_BNR = 2, EPI_BNR2 = 3, EPI_GELU = 4 };
 
 // FWD/DGRAD epilogue shared by the 4-wave and 8-wave kernels.  acc[j][i] holds the D^T fragment of
 // MFMA column tile j (4 output channels, PAIR-permuted) x row tile i (16 pixels).
@@ -301,7 +311,7 @@ __device__ __forceinline__ void igemm_epilogue_coal(const IgemmParams& p, f32x4 
   constexpr int NCH = BM / RSTEP;          // chunks per thread
   static_assert(NTHR % CPR == 0 && BM % RSTEP == 0, "coalesced epilogue geometry");
   constexpr bool stats = EPI == EPI_STATS;
-  constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
+  constexpr bool bnr = MODE == MODE_DGRAD && (EPI == EPI_BNR || EPI == EPI_BNR2);
   constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
   constexpr int NS = bnr2 ? 3 : 2;
   constexpr int D = EPD < NCH ? EPD : NCH;
@@ -512,8 +522,8 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           if (n < p.gn) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[j][i];
         }
       }
-      if constexpr (SHRED) {
-        return;   // persistent kernels never split (host-checked)
+      if constexpr (SHRED || !kSkFixup) {
+        return;   // persistent kernels never split (host-checked); fixup compiled out (PCMP_SK_FIXUP)
       } else {
         if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + n0 / BN, reinterpret_cast<int*>(smem))) return;
         const float* ws0 = reinterpret_cast<const float*>(p.out);
@@ -538,13 +548,13 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     constexpr int NV = TN * 4 / VW;           // stores per pixel row
     constexpr int NP = VW / 2;                // packed bf16 pairs per store
     constexpr bool stats = EPI == EPI_STATS;
-    constexpr bool bnr = MODE == MODE_DGRAD && EPI >= EPI_BNR;
+    constexpr bool bnr = MODE == MODE_DGRAD && (EPI == EPI_BNR || EPI == EPI_BNR2);
     constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
     constexpr int NS = bnr2 ? 3 : 2;          // per-channel sums kept
-    // GELU forward / backward epilogues (act 2 / 3) exist only in the plain-epilogue, non-persistent
-    // instantiations (the Linear GEMMs); compiling them out elsewhere keeps the register budget of
-    // the BN-epilogue and halo / streaming kernels untouched
-    constexpr bool GELU = EPI == EPI_PLAIN && !SHRED;
+    // GELU forward / backward epilogues (act 2 / 3) exist only in the EPI_GELU instantiations (the
+    // Linear GEMMs); compiling them out elsewhere keeps the conv kernels' epilogue code and register
+    // budget untouched
+    constexpr bool GELU = EPI == EPI_GELU && !SHRED;
     float sm[NS][TN][4];
 #pragma unroll
     for (int k = 0; k < NS; ++k)
@@ -2316,6 +2326,7 @@ __global__ void __launch_bounds__(NT, 2) skinny_fwd_kernel(const IgemmParams p) 
       const int m = m0 + 16 * i + fr;
       if (nok && m < p.gm) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[i];
     }
+    if constexpr (!kSkFixup) return;
     __shared__ int sk_flag;   // this kernel has no dynamic LDS
     if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + tile_n, &sk_flag)) return;
     const float* ws0 = reinterpret_cast<const float*>(p.out);
@@ -2577,6 +2588,8 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE == MODE_FWD) {
     if (epi == EPI_STATS) {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_STATS); else PCMP_IGEMM_LAUNCH(false, EPI_STATS);
+    } else if (p.relu >= 2) {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_GELU); else PCMP_IGEMM_LAUNCH(false, EPI_GELU);
     } else {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
@@ -2600,6 +2613,8 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
       if (kn_epi_depth_bnr2.get() >= 4) { if (unif) PCMP_IGEMM_LAUNCH_D(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH_D(false, EPI_BNR2); }
       else if (unif) PCMP_IGEMM_LAUNCH(true, EPI_BNR2); else PCMP_IGEMM_LAUNCH(false, EPI_BNR2);
 #undef PCMP_IGEMM_LAUNCH_D
+    } else if (p.relu >= 2) {
+      if (unif) PCMP_IGEMM_LAUNCH(true, EPI_GELU); else PCMP_IGEMM_LAUNCH(false, EPI_GELU);
     } else {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
@@ -2750,13 +2765,14 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(NTHR), smem, st, p);                                     \
   } while (0)
   if constexpr (MODE == MODE_FWD) {
-    if (epi == EPI_STATS) PCMP_DMA_LAUNCH(EPI_STATS); else PCMP_DMA_LAUNCH(EPI_PLAIN);
+    if (epi == EPI_STATS) PCMP_DMA_LAUNCH(EPI_STATS); else if (p.relu >= 2) PCMP_DMA_LAUNCH(EPI_GELU); else PCMP_DMA_LAUNCH(EPI_PLAIN);
   } else {
     if (epi == EPI_BNR) PCMP_DMA_LAUNCH(EPI_BNR);
     else if (epi == EPI_BNR2) {
       if constexpr (NTHR == 256) PCMP_DMA_LAUNCH(EPI_BNR2);
       else TORCH_CHECK(false, "igemm8: dual BN-reduce epilogue not instantiated");
-    } else PCMP_DMA_LAUNCH(EPI_PLAIN);
+    } else if (p.relu >= 2) PCMP_DMA_LAUNCH(EPI_GELU);
+    else PCMP_DMA_LAUNCH(EPI_PLAIN);
   }
 #undef PCMP_DMA_LAUNCH
   PCMP_LAUNCH_CHECK();
@@ -3209,7 +3225,7 @@ static Knob kn_sk_fixup("sk_fixup", 0);
 
 // arm the fixup for a FWD/DGRAD split launch writing bf16 `out`; false: use splitk_epilogue_kernel
 static bool arm_splitk_fixup(IgemmParams& p, void* out, int device) {
-  if (!kn_sk_fixup.get() || p.nsplit <= 1) return false;
+  if (!kSkFixup || !kn_sk_fixup.get() || p.nsplit <= 1) return false;
   // counter index = tile_m * tiles_n + tile_n over the launched kernel's tiles; the smallest tiles
   // any FWD/DGRAD kernel uses are 32 x 64
   int* cnt = counter_slots(ceil_div(p.gm, 32) * ceil_div(p.gn, 64), device);

@@ -588,8 +588,9 @@ def test_small_m_plan_kinds_match_reference(gpu, kind):
 @pytest.mark.parametrize("kind", [1, 3, 4, 5, 6])
 def test_splitk_in_kernel_fixup(gpu, kind):
     """Split-K GEMMs whose last-arriving split sums the partial tiles in split order and runs the
-    epilogue (knob sk_fixup=1, default) == the separate splitk_epilogue launch (sk_fixup=0) == the
-    fp32 reference, bitwise repeatable; FWD (bias / residual / ReLU) and a plain Linear DGRAD."""
+    epilogue (knob sk_fixup=1; compiled in only with -DPCMP_SK_FIXUP=1, otherwise the knob falls back
+    to the separate launch) == the separate splitk_epilogue launch (sk_fixup=0, default) == the fp32
+    reference, bitwise repeatable; FWD (bias / residual / ReLU) and a plain Linear DGRAD."""
     torch.manual_seed(5)
     ops = _ops()
     prev_force = ops.set_knob("plan_force", kind)
