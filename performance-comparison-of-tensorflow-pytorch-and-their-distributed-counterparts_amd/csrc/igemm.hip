@@ -154,6 +154,19 @@ __device__ __forceinline__ uint4 fold_dz(uint4 g, uint4 x, const float* k1, cons
 #define PCMP_SK_FIXUP 0
 #endif
 constexpr bool kSkFixup = PCMP_SK_FIXUP != 0;
+// Likewise the other epilogue variants that measured slower or neutral and stay off: the coalesced
+// LDS-staged epilogue (knob epi_coal, profiles/r3_epi_coal_*.txt) and the in-kernel BN-statistics
+// group reduction (knob bn_group, profiles/r2_bn_group_ab.txt).  Compiled out, they cost the
+// epilogues that never take them nothing (profiles/r3_epilogue_code_ab.txt: unused epilogue code
+// cost the step 3 % and batch-1 inference 12 %); -DPCMP_EPI_COAL=1 / -DPCMP_BN_GROUP=1 restore them.
+#ifndef PCMP_EPI_COAL
+#define PCMP_EPI_COAL 0
+#endif
+#ifndef PCMP_BN_GROUP
+#define PCMP_BN_GROUP 0
+#endif
+constexpr bool kEpiCoal = PCMP_EPI_COAL != 0;
+constexpr bool kBnGroup = PCMP_BN_GROUP != 0;
 
 // split-K ticket: publish this block's partial tile (every thread's stores drained, one agent-scope
 // release), count the arrival; returns true in every thread of the tile's last-arriving block, which
@@ -502,7 +515,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     auto chan = [&](int j) {   // channel offset inside the BN tile of acc[j][*][0]
       return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
     };
-    if constexpr (NTHR == NT && BM == 128 && (BN == 128 || BN == 64) && !SHRED && MODE != MODE_WGRAD) {
+    if constexpr (kEpiCoal && NTHR == NT && BM == 128 && (BN == 128 || BN == 64) && !SHRED && MODE != MODE_WGRAD) {
       if (p.coal && p.nsplit == 1 && p.grp == 0 && p.relu < 2) {
         igemm_epilogue_coal<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m);
         return;
@@ -792,7 +805,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           }
         }
       }
-      if (p.grp > 0) {
+      if (kBnGroup && p.grp > 0) {
         // Publish this tile's rows (plain stores -> every wave drains -> one agent-scope release ->
         // ticket); the group's last arriver acquires and sums the group's rows in row order
         // (cdna_hip_programming.md Guideline 16, split-K seam recipe).  Bitwise deterministic: the
@@ -2546,7 +2559,7 @@ template <int MODE, int BM, int BN, int NTHR>
 static size_t coal_setup(IgemmParams& p, size_t smem) {
   p.coal = 0;
   if constexpr (MODE != MODE_WGRAD && NTHR == NT && BM == 128 && (BN == 128 || BN == 64)) {
-    if (kn_epi_coal.get() && p.nsplit == 1 && p.grp == 0 && p.gn % 8 == 0 && p.relu < 2) {
+    if (kEpiCoal && kn_epi_coal.get() && p.nsplit == 1 && p.grp == 0 && p.gn % 8 == 0 && p.relu < 2) {
       p.coal = 1;
       smem = std::max(smem, (size_t)(BM * (BN + 4) + 7 * BN) * sizeof(float));
     }
@@ -3420,7 +3433,7 @@ static int bn_group_size(int T) { return std::max(16, ceil_div(T, 64)); }
 // set up the group reduction for a single-launch statistics producer; returns the reduced [G][2][gn]
 // fp64 tensor(s) (undefined when grouping is off or not worth it)
 static void setup_bn_group(IgemmParams& p, int T, const at::Tensor& like, at::Tensor& red, at::Tensor* red2) {
-  if (!kn_bn_group.get() || T <= 64) return;
+  if (!kBnGroup || !kn_bn_group.get() || T <= 64) return;
   const int grp = bn_group_size(T);
   const int G = ceil_div(T, grp);
   const int tiles_n_max = ceil_div(p.gn, 64);   // every kernel's column tile is >= 64 wide
@@ -4049,9 +4062,19 @@ void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor&
   PCMP_LAUNCH_CHECK();
 }
 
+// epilogue variants compiled into this build (PCMP_SK_FIXUP / PCMP_EPI_COAL / PCMP_BN_GROUP)
+std::vector<std::string> build_features() {
+  std::vector<std::string> f;
+  if (kSkFixup) f.push_back("sk_fixup");
+  if (kEpiCoal) f.push_back("epi_coal");
+  if (kBnGroup) f.push_back("bn_group");
+  return f;
+}
+
 }  // namespace pcmp
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("build_features() -> str[]", &pcmp::build_features);
   m.def("gemm_plans() -> str[]", &pcmp::gemm_plans);
   m.def("plan_candidates(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu) -> str[]",
         &pcmp::plan_candidates);

@@ -15,7 +15,8 @@ import threading
 import torch
 
 _PKG = pathlib.Path(__file__).resolve().parent.parent
-LIB_PATH = _PKG / "_native" / "libpcmp_hip.so"
+# PCMP_LIB: load another build of the library (same-box A/B of compile-time variants, tools/build_variant.py)
+LIB_PATH = pathlib.Path(os.environ["PCMP_LIB"]) if os.environ.get("PCMP_LIB") else _PKG / "_native" / "libpcmp_hip.so"
 
 _lock = threading.Lock()
 _loaded = False

@@ -634,9 +634,12 @@ def test_splitk_in_kernel_fixup(gpu, kind):
 def test_bn_group_reduction_in_kernel(gpu, mode):
     """The last-arriving block of each row-tile group sums the group's BN-statistics rows in fixed
     order (fp64 [G,2,C] out, no partials_reduce launch): equal to the per-tile rows' sum, bitwise
-    reproducible, and identical in the finalize result."""
+    reproducible, and identical in the finalize result.  (Compiled in only with -DPCMP_BN_GROUP=1:
+    the knob measured slower and stays off, and unused epilogue code costs the other kernels.)"""
     torch.manual_seed(3)
     ops = _ops()
+    if "bn_group" not in ops.build_features():
+        pytest.skip("BN group reduction not compiled into this build (PCMP_BN_GROUP=0)")
     N, H, C, K = 32, 56, 64, 256   # 100,352 rows -> 784 tiles of 128 -> 49 groups of 16
     x = rnd(N, H, H, C, dev=gpu)
     w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
