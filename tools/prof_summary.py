@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--step-kernel", default="sgd_flat",
                     help="kernel that ends each training step (per-step table over the trailing steps)")
     ap.add_argument("--last-steps", type=int, default=3, help="steady-state steps for the per-step table (0 = off)")
+    ap.add_argument("--around", default="", help="print the kernel timeline (queue / stream ids) around the last "
+                                                 "call of this kernel")
+    ap.add_argument("--around-n", type=int, default=14)
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True)
     if not files:
@@ -38,6 +41,33 @@ def main():
     gaps(a.dir, a.last)
     if a.last_steps:
         per_step(a.dir, a.step_kernel, a.last_steps, a.top)
+    if a.around:
+        around(a.dir, a.around, a.around_n)
+
+
+def around(d, name, n):
+    """Kernel timeline (start offset, duration, idle before, queue / stream id) of the n kernels
+    before and after the second-to-last call of ``name``: which stream a GPU idle gap waited on."""
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                             r.get("Queue_Id", "?"), r.get("Stream_Id", "?")))
+    rows.sort()
+    hits = [i for i, r in enumerate(rows) if name in r[2]]
+    if len(hits) < 2:
+        print(f"around: fewer than 2 '{name}' kernels")
+        return
+    c = hits[-2]
+    t0 = rows[c][0]
+    print(f"timeline around '{name}' (us from its start; idle = gap after the latest end so far)")
+    last_end = None
+    for r in rows[max(0, c - n): c + n + 1]:
+        idle = "" if last_end is None else f"{max(0, r[0] - last_end) / 1e3:7.1f}"
+        print(f"  {(r[0] - t0) / 1e3:9.1f} dur {(r[1] - r[0]) / 1e3:7.1f} idle {idle:>7} q {r[3]:>3} s {r[4]:>3}  {r[2][:90]}")
+        last_end = r[1] if last_end is None else max(last_end, r[1])
 
 
 def per_step(d, step_kernel, nsteps, top):
