@@ -39,9 +39,11 @@ __global__ void layernorm_fwd_kernel(const __bf16* __restrict__ x, const __bf16*
                                      const float* __restrict__ g, const float* __restrict__ b, __bf16* __restrict__ y,
                                      __bf16* __restrict__ xs, float* __restrict__ mean_out,
                                      float* __restrict__ rstd_out, int M, int D, float eps, float p,
-                                     uint64_t seed0, uint64_t off, const int64_t* __restrict__ salt) {
+                                     uint64_t seed0, uint64_t off, const int64_t* __restrict__ salt,
+                                     int rper = 0, const __bf16* __restrict__ r2 = nullptr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int rrow = rper ? row % rper : row;
   if (row >= M) return;
   const int DV = D / 8;
   constexpr int MAXV = 4;  // D <= 64*8*4 = 2048
@@ -60,10 +62,14 @@ __global__ void layernorm_fwd_kernel(const __bf16* __restrict__ x, const __bf16*
         for (int e = 0; e < 8; ++e) v[k][e] = uniform01(seed, i0 + e) >= p ? v[k][e] * scale : 0.f;
       }
       if (xs) {
-        float w[8];
-        if (r) ldv8(r + (size_t)row * D + cv * 8, w);
+        float w[8], w2[8];
+        if (r) ldv8(r + (size_t)rrow * D + cv * 8, w);
+        if (r2) ldv8(r2 + cv * 8, w2);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[k][e] += r ? w[e] : 0.f;
+        for (int e = 0; e < 8; ++e) {   // (x + r) + r2: the lane-dense kernel's order
+          v[k][e] += r ? w[e] : 0.f;
+          if (r2) v[k][e] += w2[e];
+        }
         // keep the bf16-rounded sum so backward sees exactly the normalised values
         u16x8 u;
 #pragma unroll
@@ -105,18 +111,23 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const __bf16* __restrict__ 
                                                      __bf16* __restrict__ y, __bf16* __restrict__ xs,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out, int M,
                                                      float eps, float p, uint64_t seed0, uint64_t off,
-                                                     const int64_t* __restrict__ salt) {
+                                                     const int64_t* __restrict__ salt, int rper = 0,
+                                                     const __bf16* __restrict__ r2 = nullptr) {
   constexpr int D = 256 * KC;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
+  // rper > 0: r has rper rows, row i adds r[i % rper] (BERT's position rows broadcast over the
+  // batch); r2: one more [D] row added to every row (the token-type row)
+  const int rrow = rper ? row % rper : row;
   float v[KC][4];
-  uint2 xv[KC], rv[KC];
+  uint2 xv[KC], rv[KC], r2v[KC];
 #pragma unroll
   for (int k = 0; k < KC; ++k) {
     const size_t o = (size_t)row * D + 256 * k + 4 * lane;
     xv[k] = *reinterpret_cast<const uint2*>(x + o);
-    if (r) rv[k] = *reinterpret_cast<const uint2*>(r + o);
+    if (r) rv[k] = *reinterpret_cast<const uint2*>(r + (size_t)rrow * D + 256 * k + 4 * lane);
+    if (r2) r2v[k] = *reinterpret_cast<const uint2*>(r2 + 256 * k + 4 * lane);
   }
   const bool drop = p > 0.f;
   const uint64_t seed = drop ? dropout_seed(seed0, salt) : 0;
@@ -135,6 +146,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const __bf16* __restrict__ 
       if (r) {
         v[k][0] += __uint_as_float(rv[k].x << 16); v[k][1] += __uint_as_float(rv[k].x & 0xffff0000u);
         v[k][2] += __uint_as_float(rv[k].y << 16); v[k][3] += __uint_as_float(rv[k].y & 0xffff0000u);
+      }
+      if (r2) {
+        v[k][0] += __uint_as_float(r2v[k].x << 16); v[k][1] += __uint_as_float(r2v[k].x & 0xffff0000u);
+        v[k][2] += __uint_as_float(r2v[k].y << 16); v[k][3] += __uint_as_float(r2v[k].y & 0xffff0000u);
       }
       // keep the bf16-rounded sum so backward sees exactly the normalised values
       const uint2 u = uint2{f2bf2(v[k][0], v[k][1]), f2bf2(v[k][2], v[k][3])};
@@ -1019,6 +1034,46 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<a
   return {y, xs, mean, rstd};
 }
 
+// BERT embedding sum + LayerNorm in one pass: y = LN(x + pos[row % S] + tt) with x [M, D] (the
+// gathered word rows), pos [S, D] (position rows, broadcast over the batch), tt [D] (token-type
+// row); returns [y, xs, mean, rstd] like layernorm_fwd (xs = the bf16-rounded sum).
+std::vector<at::Tensor> embed_layernorm_fwd(const at::Tensor& x, const at::Tensor& pos, const at::Tensor& tt,
+                                            const at::Tensor& g, const at::Tensor& b, double eps) {
+  PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_BF16(pos); PCMP_CHECK_CONTIG(pos);
+  PCMP_CHECK_BF16(tt); PCMP_CHECK_CONTIG(tt); PCMP_CHECK_F32(g); PCMP_CHECK_F32(b);
+  const int D = x.size(-1);
+  const int M = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 2048, "embed_layernorm: D % 8 and <= 2048");
+  TORCH_CHECK(pos.numel() % D == 0 && pos.numel() > 0, "embed_layernorm: pos must be [S, D]");
+  const int S = pos.numel() / D;
+  TORCH_CHECK(M % S == 0, "embed_layernorm: rows must be a multiple of S");
+  TORCH_CHECK(tt.numel() == D && g.numel() == D && b.numel() == D, "embed_layernorm: tt / gamma / beta must be [D]");
+  auto y = at::empty_like(x), xs = at::empty_like(x);
+  auto f32 = x.options().dtype(at::kFloat);
+  auto mean = at::empty({M}, f32), rstd = at::empty({M}, f32);
+  if (D % 256 == 0 && D <= 1024) {
+#define PCMP_ELNF(KC)                                                                                            \
+  hipLaunchKernelGGL(ln_fwd_kernel<KC>, dim3(ceil_div(M, 4)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),        \
+                     ptr<__bf16>(pos), ptr<float>(g), ptr<float>(b), ptr<__bf16>(y), ptr<__bf16>(xs),           \
+                     ptr<float>(mean), ptr<float>(rstd), M, (float)eps, 0.f, (uint64_t)0, (uint64_t)0, nullptr,  \
+                     S, ptr<__bf16>(tt))
+    switch (D / 256) {
+      case 1: PCMP_ELNF(1); break;
+      case 2: PCMP_ELNF(2); break;
+      case 3: PCMP_ELNF(3); break;
+      default: PCMP_ELNF(4); break;
+    }
+#undef PCMP_ELNF
+  } else {
+    hipLaunchKernelGGL(layernorm_fwd_kernel, dim3(ceil_div(M, 4)), dim3(256), 0, cur_stream(), ptr<__bf16>(x),
+                       ptr<__bf16>(pos), ptr<float>(g), ptr<float>(b), ptr<__bf16>(y), ptr<__bf16>(xs),
+                       ptr<float>(mean), ptr<float>(rstd), M, D, (float)eps, 0.f, (uint64_t)0, (uint64_t)0, nullptr, S,
+                       ptr<__bf16>(tt));
+  }
+  PCMP_LAUNCH_CHECK();
+  return {y, xs, mean, rstd};
+}
+
 // returns dx; dgamma/dbeta written (or accumulated) into the given fp32 tensors when defined
 std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tensor& xs, const at::Tensor& mean,
                                             const at::Tensor& rstd, const at::Tensor& g,
@@ -1233,6 +1288,8 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor g, Tensor(a!)? dg, Tensor(b!)? db, "
         "bool accumulate) -> Tensor",
         &pcmp::layernorm_bwd);
+  m.def("embed_layernorm_fwd(Tensor x, Tensor pos, Tensor tt, Tensor g, Tensor b, float eps) -> Tensor[]",
+        &pcmp::embed_layernorm_fwd);
   m.def("gelu_fwd(Tensor x) -> Tensor", &pcmp::gelu_fwd);
   m.def("gelu_bwd(Tensor dy, Tensor x) -> Tensor", &pcmp::gelu_bwd);
   m.def("tanh_fwd(Tensor x) -> Tensor", &pcmp::tanh_fwd);

@@ -24,12 +24,13 @@ from torch import nn
 from ..ops import _lib
 from ..ops.functions import cross_entropy
 from ..ops.rnn import EmbeddingFn
-from ..ops.transformer import BertAttentionBlockFn, BertFFNBlockFn, attention, gelu, layer_norm, tanh
+from ..ops.transformer import BertAttentionBlockFn, BertFFNBlockFn, EmbedLayerNormFn, attention, gelu, layer_norm, tanh
 from .layers import Dropout, Linear
 
 # PCMP_BERT_FUSED=0: the op-by-op layer (separate dropout / GELU / LayerNorm-backward / bias-grad
 # launches and the autograd add of h's two gradients) -- for A/B runs and parity tests
 _FUSED = os.environ.get("PCMP_BERT_FUSED", "1") != "0"
+_EMB_FUSED = os.environ.get("PCMP_BERT_EMB_FUSED", "1") != "0"
 
 
 @dataclass
@@ -138,13 +139,15 @@ class BertForSequenceClassification(nn.Module):
         # key mask: attention_mask if given (reference passes ids>0), else ids > 0
         mask_ids = input_ids if attention_mask is None else attention_mask.long()
         w = EmbeddingFn.apply(input_ids, self.word, 0, dt).reshape(B * S, d)
-        tt = self.token_type[0] if token_type_ids is None else None
-        if tt is not None:
-            pt = (self.position[:S] + tt).to(dt)
-            pt = pt.unsqueeze(0).expand(B, S, d).reshape(B * S, d)
-        else:
-            pt = (self.position[:S].unsqueeze(0) + self.token_type[token_type_ids]).to(dt).reshape(B * S, d)
-        h = self.emb_drop(self.emb_ln(w, pt.contiguous()))
+        if token_type_ids is None and _EMB_FUSED:
+            # word + position + token-type-0 rows summed inside the LayerNorm kernel
+            h = EmbedLayerNormFn.apply(w, self.position, self.token_type, self.emb_ln.weight, self.emb_ln.bias,
+                                       self.emb_ln.eps, S)
+        else:   # eager torch broadcast (PCMP_BERT_EMB_FUSED=0: the round-3 form, for A/B runs)
+            tt = self.token_type[0] if token_type_ids is None else self.token_type[token_type_ids]
+            pt = (self.position[:S].unsqueeze(0) + tt).to(dt).expand(B, S, d).reshape(B * S, d)
+            h = self.emb_ln(w, pt.contiguous())
+        h = self.emb_drop(h)
         for layer in self.layers:
             h = layer(h, mask_ids, B, S)
         cls = h.reshape(B, S, d)[:, 0].contiguous()

@@ -24,7 +24,7 @@ OP_NAMES = (
     "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16", "wt_transpose_multi",
     "embedding_fwd", "embedding_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
     "masked_mean_fwd", "masked_mean_bwd",
-    "layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd",
+    "layernorm_fwd", "embed_layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd",
     "linear_gelu_fwd", "linear_dgrad_gelu", "attention_fwd", "attention_bwd", "tanh_fwd", "tanh_bwd", "add_bf16",
     "topk_rows", "synth_images",
 )
@@ -34,7 +34,8 @@ OP_NAMES = (
 # (``--dtype fp32``) they run the PyTorch reference implementation -- an explicit, documented list,
 # not a silent fallback; every other op has an fp32 HIP kernel (csrc/f32.hip).
 FP32_REF_OPS = frozenset({
-    "layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd", "linear_gelu_fwd",
+    "layernorm_fwd", "embed_layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd",
+    "linear_gelu_fwd",
     "linear_dgrad_gelu", "tanh_fwd", "tanh_bwd", "attention_fwd", "attention_bwd", "add_bf16", "embedding_fwd", "embedding_bwd",
     "lstm_seq_fwd", "lstm_seq_bwd", "masked_mean_fwd", "masked_mean_bwd",
 })

@@ -556,6 +556,19 @@ def layernorm_fwd(x, r, g, b, eps, p=0.0, seed=0, offset=0, salt=None):
     return [y.to(x.dtype), xs.to(x.dtype), mean.reshape(-1), rstd.reshape(-1)]
 
 
+def embed_layernorm_fwd(x, pos, tt, g, b, eps):
+    """csrc/transformer.hip embed_layernorm_fwd: LN(x + pos[row % S] + tt), the sum rounded once."""
+    D = x.shape[-1]
+    S = pos.numel() // D
+    xs = (x.float().reshape(-1, S, D) + pos.float().reshape(1, S, D) + tt.float().reshape(1, 1, D)).reshape(x.shape)
+    xs = xs.to(x.dtype).float()
+    mean = xs.mean(-1)
+    var = ((xs - mean.unsqueeze(-1)) ** 2).mean(-1)
+    rstd = torch.rsqrt(var + eps)
+    y = (xs - mean.unsqueeze(-1)) * rstd.unsqueeze(-1) * g + b
+    return [y.to(x.dtype), xs.to(x.dtype), mean.reshape(-1), rstd.reshape(-1)]
+
+
 def layernorm_bwd(dy, xs, mean, rstd, g, dg, db, accumulate):
     D = xs.shape[-1]
     dyf = dy.float().reshape(-1, D)

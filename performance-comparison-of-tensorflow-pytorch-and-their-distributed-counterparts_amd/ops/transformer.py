@@ -75,6 +75,57 @@ class AttentionFn(torch.autograd.Function):
         return dqkv, None, None, None, None, None
 
 
+def _partial_rows_grad(p, src2d, n):
+    """Gradient of a table parameter whose first ``n`` elements get the column sums of ``src2d``
+    (``K.colsum``) and whose other rows get none (BERT's position rows past S, token-type rows > 0).
+    Those rows are zeroed only when they may hold something: a fresh temporary, the first write of
+    the flat slot, or a shorter S than the last write."""
+    def compute(out, acc):
+        flat = out.view(-1)
+        K.colsum(src2d, flat[:n], acc)
+        if flat.numel() > n and not acc:
+            own = out is getattr(p, "main_grad", None)
+            seen = getattr(p, "_pcmp_rows_written", None) if own else None
+            if seen is None or seen > n:
+                flat[n:].zero_()
+            if own:
+                p._pcmp_rows_written = n
+    return emit_grad(p, compute)
+
+
+class EmbedLayerNormFn(torch.autograd.Function):
+    """BERT embeddings: y = LayerNorm(word_rows + position[:S] (broadcast over the batch) +
+    token_type[0]) in one kernel (``embed_layernorm_fwd``, csrc/transformer.hip), reading the
+    position / token-type rows from the bf16 shadow.  Backward: the LayerNorm backward kernel, then
+    the position gradient as the column sums of dx over the batch and the token-type gradient as
+    its column sums over every row (``colsum``) -- no broadcast / cast / add launches of eager torch.
+    HF parity: ``BertEmbeddings`` with ``token_type_ids=None`` (pytorch_on_language_distr.py:151-161)."""
+
+    @staticmethod
+    def forward(ctx, w_rows, position, token_type, gamma, beta, eps, S):
+        dt = w_rows.dtype
+        pos = compute_weight(position, dt)[:S].contiguous()
+        tt = compute_weight(token_type, dt)[0].contiguous()
+        y, xs, mean, rstd = K.embed_layernorm_fwd(w_rows.contiguous(), pos, tt, gamma.detach(), beta.detach(), eps)
+        ctx.save_for_backward(xs, mean, rstd)
+        ctx.params, ctx.S = (position, token_type, gamma, beta), S
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, mean, rstd = ctx.saved_tensors
+        position, token_type, gamma, beta = ctx.params
+        gout, acc, fin = sink_or_temp(gamma)
+        bout, bacc, bfin = sink_or_temp(beta)
+        dx = K.layernorm_bwd(dy.contiguous(), xs, mean, rstd, gamma.detach(), gout, bout, acc or bacc)
+        gg, gb = fin(), bfin()
+        D, S = dx.shape[-1], ctx.S
+        B = dx.numel() // (S * D)
+        gp = _partial_rows_grad(position, dx.reshape(B, S * D), S * D)
+        gt = _partial_rows_grad(token_type, dx.reshape(B * S, D), D)
+        return dx, gp, gt, gg, gb, None, None
+
+
 def layer_norm(x, gamma, beta, eps, resid=None):
     return LayerNormFn.apply(x, resid, gamma, beta, eps)
 

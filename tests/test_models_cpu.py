@@ -102,6 +102,13 @@ def test_bert_matches_hf():
     loss.backward()
     sd = dict(hf.named_parameters())
     assert _rel(m.layers[1].ffn1.weight.grad, sd["bert.encoder.layer.1.intermediate.dense.weight"].grad) < 1e-4
+    # embeddings (EmbedLayerNormFn): position rows [:S] and token-type row 0 get the summed gradient,
+    # the rows no token used stay zero
+    hp = sd["bert.embeddings.position_embeddings.weight"].grad
+    ht = sd["bert.embeddings.token_type_embeddings.weight"].grad
+    assert _rel(m.position.grad[:32], hp[:32]) < 1e-4 and float(m.position.grad[32:].abs().max()) == 0.0
+    assert _rel(m.token_type.grad, ht) < 1e-4
+    assert _rel(m.emb_ln.weight.grad, sd["bert.embeddings.LayerNorm.weight"].grad) < 1e-4
 
 
 def test_bert_fused_sublayers_match_op_by_op(monkeypatch):

@@ -88,6 +88,27 @@ def test_layernorm_act(gpu):
     close(ops().tanh_bwd(z, t), ref.tanh_bwd(z, t))
 
 
+@pytest.mark.parametrize("D", [768, 64])
+def test_embed_layernorm_fwd(gpu, D):
+    """word rows + position rows broadcast over the batch + one token-type row, then LayerNorm
+    (lane-dense kernel at D = 768, generic kernel at D = 64) against the fp32 reference."""
+    B, S = 4, 48
+    x = torch.randn(B * S, D, device=gpu).to(torch.bfloat16)
+    pos = torch.randn(S, D, device=gpu).to(torch.bfloat16)
+    tt = torch.randn(D, device=gpu).to(torch.bfloat16)
+    g = torch.rand(D, device=gpu) + 0.5
+    b = torch.randn(D, device=gpu)
+    y, xs, m, s = ops().embed_layernorm_fwd(x, pos, tt, g, b, 1e-12)
+    xsf = (x.float().view(B, S, D) + pos.float() + tt.float()).view(B * S, D)
+    close(xs, xsf, 0, 1e-2)
+    yr = torch.nn.functional.layer_norm(xs.float(), (D,), g, b, 1e-12)
+    close(y, yr)
+    yr2, xsr, mr, sr = ref.embed_layernorm_fwd(x, pos, tt, g, b, 1e-12)
+    assert torch.equal(xs, xsr)
+    close(m, mr, 0, 1e-3)
+    close(s, sr, 1e-3, 0)
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_layernorm_dropout_fused(gpu, p):
     """LayerNorm(drop(x) + r) forward and the fused backward (dx, dropped-branch grad, dgamma,
