@@ -102,12 +102,16 @@ def build(verbose: bool = True, jobs: int | None = None) -> pathlib.Path:
                     print(f"[pcmp build] compiled {s.name}", flush=True)
     need_link = bool(todo) or not LIB.exists() or any(o.stat().st_mtime > LIB.stat().st_mtime for o in objs)
     if need_link:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+        # link to a temporary name and rename: a reader (a running process, a tree snapshot) sees
+        # the old or the new library, never a partly written one
+        tmp = LIB.with_name(LIB.name + ".tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
                f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
                "-ltorch_hip", "-fopenmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
         if verbose:
             print(f"[pcmp build] linked {LIB}", flush=True)
     return LIB

@@ -2539,6 +2539,36 @@ __global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src
   local -= t * nc * nk;
   const int k0 = (local / nc) * 64, c0 = (local % nc) * 64;
   const int ts = (r0 + step * (t / subS)) * S + s0 + step * (t % subS);
+  if ((C & 7) == 0 && (K & 7) == 0 && (d[0] & 7) == 0 && (d[1] & 7) == 0) {
+    // 16-byte path (every BERT / ResNet weight): each thread moves two 8-element chunks in and two
+    // out, so a wave's load / store instruction covers 8 rows x 128 B instead of 1 row x 128 B
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = threadIdx.x + 256 * u;
+      const int r = j >> 3, cc = (j & 7) * 8;
+      const int k = k0 + r, c = c0 + cc;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if (k < K && c < C) v = *reinterpret_cast<const uint4*>(w + ((size_t)k * RS + ts) * C + c);
+      const unsigned short* e = reinterpret_cast<const unsigned short*>(&v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tile[r][cc + q] = e[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = threadIdx.x + 256 * u;
+      const int r = j >> 3, kc = (j & 7) * 8;   // r: output row (c), kc: first k of the chunk
+      const int c = c0 + r, k = k0 + kc;
+      if (c < C && k < K) {
+        uint4 v;
+        unsigned short* e = reinterpret_cast<unsigned short*>(&v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) e[q] = tile[kc + q][r];
+        *reinterpret_cast<uint4*>(wt + ((size_t)c * T + t) * K + k) = v;
+      }
+    }
+    return;
+  }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int k = k0 + r, c = c0 + tx;

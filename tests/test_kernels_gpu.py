@@ -404,11 +404,15 @@ def test_batched_weight_transpose_and_dgrad_with_pretransposed(gpu):
     from pcmp.utils.flat import FlatParams
     shapes = [(64, 3, 3, 64), (256, 1, 1, 64), (72, 7, 7, 8), (512, 1, 1, 256), (128, 3, 3, 128)]
     ps = [torch.nn.Parameter(torch.randn(*s, device=gpu) * 0.05) for s in shapes]
+    # channel counts off the 8-element grid take the kernel's 2-byte path (the rest its 16-byte path)
+    odd = torch.nn.Parameter(torch.randn(20, 3, 3, 12, device=gpu) * 0.05)
     ps[2]._pcmp_s2_pad = 3     # stride-2 7x7 and 3x3 (ConvBN marks them): class-blocked layout
     ps[4]._pcmp_s2_pad = 1
     lin = torch.nn.Parameter(torch.randn(40, 24, device=gpu))     # 2-D: no transposed copy
-    flat = FlatParams(ps + [lin])
+    flat = FlatParams(ps + [odd, lin])
     assert getattr(lin, "_flat_owner", None) is None
+    assert torch.equal(compute_weight_t(odd, torch.bfloat16),
+                       compute_weight(odd, torch.bfloat16).permute(3, 1, 2, 0).contiguous())
     for p in ps:
         wt = compute_weight_t(p, torch.bfloat16)
         full = compute_weight(p, torch.bfloat16).permute(3, 1, 2, 0).contiguous()   # [C,R,S,K]
