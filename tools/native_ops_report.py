@@ -68,8 +68,15 @@ def main():
         # only leaf-most aten ops (children launch nothing themselves)
         if any(getattr(ch, "kernels", None) for ch in e.cpu_children):
             continue
-        frames = [f for f in (e.stack or []) if "pcmp" in f or "counterparts_amd" in f or "tools/" in f]
-        where = frames[0] if frames else (e.stack[0] if e.stack else "?")
+        # the leaf op often carries no Python stack: walk up to the first ancestor that has one
+        # (and name the ancestor op chain, e.g. aten::zeros > aten::zero_ > aten::fill_)
+        anc, chain = e, []
+        while anc is not None and not anc.stack:
+            chain.append(anc.name)
+            anc = anc.cpu_parent
+        stack = anc.stack if anc is not None else []
+        frames = [f for f in stack if "pcmp" in f or "counterparts_amd" in f or "tools/" in f]
+        where = (frames[0] if frames else (stack[0] if stack else "?")) + "  [" + " < ".join(chain[:4]) + "]"
         for k in kern:
             lines[(e.name, k.name[:60], where[-110:])] += 1
     print(f"non-pcmp GPU kernels in one {which} step:")
