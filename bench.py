@@ -84,8 +84,10 @@ def parse():
                     help="gradient all-reduce dtype (default fp32, exact)")
     ap.add_argument("--infer-images", type=int, default=200,
                     help="batch-1 inference latency images measured after the timed loop (0 = skip)")
-    ap.add_argument("--watchdog", type=float, default=0.0,
-                    help="abort (exit 3) if a step makes no progress for this many seconds (0 = off)")
+    ap.add_argument("--watchdog", type=float, default=None,
+                    help="abort (exit 3) if a step makes no progress for this many seconds (0 = off; "
+                         "default 300 when N > 1, so a hung collective fails the job promptly "
+                         "instead of waiting out the 600 s RCCL timeout; off at N = 1)")
     ap.add_argument("--master-port", type=int, default=0, help="self-launch rendezvous port (0 = pick a free one)")
     ap.add_argument("--local_rank", "--local-rank", type=int, default=None)
     return ap.parse_args()
@@ -165,10 +167,11 @@ def build_hip(args, env):
     # critical-path (DGRAD / BN chain) workgroups ahead of the WGRAD side stream's when CUs free up:
     # 12,213-12,283 -> 12,392-12,409 img/s in 3 interleaved rounds (profiles/r3_prio_pf2_ab.txt);
     # PCMP_STEP_PRIO=0 runs it on the default stream
-    prio_stream = None
-    if os.environ.get("PCMP_STEP_PRIO", "1") == "1" and env.device.type == "cuda":
-        prio_stream = torch.cuda.Stream(env.device, priority=-1)
-        prio_stream.wait_stream(torch.cuda.current_stream(env.device))
+    # PriorityStream.step orders the step after the caller's stream (set_lr's device write, the
+    # input batch) and the caller's stream after the step, every step; it stays on the capturing
+    # stream during a hipGraph capture (--graph), so the captured graph holds the whole step
+    from pcmp.utils.misc import PriorityStream
+    prio = PriorityStream(env.device)
 
     def step_body(x, y):
         opt.zero_grad()
@@ -182,9 +185,7 @@ def build_hip(args, env):
         return loss
 
     def step(x, y):
-        if prio_stream is None:
-            return step_body(x, y)
-        with torch.cuda.stream(prio_stream):
+        with prio.step(x, y):
             return step_body(x, y)
 
     step.model = model
@@ -254,6 +255,8 @@ def main():
     if env.world_size != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but the job has WORLD_SIZE={env.world_size} ranks: refusing to "
                          f"report a {env.world_size}-rank number as {args.gpus} GPUs")
+    if args.watchdog is None:
+        args.watchdog = 300.0 if env.world_size > 1 else 0.0
     wd = Watchdog(args.watchdog, abort=True).start() if args.watchdog > 0 else None
     # the communicator really spans WORLD_SIZE ranks: all-reduce of ones over the process group
     world_check = 1
@@ -285,6 +288,10 @@ def main():
         if opt is not None:
             opt.set_lr(args.lr * (i + 1) / ramp)
         loss = step(x, y)
+        if i == 0 and env.world_size > 1:
+            # every shape is planned by now: all ranks take rank 0's autotuned kernels
+            from pcmp.parallel.ddp import sync_autotune
+            sync_autotune()
         if wd is not None:
             wd.kick(i, "warmup")
     if opt is not None:
@@ -314,10 +321,13 @@ def main():
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(args.profile)
-    t = torch.tensor([dt], dtype=torch.float64, device=env.device)
-    if env.world_size > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+    # per-rank spread (a straggler shows here); the reported step time is the MAX over ranks
+    from pcmp.parallel.ddp import step_time_spread
+    spread = step_time_spread(dt)
+    comm["rank_ms_per_step"] = {"min": round(spread["min_s"] / args.steps * 1e3, 3),
+                                "max": round(spread["max_s"] / args.steps * 1e3, 3),
+                                "slowest_rank": spread["slowest_rank"]}
+    dt = spread["max_s"]
     infer = None
     if args.infer_images > 0 and hip_model is not None and env.device.type == "cuda":
         infer = batch1_latency(hip_model, args, env)

@@ -51,5 +51,38 @@ at::Tensor dropout(const at::Tensor& x, double p, int64_t seed, int64_t offset, 
 at::Tensor relu_bwd(const at::Tensor& dy, const at::Tensor& y);
 void colsum(const at::Tensor& x, at::Tensor out, bool accumulate);
 
+// text encoders (text_f32.hip): LayerNorm, attention, GELU / tanh, embedding, pooling, BiLSTM
+at::Tensor act_fwd(const at::Tensor& x, int mode);                               // 0 GELU, 1 tanh
+at::Tensor act_bwd(const at::Tensor& dy, const at::Tensor& xy, int mode);
+at::Tensor add(const at::Tensor& a, const at::Tensor& b);
+std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& g,
+                                      const at::Tensor& b, double eps, double p, int64_t seed, int64_t offset,
+                                      const c10::optional<at::Tensor>& salt);
+std::vector<at::Tensor> embed_layernorm_fwd(const at::Tensor& x, const at::Tensor& pos, const at::Tensor& tt,
+                                            const at::Tensor& g, const at::Tensor& b, double eps);
+std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tensor& xs, const at::Tensor& mean,
+                                            const at::Tensor& rstd, const at::Tensor& g,
+                                            const c10::optional<at::Tensor>& dg, const c10::optional<at::Tensor>& db,
+                                            const c10::optional<at::Tensor>& dbias, int64_t accmask, double p,
+                                            int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt);
+at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& xs, const at::Tensor& mean, const at::Tensor& rstd,
+                         const at::Tensor& g, const c10::optional<at::Tensor>& dg, const c10::optional<at::Tensor>& db,
+                         bool accumulate);
+std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& ids, int64_t B,
+                                      int64_t S, int64_t H, double p_drop, int64_t seed, int64_t offset,
+                                      const c10::optional<at::Tensor>& salt);
+at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at::Tensor& ctx, const at::Tensor& lse,
+                         const c10::optional<at::Tensor>& ids, int64_t B, int64_t S, int64_t H, double p_drop,
+                         int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt);
+at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W);
+void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, int64_t padding_idx, bool accumulate);
+at::Tensor masked_mean_fwd(const at::Tensor& x, const at::Tensor& ids);
+at::Tensor masked_mean_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t S);
+std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh, const at::Tensor& ids);
+std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& gates, const at::Tensor& cst,
+                                     const at::Tensor& whh, const at::Tensor& ids);
+std::vector<at::Tensor> linear_gelu_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias);
+at::Tensor linear_dgrad_gelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& u);
+
 }  // namespace f32
 }  // namespace pcmp

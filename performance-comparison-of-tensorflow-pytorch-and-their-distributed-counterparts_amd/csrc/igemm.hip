@@ -3324,6 +3324,8 @@ static bool plain_gemm_eligible(const IgemmParams& p) {
 
 static std::mutex g_plan_mu;
 static std::unordered_map<std::string, GemmPlan> g_plan_cache;
+// wgrad_nsplit's tuned split counts (same mutex)
+static std::unordered_map<std::string, int> g_wsplit_cache;
 static std::vector<std::string>* g_plan_log = nullptr;   // candidate timings (plan_candidates op)
 
 // "mode,gm,gn,gk,bias,resid,relu -> kind/nsplit" for every planned shape (reports, tests)
@@ -3655,6 +3657,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
 // -> [gelu(u), u] (u = x W^T + b, kept for the backward).  BERT's FFN up-projection
 // (pytorch_on_language_distr.py:151-161 via BertIntermediate).
 std::vector<at::Tensor> linear_gelu_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  if (x.scalar_type() == at::kFloat) return f32::linear_gelu_fwd(x, w, bias);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "linear_gelu_fwd: x [M, C], w [N, C]");
   const int64_t M = x.size(0), C = x.size(1), N = w.size(0);
   auto r = conv_fwd_impl(x.view({M, 1, 1, C}), w.view({N, 1, 1, C}), 1, 0, bias, c10::nullopt, 2, false);
@@ -3870,6 +3873,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
 // pre-activation saved by linear_gelu_fwd (the GELU backward fused into the DGRAD epilogue).
 at::Tensor linear_dgrad_gelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& u,
                              const c10::optional<at::Tensor>& wt) {
+  if (dy.scalar_type() == at::kFloat) return f32::linear_dgrad_gelu(dy, w, u);
   TORCH_CHECK(dy.dim() == 2 && w.dim() == 2 && u.dim() == 2 && dy.size(1) == w.size(0) && u.size(1) == w.size(1) &&
               u.size(0) == dy.size(0), "linear_dgrad_gelu: dy [M, N], w [N, C], u [M, C]");
   const int64_t M = dy.size(0), N = w.size(0), C = w.size(1);
@@ -3994,8 +3998,8 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   if (kn_wgrad_wgs.get() > 0) return nsplit_for(std::max(64, kn_wgrad_wgs.get()));
   const int dflt = nsplit_for(1024);
   if (!tune) return dflt;
-  static std::mutex mu;
-  static std::unordered_map<std::string, int> cache;
+  auto& mu = g_plan_mu;
+  auto& cache = g_wsplit_cache;
   char key[160];
   snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
            (int)use_wgrad8(p));
@@ -4092,6 +4096,43 @@ void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor&
   PCMP_LAUNCH_CHECK();
 }
 
+// Autotune tables as portable strings -- "G;<plan key>;<kind>;<nsplit>" (plan_gemm) and
+// "W;<shape key>;<nsplit>" (wgrad_nsplit) -- so a data-parallel job can make every rank run rank 0's
+// kernel choices (pcmp.parallel.ddp.sync_autotune): each rank times its candidates on its own GPU,
+// and timing noise would otherwise let ranks pick different kernels (different speed, different
+// summation order), the slowest rank gating every step.
+std::vector<std::string> autotune_table() {
+  std::lock_guard<std::mutex> g(g_plan_mu);
+  std::vector<std::string> r;
+  for (auto& kv : g_plan_cache)
+    r.push_back("G;" + kv.first + ";" + std::to_string(kv.second.kind) + ";" + std::to_string(kv.second.nsplit));
+  for (auto& kv : g_wsplit_cache) r.push_back("W;" + kv.first + ";" + std::to_string(kv.second));
+  std::sort(r.begin(), r.end());
+  return r;
+}
+
+// insert or overwrite entries of autotune_table()'s form; returns how many were applied
+int64_t autotune_load(std::vector<std::string> entries) {
+  std::lock_guard<std::mutex> g(g_plan_mu);
+  int64_t n = 0;
+  for (const std::string& e : entries) {
+    std::vector<std::string> f;
+    size_t b = 0;
+    for (size_t i = 0; i <= e.size(); ++i)
+      if (i == e.size() || e[i] == ';') { f.push_back(e.substr(b, i - b)); b = i + 1; }
+    if (f.size() == 4 && f[0] == "G") {
+      g_plan_cache[f[1]] = GemmPlan{std::stoi(f[2]), std::stoi(f[3])};
+      ++n;
+    } else if (f.size() == 3 && f[0] == "W") {
+      g_wsplit_cache[f[1]] = std::stoi(f[2]);
+      ++n;
+    } else {
+      TORCH_CHECK(false, "autotune_load: malformed entry '", e, "'");
+    }
+  }
+  return n;
+}
+
 // epilogue variants compiled into this build (PCMP_SK_FIXUP / PCMP_EPI_COAL / PCMP_BN_GROUP)
 std::vector<std::string> build_features() {
   std::vector<std::string> f;
@@ -4106,6 +4147,8 @@ std::vector<std::string> build_features() {
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("build_features() -> str[]", &pcmp::build_features);
   m.def("gemm_plans() -> str[]", &pcmp::gemm_plans);
+  m.def("autotune_table() -> str[]", &pcmp::autotune_table);
+  m.def("autotune_load(str[] entries) -> int", &pcmp::autotune_load);
   m.def("plan_candidates(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu) -> str[]",
         &pcmp::plan_candidates);
   m.def("wt_transpose_multi(Tensor src, Tensor(a!) dst, Tensor desc, int blocks) -> ()", &pcmp::wt_transpose_multi);

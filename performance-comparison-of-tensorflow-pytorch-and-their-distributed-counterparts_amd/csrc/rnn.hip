@@ -22,6 +22,7 @@
 // (workgroup j owns columns j of dh_rec and the W_hh[:, j] slice); weight gradients are then
 // plain MFMA GEMMs over all timesteps (igemm wgrad), outside the recurrence.
 #include "common.h"
+#include "f32.h"
 
 namespace pcmp {
 
@@ -443,6 +444,7 @@ __global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p)
 static int ew_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256)); }
 
 at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
+  if (W.scalar_type() == at::kFloat) return f32::embedding_fwd(ids, W);
   PCMP_CHECK_CUDA(ids); PCMP_CHECK_BF16(W); PCMP_CHECK_CONTIG(W);
   TORCH_CHECK(ids.scalar_type() == at::kLong, "ids int64");
   const int E = W.size(1);
@@ -459,6 +461,7 @@ at::Tensor embedding_fwd(const at::Tensor& ids, const at::Tensor& W) {
 }
 
 void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, int64_t padding_idx, bool accumulate) {
+  if (dy.scalar_type() == at::kFloat) return f32::embedding_bwd(ids, dy, dW, padding_idx, accumulate);
   PCMP_CHECK_BF16(dy); PCMP_CHECK_F32(dW);
   auto idc = ids.contiguous();
   auto dyc = dy.contiguous();
@@ -471,6 +474,7 @@ void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, i
 }
 
 at::Tensor masked_mean_fwd(const at::Tensor& x, const at::Tensor& ids) {
+  if (x.scalar_type() == at::kFloat) return f32::masked_mean_fwd(x, ids);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   const int B = x.size(0), S = x.size(1), D = x.size(2);
   auto y = at::empty({B, D}, x.options());
@@ -482,6 +486,7 @@ at::Tensor masked_mean_fwd(const at::Tensor& x, const at::Tensor& ids) {
 }
 
 at::Tensor masked_mean_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t S) {
+  if (dy.scalar_type() == at::kFloat) return f32::masked_mean_bwd(dy, ids, S);
   PCMP_CHECK_BF16(dy);
   const int B = dy.size(0), D = dy.size(1);
   auto dx = at::empty({B, S, D}, dy.options());
@@ -501,6 +506,7 @@ static void check_lstm_shapes(int B, int H) {
 // gx [B][S][2][4H] bf16 (input projection incl. biases), whh [2][4H][H] bf16, ids [B][S]
 // -> [hout bf16 [B][S][2H], gates f32 [B][S][2][4H], c f32 [B][S][2][H]]
 std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh, const at::Tensor& ids) {
+  if (gx.scalar_type() == at::kFloat) return f32::lstm_seq_fwd(gx, whh, ids);
   PCMP_CHECK_BF16(gx); PCMP_CHECK_CONTIG(gx); PCMP_CHECK_BF16(whh); PCMP_CHECK_CONTIG(whh);
   const int B = gx.size(0), S = gx.size(1), H = whh.size(2);
   check_lstm_shapes(B, H);
@@ -525,6 +531,7 @@ std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh
 // -> dgates bf16 [B][S][2][4H]  (and the sync/error words)
 std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& gates, const at::Tensor& cst,
                                      const at::Tensor& whh, const at::Tensor& ids) {
+  if (whh.scalar_type() == at::kFloat) return f32::lstm_seq_bwd(dhout, gates, cst, whh, ids);
   PCMP_CHECK_BF16(dhout); PCMP_CHECK_F32(gates); PCMP_CHECK_F32(cst);
   const int B = gates.size(0), S = gates.size(1), H = whh.size(2);
   check_lstm_shapes(B, H);

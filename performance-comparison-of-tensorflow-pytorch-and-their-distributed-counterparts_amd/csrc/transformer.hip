@@ -15,6 +15,7 @@
 // Q, K and the saved LSE, computes dV += Pd^T dO, dP^T = V dO^T, dS^T = P^T (dP^T - D) and
 // dK = dS^T Q on MFMA; dQ = dS K is taken after the waves exchange dS^T through LDS.
 #include "common.h"
+#include "f32.h"
 
 namespace pcmp {
 
@@ -997,6 +998,7 @@ __global__ void __launch_bounds__(256) attention_bwd_kernel(const AttnParams p) 
 std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& g,
                                       const at::Tensor& b, double eps, double p, int64_t seed, int64_t offset,
                                       const c10::optional<at::Tensor>& salt) {
+  if (x.scalar_type() == at::kFloat) return f32::layernorm_fwd(x, r, g, b, eps, p, seed, offset, salt);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(g); PCMP_CHECK_F32(b);
   const int D = x.size(-1);
   const int M = x.numel() / D;
@@ -1039,6 +1041,7 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<a
 // row); returns [y, xs, mean, rstd] like layernorm_fwd (xs = the bf16-rounded sum).
 std::vector<at::Tensor> embed_layernorm_fwd(const at::Tensor& x, const at::Tensor& pos, const at::Tensor& tt,
                                             const at::Tensor& g, const at::Tensor& b, double eps) {
+  if (x.scalar_type() == at::kFloat) return f32::embed_layernorm_fwd(x, pos, tt, g, b, eps);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x); PCMP_CHECK_BF16(pos); PCMP_CHECK_CONTIG(pos);
   PCMP_CHECK_BF16(tt); PCMP_CHECK_CONTIG(tt); PCMP_CHECK_F32(g); PCMP_CHECK_F32(b);
   const int D = x.size(-1);
@@ -1084,6 +1087,7 @@ std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tens
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& xs, const at::Tensor& mean, const at::Tensor& rstd,
                          const at::Tensor& g, const c10::optional<at::Tensor>& dg, const c10::optional<at::Tensor>& db,
                          bool accumulate) {
+  if (xs.scalar_type() == at::kFloat) return f32::layernorm_bwd(dy, xs, mean, rstd, g, dg, db, accumulate);
   const int D = xs.size(-1);
   static const bool v1 = [] { const char* e = std::getenv("PCMP_LN_BWD_V1"); return e && e[0] == '1'; }();
   if (!v1 && D % 256 == 0 && D <= 1024)   // the lane-dense kernel (no dropout, no bias output)
@@ -1126,6 +1130,8 @@ std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tens
                                             const c10::optional<at::Tensor>& dg, const c10::optional<at::Tensor>& db,
                                             const c10::optional<at::Tensor>& dbias, int64_t accmask, double p,
                                             int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt) {
+  if (xs.scalar_type() == at::kFloat)
+    return f32::layernorm_bwd_fused(dy, xs, mean, rstd, g, dg, db, dbias, accmask, p, seed, offset, salt);
   PCMP_CHECK_BF16(xs); PCMP_CHECK_CONTIG(xs); PCMP_CHECK_F32(g); PCMP_CHECK_F32(mean); PCMP_CHECK_F32(rstd);
   auto dyc = dy.contiguous();
   PCMP_CHECK_BF16(dyc);
@@ -1178,6 +1184,7 @@ std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tens
 }
 
 static at::Tensor act_fwd(const at::Tensor& x, int mode) {
+  if (x.scalar_type() == at::kFloat) return f32::act_fwd(x, mode);
   PCMP_CHECK_BF16(x); PCMP_CHECK_CONTIG(x);
   TORCH_CHECK(x.numel() % 8 == 0, "activation numel % 8");
   auto y = at::empty_like(x);
@@ -1187,6 +1194,7 @@ static at::Tensor act_fwd(const at::Tensor& x, int mode) {
   return y;
 }
 static at::Tensor act_bwd(const at::Tensor& dy, const at::Tensor& xy, int mode) {
+  if (xy.scalar_type() == at::kFloat) return f32::act_bwd(dy, xy, mode);
   auto dyc = dy.contiguous();
   auto dx = at::empty_like(xy);
   hipLaunchKernelGGL(act_bwd_kernel, dim3(egrid(xy.numel() / 8)), dim3(256), 0, cur_stream(), ptr<__bf16>(dyc),
@@ -1200,6 +1208,7 @@ at::Tensor tanh_fwd(const at::Tensor& x) { return act_fwd(x, 1); }
 at::Tensor tanh_bwd(const at::Tensor& dy, const at::Tensor& y) { return act_bwd(dy, y, 1); }
 
 at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b) {
+  if (a.scalar_type() == at::kFloat) return f32::add(a, b);
   PCMP_CHECK_BF16(a); PCMP_CHECK_BF16(b);
   auto ac = a.contiguous(), bc = b.contiguous();
   TORCH_CHECK(ac.numel() == bc.numel() && ac.numel() % 8 == 0, "add_bf16: shapes");
@@ -1217,6 +1226,7 @@ static size_t attn_bwd_smem() { return ((size_t)4 * AS * ADP + AS * ASP) * 2 + 3
 std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& ids, int64_t B,
                                       int64_t S, int64_t H, double p_drop, int64_t seed, int64_t offset,
                                       const c10::optional<at::Tensor>& salt) {
+  if (qkv.scalar_type() == at::kFloat) return f32::attention_fwd(qkv, ids, B, S, H, p_drop, seed, offset, salt);
   PCMP_CHECK_BF16(qkv); PCMP_CHECK_CONTIG(qkv);
   const int D3 = qkv.size(-1), D = D3 / 3;
   TORCH_CHECK(D == H * AD, "attention: head dim must be 64");
@@ -1249,6 +1259,8 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional
 at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at::Tensor& ctx, const at::Tensor& lse,
                          const c10::optional<at::Tensor>& ids, int64_t B, int64_t S, int64_t H, double p_drop,
                          int64_t seed, int64_t offset, const c10::optional<at::Tensor>& salt) {
+  if (qkv.scalar_type() == at::kFloat)
+    return f32::attention_bwd(dctx, qkv, ctx, lse, ids, B, S, H, p_drop, seed, offset, salt);
   PCMP_CHECK_BF16(qkv); PCMP_CHECK_CONTIG(qkv); PCMP_CHECK_BF16(ctx); PCMP_CHECK_CONTIG(ctx); PCMP_CHECK_F32(lse);
   auto dc = dctx.contiguous();
   const int D3 = qkv.size(-1), D = D3 / 3;

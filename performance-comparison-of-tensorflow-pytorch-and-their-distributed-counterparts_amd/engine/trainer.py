@@ -51,6 +51,7 @@ class TrainState:
     timer: PhaseTimer | None = None   # per-phase device time, PCMP_PHASE_TIMES=1
     throttle: StepThrottle | None = None   # host run-ahead bound (allocator footprint)
     prio: PriorityStream | None = None     # high-priority compute stream for the step
+    steps_done: int = 0
 
     def phase(self, name):
         """Phase bracket: HIP-event device time + a roctx range for rocprofv3 (when timing)."""
@@ -83,6 +84,11 @@ class TrainState:
             self.timer.step()
         if self.throttle is not None:
             self.throttle.tick()
+        self.steps_done += 1
+        if self.steps_done == 1 and self.ddp is not None and self.ddp.world > 1:
+            # every shape has been planned in this first step: all ranks take rank 0's kernels
+            from ..parallel.ddp import sync_autotune
+            sync_autotune(self.ddp.pg)
         watchdog_kick("train_step")
 
     def phase_report(self, printer=None):

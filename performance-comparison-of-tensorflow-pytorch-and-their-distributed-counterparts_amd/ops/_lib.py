@@ -81,9 +81,9 @@ def set_precision(name: str) -> None:
     reference's precision, SURVEY §0.1 / §5.6: another_neural_net.py:95-115 and nb :655-702 run
     fp32 everywhere).  Both stay on the HIP kernels: fp32 activations select the fp32 kernels of
     ``csrc/f32.hip`` (convolutions / Linear on v_mfma_f32_16x16x4_f32, BatchNorm, pooling, dropout,
-    losses).  The text encoders' bf16-only kernels (LayerNorm, GELU, tanh, attention, embedding,
-    LSTM) have no fp32 twin; in fp32 mode those ops run the PyTorch reference (``kernels.FP32_REF_OPS``,
-    listed in the JSON record of the text entry point)."""
+    losses) and ``csrc/text_f32.hip`` (LayerNorm, attention, GELU / tanh, embedding, masked mean,
+    the BiLSTM recurrence, Linear+GELU): no op falls back to PyTorch (``kernels.FP32_REF_OPS`` is
+    empty)."""
     global _compute_dtype
     assert name in ("bf16", "fp32"), name
     _compute_dtype = torch.float32 if name == "fp32" else None

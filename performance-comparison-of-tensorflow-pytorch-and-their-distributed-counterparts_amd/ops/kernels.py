@@ -30,15 +30,10 @@ OP_NAMES = (
 )
 
 
-# Ops whose HIP kernels are bf16-only (the text encoders').  In the fp32 precision mode
-# (``--dtype fp32``) they run the PyTorch reference implementation -- an explicit, documented list,
-# not a silent fallback; every other op has an fp32 HIP kernel (csrc/f32.hip).
-FP32_REF_OPS = frozenset({
-    "layernorm_fwd", "embed_layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd",
-    "linear_gelu_fwd",
-    "linear_dgrad_gelu", "tanh_fwd", "tanh_bwd", "attention_fwd", "attention_bwd", "add_bf16", "embedding_fwd", "embedding_bwd",
-    "lstm_seq_fwd", "lstm_seq_bwd", "masked_mean_fwd", "masked_mean_bwd",
-})
+# Ops that run the PyTorch reference in the fp32 precision mode (``--dtype fp32``).  Empty: every op
+# has an fp32 HIP kernel -- the image ops in csrc/f32.hip, the text encoders' (LayerNorm, attention,
+# GELU / tanh, embedding, masked mean, BiLSTM recurrence, Linear+GELU) in csrc/text_f32.hip.
+FP32_REF_OPS = frozenset()
 
 
 def _first_tensor(args):

@@ -308,3 +308,42 @@ def convert_sync_batchnorm(module: torch.nn.Module, process_group=None) -> torch
             m.sync_group = process_group if process_group is not None else True
     return module
 
+
+
+def sync_autotune(process_group=None) -> int:
+    """Make every rank run rank 0's autotuned kernel choices.
+
+    The conv / GEMM planner (``plan_gemm``) and the WGRAD split-K tuner (``wgrad_nsplit``) time
+    their candidates on each rank's own GPU the first time a shape is seen.  Timing noise lets
+    ranks pick different kernels, and in data parallelism the slowest rank gates every step (and
+    a different split count changes the gradient's summation order).  Call this once after the
+    first (warm-up) step, when every shape has been planned: rank 0's tables are broadcast and
+    loaded over every rank's own (``torch.ops.pcmp.autotune_table`` / ``autotune_load``).
+    Returns the number of entries applied on this rank (0 at world size 1 or without the native
+    library)."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) <= 1:
+        return 0
+    from ..ops import _lib
+    have = _lib.load()
+    table = [list(torch.ops.pcmp.autotune_table()) if have else []]
+    src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+    dist.broadcast_object_list(table, src=src, group=process_group)
+    if not have or not table[0]:
+        return 0
+    return int(torch.ops.pcmp.autotune_load(table[0]))
+
+
+def step_time_spread(seconds: float, process_group=None) -> dict:
+    """Per-rank wall time of a timed region -> {min, max, mean, argmax rank} over all ranks (one
+    small all-gather).  The bench reports MAX (the job's pace) but a straggler is only visible in
+    the spread."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) <= 1:
+        return {"min_s": seconds, "max_s": seconds, "mean_s": seconds, "slowest_rank": 0}
+    world = dist.get_world_size(process_group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(process_group) == "nccl" \
+        else torch.device("cpu")
+    t = torch.tensor([float(seconds)], dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=process_group)
+    v = [float(x.item()) for x in out]
+    return {"min_s": min(v), "max_s": max(v), "mean_s": sum(v) / world, "slowest_rank": int(max(range(world), key=v.__getitem__))}

@@ -210,11 +210,11 @@ def test_mlp_cpu_reports_held_out_metrics():
 
 
 def test_dtype_fp32_stays_on_hip_backend():
-    """--dtype fp32 (the reference's precision) keeps the HIP backend (fp32 kernels of csrc/f32.hip);
-    only the listed bf16-only text ops run the reference in that mode."""
+    """--dtype fp32 (the reference's precision) keeps the HIP backend: fp32 kernels of csrc/f32.hip
+    (image ops) and csrc/text_f32.hip (text encoders); no op runs the PyTorch reference."""
     from pcmp.ops import _lib
     from pcmp.ops.kernels import FP32_REF_OPS
-    assert "conv_fwd" not in FP32_REF_OPS and "layernorm_fwd" in FP32_REF_OPS
+    assert len(FP32_REF_OPS) == 0
     try:
         _lib.set_precision("fp32")
         assert _lib.backend() == "hip" and _lib.precision() == "fp32"

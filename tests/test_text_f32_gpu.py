@@ -1,0 +1,172 @@
+"""fp32 text path on HIP (``--dtype fp32``, the reference's precision: its BERT fine-tune is fp32 end to
+end, /root/reference/pytorch_on_language_distr.py:151-161,258-275).  Every text op has an fp32 HIP
+kernel (csrc/text_f32.hip); these tests check them op by op against the PyTorch fp32 reference of
+the same op (ops/ref.py), and whole-model gradients (BERT 2-layer, BiLSTM) of the HIP fp32 path
+against the PyTorch fp32 run of the same model at 1e-4 relative error."""
+import pytest
+import torch
+
+import pcmp  # noqa: F401
+from pcmp.ops import _lib, ref
+from pcmp.ops.kernels import FP32_REF_OPS
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    return torch.ops.pcmp
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def test_no_fp32_reference_fallback():
+    assert len(FP32_REF_OPS) == 0
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_layernorm_f32(gpu, p):
+    torch.manual_seed(0)
+    M, D = 300, 768
+    x, r = torch.randn(M, D, device=gpu), torch.randn(M, D, device=gpu)
+    g, b = torch.rand(D, device=gpu) + 0.5, torch.randn(D, device=gpu)
+    got = _ops().layernorm_fwd(x, r, g, b, 1e-12, p, 7, 11)
+    exp = ref.layernorm_fwd(x, r, g, b, 1e-12, p, 7, 11)
+    for a, e in zip(got, exp):
+        assert a.dtype == torch.float32
+        assert _rel(a, e) < 1e-5
+    dy = torch.randn(M, D, device=gpu)
+    outs = [torch.zeros(D, device=gpu) for _ in range(3)]
+    outr = [torch.zeros(D, device=gpu) for _ in range(3)]
+    gd = _ops().layernorm_bwd_fused(dy, got[1], got[2], got[3], g, outs[0], outs[1], outs[2], 0, p, 3, 5)
+    ed = ref.layernorm_bwd_fused(dy, exp[1], exp[2], exp[3], g, outr[0], outr[1], outr[2], 0, p, 3, 5)
+    assert _rel(gd[0], ed[0]) < 1e-5 and _rel(gd[1], ed[1]) < 1e-5
+    for a, e in zip(outs, outr):
+        assert _rel(a, e) < 1e-5
+
+
+def test_embed_layernorm_f32(gpu):
+    torch.manual_seed(1)
+    S, D = 64, 256
+    x, pos, tt = torch.randn(4 * S, D, device=gpu), torch.randn(S, D, device=gpu), torch.randn(D, device=gpu)
+    g, b = torch.rand(D, device=gpu), torch.randn(D, device=gpu)
+    for a, e in zip(_ops().embed_layernorm_fwd(x, pos, tt, g, b, 1e-12), ref.embed_layernorm_fwd(x, pos, tt, g, b, 1e-12)):
+        assert _rel(a, e) < 1e-5
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_f32(gpu, p):
+    torch.manual_seed(2)
+    B, S, H = 3, 128, 4
+    D = 64 * H
+    qkv = torch.randn(B * S, 3 * D, device=gpu)
+    ids = torch.randint(1, 100, (B, S), device=gpu)
+    ids[1, 70:] = 0
+    ids[2, 5:] = 0
+    ctx, lse = _ops().attention_fwd(qkv, ids, B, S, H, p, 9, 3)
+    rc, rl = ref.attention_fwd(qkv, ids, B, S, H, p, 9, 3)
+    assert _rel(ctx, rc) < 1e-5 and _rel(lse, rl) < 1e-6
+    dctx = torch.randn_like(ctx)
+    got = _ops().attention_bwd(dctx, qkv, ctx, lse, ids, B, S, H, p, 9, 3)
+    exp = ref.attention_bwd(dctx, qkv, rc, rl, ids, B, S, H, p, 9, 3)
+    assert _rel(got, exp) < 1e-5
+
+
+def test_act_embedding_pooling_f32(gpu):
+    torch.manual_seed(3)
+    x = torch.randn(1000, 64, device=gpu)
+    dy = torch.randn_like(x)
+    assert _rel(_ops().gelu_fwd(x), ref.gelu_fwd(x)) < 1e-6
+    assert _rel(_ops().gelu_bwd(dy, x), ref.gelu_bwd(dy, x)) < 1e-6
+    y = _ops().tanh_fwd(x)
+    assert _rel(y, ref.tanh_fwd(x)) < 1e-6
+    assert _rel(_ops().tanh_bwd(dy, y), ref.tanh_bwd(dy, y)) < 1e-6
+    assert _rel(_ops().add_bf16(x, dy), x + dy) == 0.0
+    W = torch.randn(500, 32, device=gpu)
+    ids = torch.randint(0, 500, (6, 40), device=gpu)
+    ids[:, 30:] = 0
+    assert torch.equal(_ops().embedding_fwd(ids, W), W[ids])
+    g = torch.randn(6, 40, 32, device=gpu)
+    dW, dWr = torch.zeros_like(W), torch.zeros_like(W)
+    _ops().embedding_bwd(ids, g, dW, 0, False)
+    ref.embedding_bwd(ids, g, dWr, 0, False)
+    assert _rel(dW, dWr) < 1e-6
+    xs = torch.randn(6, 40, 32, device=gpu)
+    assert _rel(_ops().masked_mean_fwd(xs, ids), ref.masked_mean_fwd(xs, ids)) < 1e-6
+    d2 = torch.randn(6, 32, device=gpu)
+    assert _rel(_ops().masked_mean_bwd(d2, ids, 40), ref.masked_mean_bwd(d2, ids, 40)) < 1e-6
+
+
+def test_lstm_seq_f32(gpu):
+    torch.manual_seed(4)
+    B, S, H = 9, 40, 64
+    gx = torch.randn(B, S, 2, 4 * H, device=gpu)
+    whh = torch.randn(2, 4 * H, H, device=gpu) * 0.1
+    ids = torch.randint(1, 50, (B, S), device=gpu)
+    ids[3, 25:] = 0
+    ids[5, :3] = 0
+    got = _ops().lstm_seq_fwd(gx, whh, ids)
+    exp = ref.lstm_seq_fwd(gx, whh, ids)
+    for a, e in zip(got[:3], exp[:3]):
+        assert _rel(a, e) < 1e-5
+    dh = torch.randn(B, S, 2 * H, device=gpu)
+    gd = _ops().lstm_seq_bwd(dh, got[1], got[2], whh, ids)[0]
+    ed = ref.lstm_seq_bwd(dh, exp[1], exp[2], whh, ids)[0]
+    assert _rel(gd, ed) < 1e-5
+
+
+def _grads_fp32(model, fn, backend):
+    from pcmp.ops.functions import dropout_rng
+    dropout_rng.reseed(1234)
+    _lib.set_backend(backend)
+    old = model.compute_dtype
+    model.compute_dtype = torch.float32
+    try:
+        for p in model.parameters():
+            p.grad = None
+        loss = fn()
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.item(), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+    finally:
+        model.compute_dtype = old
+        _lib.set_backend("hip")
+
+
+def _check_model(m, fn, label, tol=1e-4):
+    lr, gr = _grads_fp32(m, fn, "torch")
+    lh, gh = _grads_fp32(m, fn, "hip")
+    errs = sorted(((_rel(gh[n], gr[n]), n) for n in gr if gr[n].norm() > 0), reverse=True)
+    print(label, "loss torch-fp32 %.7f hip-fp32 %.7f" % (lr, lh), "worst", errs[:3])
+    assert set(gh) == set(gr)
+    assert abs(lh - lr) <= 1e-5 * max(1.0, abs(lr))
+    assert errs[0][0] < tol, errs[:3]
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.1])
+def test_bert2_fp32_grads_match_torch_fp32(gpu, drop):
+    from pcmp.models.bert import BertConfig, BertForSequenceClassification
+    torch.manual_seed(0)
+    m = BertForSequenceClassification(BertConfig(num_hidden_layers=2, hidden_dropout_prob=drop,
+                                                 attention_probs_dropout_prob=drop)).to(gpu).train()
+    g = torch.Generator(device=gpu).manual_seed(2)
+    ids = torch.randint(1000, 30522, (8, 128), device=gpu, generator=g)
+    for i, L in enumerate([128, 100, 50, 7, 128, 64, 32, 90]):
+        ids[i, L:] = 0
+    y = torch.randint(0, 2, (8,), device=gpu, generator=g)
+    _check_model(m, lambda: m(ids, None, (ids > 0).long(), y)[0], f"bert2 drop={drop}")
+
+
+def test_bilstm_fp32_grads_match_torch_fp32(gpu):
+    from pcmp.models.bilstm import BiLSTMClassifier
+    from pcmp.ops import cross_entropy
+    torch.manual_seed(0)
+    m = BiLSTMClassifier(2000, 128, 128, 2, 2, 0.0).to(gpu).train()
+    g = torch.Generator(device=gpu).manual_seed(1)
+    ids = torch.randint(1, 2000, (40, 64), device=gpu, generator=g)
+    ids[:, 50:] = 0
+    ids[3, 20:] = 0
+    y = torch.randint(0, 2, (40,), device=gpu, generator=g)
+    _check_model(m, lambda: cross_entropy(m.forward_logits(ids), y), "bilstm")
