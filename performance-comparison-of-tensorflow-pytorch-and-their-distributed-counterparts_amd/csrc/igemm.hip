@@ -90,28 +90,6 @@ struct IgemmParams {
   // instead of bn_mask -- 1/16 of the bytes of the bf16 tensor
   const uint8_t* bn_mbits;
   int stats_cap;   // BM-row tiles the stats / stats2 buffers hold (host-side bounds check)
-  // in-kernel group reduction of the per-tile statistics rows (grp > 0): the last-arriving block of
-  // every group of grp consecutive row tiles (same column tile) sums the group's rows in fixed order
-  // into grp_red[g][2][gn] (fp64; grp_red2 for stats2), so the BN finalize reads <= 64 rows and
-  // needs no separate partial-reduction launch.  grp_cnt: per-(group, column tile) arrival counters,
-  // zero on entry, reset to zero by the last arriver.
-  int grp;
-  int* grp_cnt;
-  double* grp_red;
-  double* grp_red2;
-  // coalesced epilogue (4-wave kernels, BM = 128, no split-K, no in-kernel group reduction): the
-  // fp32 accumulator tile is re-laid out through LDS so every epilogue load / store moves whole
-  // cache lines (igemm_epilogue_coal); set by the host when the launch's LDS allocation covers it
-  int coal;
-  // in-kernel split-K fixup (sk_cnt != null, nsplit > 1): every split writes its fp32 partial tile
-  // to the workspace (out), then takes a ticket on sk_cnt[tile]; the LAST arriver of a tile sums the
-  // nsplit partials in split order (bitwise independent of arrival order) and runs the regular
-  // epilogue into sk_out (FWD/DGRAD plain-epilogue launches, bf16 [gm][gn]; WGRAD keeps its separate
-  // deterministic split reduction) --
-  // no separate reduction / epilogue launch.  Counters come from counter_slots (zero on entry, reset
-  // by the last arriver).
-  int* sk_cnt;
-  void* sk_out;
   // BatchNorm-backward fold (register-staged DGRAD / WGRAD of 1x1 stride-1 convs, fold_x != null):
   // the dy operand is dz = k1*g + k2*x + k3, computed while the tile is staged from g (= a),
   // x (= fold_x, same layout and extent as a) and per-channel coefficients fold_coef[3][K]
@@ -145,57 +123,6 @@ __device__ __forceinline__ uint4 fold_dz(uint4 g, uint4 x, const float* k1, cons
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = ok ? f2bf(k1[e] * bf2f(gv[e]) + k2[e] * bf2f(xv[e]) + k3[e]) : (unsigned short)0;
   return __builtin_bit_cast(uint4, o);
-}
-
-// The in-kernel split-K fixup is compiled in only with -DPCMP_SK_FIXUP=1: it measured slower than the
-// separate epilogue launch everywhere (profiles/r3_sk_fixup_ab.txt), and its code in the plain
-// epilogue slowed the small-M inference kernels that never take it.
-#ifndef PCMP_SK_FIXUP
-#define PCMP_SK_FIXUP 0
-#endif
-constexpr bool kSkFixup = PCMP_SK_FIXUP != 0;
-// Likewise the other epilogue variants that measured slower or neutral and stay off: the coalesced
-// LDS-staged epilogue (knob epi_coal, profiles/r3_epi_coal_*.txt) and the in-kernel BN-statistics
-// group reduction (knob bn_group, profiles/r2_bn_group_ab.txt).  Compiled out, they cost the
-// epilogues that never take them nothing (profiles/r3_epilogue_code_ab.txt: unused epilogue code
-// cost the step 3 % and batch-1 inference 12 %); -DPCMP_EPI_COAL=1 / -DPCMP_BN_GROUP=1 restore them.
-#ifndef PCMP_EPI_COAL
-#define PCMP_EPI_COAL 0
-#endif
-#ifndef PCMP_BN_GROUP
-#define PCMP_BN_GROUP 0
-#endif
-constexpr bool kEpiCoal = PCMP_EPI_COAL != 0;
-constexpr bool kBnGroup = PCMP_BN_GROUP != 0;
-
-// split-K ticket: publish this block's partial tile (every thread's stores drained, one agent-scope
-// release), count the arrival; returns true in every thread of the tile's last-arriving block, which
-// has then acquired the other splits' partials (cdna_hip_programming.md split-K seam recipe)
-// `flag` is one int of LDS: the kernel's dynamic LDS array (its stage buffers are dead here) or, in
-// a kernel without one, a static __shared__ int.  A static __shared__ object inside this inlined
-// helper would add static LDS to every kernel that calls it -- those kernels request the whole
-// 160 KB as dynamic LDS (hipFuncSetAttribute then fails) -- and a second __shared__ object beside
-// an LDS-DMA staging array can de-pipeline the K loop (cdna_hip_programming.md §5, item 4(a)).
-// The trailing barrier keeps every thread's read of the flag ahead of any later LDS reuse.
-__device__ __forceinline__ bool splitk_ticket(const IgemmParams& p, int tile, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(p.sk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == p.nsplit - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(p.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  const bool last = *flag != 0;
-  __syncthreads();
-  return last;
 }
 
 constexpr int BK = 64;
@@ -302,205 +229,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 
-// Coalesced epilogue for the 4-wave FWD / DGRAD kernels (BM = 128, BN = 64 / 128, 256 threads).
-// The MFMA accumulator layout gives each lane 8 channels of one pixel row, so the fragment-shaped
-// epilogue moves 16 rows x 64 B per wave instruction: every 128-B line of the residual, the BN
-// input(s), the ReLU mask and the output is requested twice, and the texture path, not HBM, sets
-// the rate (cdna_hip_programming.md §5, "fragment-shaped x costs +18-45 %, TA_BUSY 2x").  Here the
-// fp32 tile is staged in LDS (the stage buffers are dead) and re-read row-major: thread t keeps the
-// 8-channel chunk (t % (BN/8)) and walks rows t / (BN/8), + NTHR/(BN/8), ...; a wave instruction then
-// covers 4 (BN = 128) or 8 (BN = 64) rows x BN channels of whole lines.  Per-element math is that of
-// igemm_epilogue_fd (fp32 sum, one bf16 rounding, mask on the rounded value), so outputs are bitwise
-// equal; the BN partial sums are reduced in another (fixed) order.
-template <int MODE, int BM, int BN, int WM, int WN, int EPI, int NTHR, int EPD>
-__device__ __forceinline__ void igemm_epilogue_coal(const IgemmParams& p, f32x4 (&acc)[BN / WN / 16][BM / WM / 16],
-                                                    char* smem, int tid, int m0, int n0, int tile_m) {
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr bool PAIR = (TN % 2 == 0);
-  constexpr int LDT = BN + 4;              // fp32 row stride of the staged tile
-  constexpr int CPR = BN / 8;              // 8-channel chunks per row
-  constexpr int RSTEP = NTHR / CPR;        // rows between a thread's chunks
-  constexpr int NCH = BM / RSTEP;          // chunks per thread
-  static_assert(NTHR % CPR == 0 && BM % RSTEP == 0, "coalesced epilogue geometry");
-  constexpr bool stats = EPI == EPI_STATS;
-  constexpr bool bnr = MODE == MODE_DGRAD && (EPI == EPI_BNR || EPI == EPI_BNR2);
-  constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
-  constexpr int NS = bnr2 ? 3 : 2;
-  constexpr int D = EPD < NCH ? EPD : NCH;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wr = wid / WN, wc = wid % WN;
-  const int fr = lane & 15, fq = lane >> 4;
-  float* T = reinterpret_cast<float*>(smem);
-  float* ctab = T + BM * LDT;
-  auto chan = [&](int j) {
-    return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
-  };
-  lds_sync();   // every wave is past its last operand read of the stage buffers
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      *reinterpret_cast<f32x4*>(T + (wr * WTM + i * 16 + fr) * LDT + chan(j)) = acc[j][i];
-  const bool has_bias = MODE == MODE_FWD && p.bias != nullptr;
-  const bool has_res = p.resid != nullptr;
-  const bool has_mb = bnr && p.bn_mbits != nullptr;
-  const bool has_mk = bnr && !has_mb && p.bn_mask != nullptr;
-  const bool mfx = bnr && !has_mb && !has_mk && p.bn_msc != nullptr;
-  for (int idx = tid; idx < BN; idx += NTHR) {
-    const int c = min(n0 + idx, p.gn - 1);
-    ctab[idx] = has_bias ? p.bias[c] : 0.f;
-    if constexpr (bnr) {
-      const float is = p.bn_istd[c];
-      ctab[1 * BN + idx] = is;
-      ctab[2 * BN + idx] = -p.bn_mean[c] * is;
-      ctab[3 * BN + idx] = mfx ? p.bn_msc[c] : 0.f;
-      ctab[4 * BN + idx] = mfx ? p.bn_msh[c] : 0.f;
-      if constexpr (bnr2) {
-        const float is2 = p.bn_istd2[c];
-        ctab[5 * BN + idx] = is2;
-        ctab[6 * BN + idx] = -p.bn_mean2[c] * is2;
-      }
-    }
-  }
-  __syncthreads();
-  const int c8 = (tid % CPR) * 8, rbase = tid / CPR;
-  const int n = n0 + c8;
-  const bool nok = n < p.gn;   // gn % 8 == 0: a chunk is wholly in or out
-  float bias[8], ka[8], kb[8], msc[8], msh[8], ka2[8], kb2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    bias[e] = ctab[c8 + e];
-    if constexpr (bnr) {
-      ka[e] = ctab[1 * BN + c8 + e]; kb[e] = ctab[2 * BN + c8 + e];
-      msc[e] = ctab[3 * BN + c8 + e]; msh[e] = ctab[4 * BN + c8 + e];
-      if constexpr (bnr2) { ka2[e] = ctab[5 * BN + c8 + e]; kb2[e] = ctab[6 * BN + c8 + e]; }
-    }
-  }
-  float sm[NS][8];
-#pragma unroll
-  for (int k = 0; k < NS; ++k)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sm[k][e] = 0.f;
-  auto out_off = [&](int row, bool& ok) -> size_t {
-    const int m = m0 + row;
-    ok = nok && m < p.gm;
-    size_t orow = ok ? m : 0;
-    if constexpr (MODE == MODE_DGRAD) {
-      if (p.sub && ok) {
-        const int nn = fdiv(m, p.fd_HW);
-        const int rem = m - nn * p.dH * p.dW;
-        const int hh = fdiv(rem, p.fd_W);
-        const int ww = rem - hh * p.dW;
-        orow = ((size_t)nn * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
-      }
-    }
-    return orow * p.gn + (ok ? n : 0);
-  };
-  uint4 rv[D], xv[D], xv2[D], mk[D];
-  unsigned mb[D];
-  auto issue = [&](int k, int b) {
-    bool ok;
-    const size_t o = out_off(rbase + k * RSTEP, ok);
-    const uint4 z = uint4{0, 0, 0, 0};
-    if (has_res) rv[b] = ok ? *reinterpret_cast<const uint4*>(p.resid + o) : z;
-    if constexpr (bnr) {
-      if (has_mb) mb[b] = ok ? (unsigned)p.bn_mbits[o >> 3] : 0u;
-      if (has_mk) mk[b] = ok ? *reinterpret_cast<const uint4*>(p.bn_mask + o) : z;
-      xv[b] = ok ? *reinterpret_cast<const uint4*>(p.bn_x + o) : z;
-      if constexpr (bnr2) xv2[b] = ok ? *reinterpret_cast<const uint4*>(p.bn_x2 + o) : z;
-    }
-  };
-  __bf16* out = reinterpret_cast<__bf16*>(p.out);
-#pragma unroll
-  for (int d = 0; d < D - 1; ++d) issue(d, d);
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int b = k % D;
-    if (k + D - 1 < NCH) issue(k + D - 1, (k + D - 1) % D);
-    const int row = rbase + k * RSTEP;
-    bool ok;
-    const size_t o = out_off(row, ok);
-    if (!ok) continue;
-    const f32x4 a0 = *reinterpret_cast<const f32x4*>(T + row * LDT + c8);
-    const f32x4 a1 = *reinterpret_cast<const f32x4*>(T + row * LDT + c8 + 4);
-    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-    const unsigned rw[4] = {rv[b].x, rv[b].y, rv[b].z, rv[b].w};
-    const unsigned xw[4] = {xv[b].x, xv[b].y, xv[b].z, xv[b].w};
-    const unsigned xw2[4] = {xv2[b].x, xv2[b].y, xv2[b].z, xv2[b].w};
-    const unsigned mw[4] = {mk[b].x, mk[b].y, mk[b].z, mk[b].w};
-    unsigned ov[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ce = 2 * q;
-      float x0 = av[ce] + bias[ce], x1 = av[ce + 1] + bias[ce + 1];
-      if (has_res) {
-        x0 += __uint_as_float(rw[q] << 16);
-        x1 += __uint_as_float(rw[q] & 0xffff0000u);
-      }
-      if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
-      unsigned u = f2bf2(x0, x1);
-      if constexpr (bnr) {
-        const float xa = __uint_as_float(xw[q] << 16), xb = __uint_as_float(xw[q] & 0xffff0000u);
-        if (has_mb) {
-          const unsigned bits = mb[b] >> ce;
-          u &= ((bits & 1u) ? 0x0000ffffu : 0u) | ((bits & 2u) ? 0xffff0000u : 0u);
-        } else if (has_mk) {
-          const unsigned y = mw[q];
-          u &= (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
-               (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
-        } else if (mfx) {
-          const float z0 = fmaf(xa, msc[ce], msh[ce]);
-          const float z1 = fmaf(xb, msc[ce + 1], msh[ce + 1]);
-          u &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
-        }
-        const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
-        sm[0][ce] += r0; sm[0][ce + 1] += r1;
-        sm[1][ce] += r0 * fmaf(xa, ka[ce], kb[ce]);
-        sm[1][ce + 1] += r1 * fmaf(xb, ka[ce + 1], kb[ce + 1]);
-        if constexpr (bnr2) {
-          sm[2][ce] += r0 * fmaf(__uint_as_float(xw2[q] << 16), ka2[ce], kb2[ce]);
-          sm[2][ce + 1] += r1 * fmaf(__uint_as_float(xw2[q] & 0xffff0000u), ka2[ce + 1], kb2[ce + 1]);
-        }
-      } else if constexpr (stats) {
-        const float r0 = __uint_as_float(u << 16), r1 = __uint_as_float(u & 0xffff0000u);
-        sm[0][ce] += r0; sm[0][ce + 1] += r1;
-        sm[1][ce] += r0 * r0; sm[1][ce + 1] += r1 * r1;
-      }
-      ov[q] = u;
-    }
-    *reinterpret_cast<uint4*>(out + o) = uint4{ov[0], ov[1], ov[2], ov[3]};
-  }
-  if constexpr (stats || bnr) {
-    // column sums: the RSTEP threads of a chunk column combine through LDS (T is dead now), then one
-    // thread per channel sums the RSTEP rows in order
-    float* red = T;   // [RSTEP][NS][BN]
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NS; ++k) {
-      *reinterpret_cast<f32x4*>(red + (rbase * NS + k) * BN + c8) = f32x4{sm[k][0], sm[k][1], sm[k][2], sm[k][3]};
-      *reinterpret_cast<f32x4*>(red + (rbase * NS + k) * BN + c8 + 4) = f32x4{sm[k][4], sm[k][5], sm[k][6], sm[k][7]};
-    }
-    __syncthreads();
-    float* st = p.stats + (size_t)tile_m * 2 * p.gn;
-    float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
-    for (int i = tid; i < NS * BN; i += NTHR) {
-      const int k = i / BN, ci = i - k * BN, c = n0 + ci;
-      if (c >= p.gn) continue;
-      float t = 0.f;
-#pragma unroll 4
-      for (int r = 0; r < RSTEP; ++r) t += red[(r * NS + k) * BN + ci];
-      if (k == 0) { st[c] = t; if (bnr2) st2[c] = t; }
-      else if (k == 1) st[p.gn + c] = t;
-      else st2[p.gn + c] = t;
-    }
-  }
-}
-
-// SHRED: column sums reduced across the 16 pixel lanes with DPP instead of an LDS transpose, so
-// the epilogue's LDS scratch is only [6][BN] coefficient rows + [WM][NS][BN] partials (smem must
-// then point at a region that no stage buffer uses: the persistent streaming kernel keeps
-// prefetching the next tile into its stage buffers while this epilogue runs).
+// SHRED: the epilogue scratch is the fixed region at `smem` (the halo kernel keeps its next tile's
+// halo in the rest of LDS): column sums by DPP row reductions, LDS-only barriers
 template <int MODE, int BM, int BN, int WM, int WN, int EPI, int NTHR, int EPD = 2, bool SHRED = false>
 __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&acc)[BN / WN / 16][BM / WM / 16],
                                                   char* smem, int tid, int m0, int n0, int tile_m, int split) {
@@ -515,15 +245,8 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     auto chan = [&](int j) {   // channel offset inside the BN tile of acc[j][*][0]
       return PAIR ? wc * WTN + (j >> 1) * 32 + fq * 8 + (j & 1) * 4 : wc * WTN + j * 16 + fq * 4;
     };
-    if constexpr (kEpiCoal && NTHR == NT && BM == 128 && (BN == 128 || BN == 64) && !SHRED && MODE != MODE_WGRAD) {
-      if (p.coal && p.nsplit == 1 && p.grp == 0 && p.relu < 2) {
-        igemm_epilogue_coal<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m);
-        return;
-      }
-    }
     if (p.nsplit > 1) {
-      // split-K: raw fp32 partials; the epilogue runs in the reduction kernel or, with the in-kernel
-      // fixup, in the tile's last-arriving split
+      // split-K: raw fp32 partials; the epilogue runs in the reduction kernel
       float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -535,28 +258,9 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           if (n < p.gn) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[j][i];
         }
       }
-      if constexpr (SHRED || !kSkFixup) {
-        return;   // persistent kernels never split (host-checked); fixup compiled out (PCMP_SK_FIXUP)
-      } else {
-        if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + n0 / BN, reinterpret_cast<int*>(smem))) return;
-        const float* ws0 = reinterpret_cast<const float*>(p.out);
-        const size_t slab = (size_t)p.gm * p.gn;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int m = m0 + wr * WTM + i * 16 + fr;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int n = n0 + chan(j);
-            if (m >= p.gm || n >= p.gn) continue;
-            f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (int sp = 0; sp < p.nsplit; ++sp)
-              t += sp == split ? acc[j][i] : *reinterpret_cast<const f32x4*>(ws0 + sp * slab + (size_t)m * p.gn + n);
-            acc[j][i] = t;
-          }
-        }
-      }
+      return;   // the split partials are reduced (+ epilogue) by splitk_epilogue_kernel
     }
-    __bf16* out = reinterpret_cast<__bf16*>(p.nsplit > 1 ? p.sk_out : p.out);
+    __bf16* out = reinterpret_cast<__bf16*>(p.out);
     constexpr int VW = PAIR ? 8 : 4;          // channels per store
     constexpr int NV = TN * 4 / VW;           // stores per pixel row
     constexpr int NP = VW / 2;                // packed bf16 pairs per store
@@ -803,45 +507,6 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
             st2[c] = t[0];
             st2[p.gn + c] = t[2];
           }
-        }
-      }
-      if (kBnGroup && p.grp > 0) {
-        // Publish this tile's rows (plain stores -> every wave drains -> one agent-scope release ->
-        // ticket); the group's last arriver acquires and sums the group's rows in row order
-        // (cdna_hip_programming.md Guideline 16, split-K seam recipe).  Bitwise deterministic: the
-        // summation order does not depend on which block arrives last.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int* flag = reinterpret_cast<int*>(smem);   // the epilogue scratch is dead here
-        const int tile_n = n0 / BN;
-        const int g = tile_m / p.grp;
-        int* cnt = p.grp_cnt + g * p.tiles_n + tile_n;
-        if (tid == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const int members = min(p.grp, p.tiles_m - g * p.grp);
-          const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *flag = (t == members - 1) ? 1 : 0;
-        }
-        __syncthreads();
-        if (*flag) {
-          if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          }
-          __syncthreads();
-          const int r0 = g * p.grp, r1 = min(p.tiles_m, r0 + p.grp);
-          constexpr int NO = bnr2 ? 4 : 2;   // (buffer, sum index) pairs
-          for (int i = tid; i < NO * BN; i += NTHR) {
-            const int k = i / BN, c = n0 + (i - k * BN);
-            if (c >= p.gn) continue;
-            const float* src = (k < 2 ? p.stats : p.stats2) + (size_t)(k & 1) * p.gn + c;
-            double acc = 0.0;
-            for (int r = r0; r < r1; ++r) acc += (double)src[(size_t)r * 2 * p.gn];
-            double* dst = (k < 2 ? p.grp_red : p.grp_red2) + (size_t)g * 2 * p.gn + (size_t)(k & 1) * p.gn + c;
-            *dst = acc;
-          }
-          if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -1299,197 +964,6 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
 }
 
 // ------------------------------------------------------------------------------------------------
-// LDS-DMA WGRAD kernel: dW[co][j] (+)= sum_m dy[m][co] * im2col(x)[m][j] with both operand tiles
-// moved global -> LDS by buffer_load ... lds (no VGPR round trip, no ds_write, no loader VALU on
-// the critical path) into the transposed-read images of the register-staged WGRAD kernel
-// (tr_off: [BK reduction rows][cols], read with ds_read_b64_tr_b16).  A DMA instruction writes
-// 1 KB of consecutive LDS (64 lanes x 16 B), so lane -> (row, chunk) is the INVERSE of the
-// image's swizzle: lane l of wave w, instruction i fills LDS chunk position P = (i*NW + w)*64 + l,
-// i.e. row P / CPR and logical chunk (P % CPR) ^ 2f(row), and fetches that chunk from global
-// (dy row for A; the im2col gather of x for B, whose per-row (n, p, q) walk advances by BK rows
-// per stage without divisions).  Double-buffered: the DMA of stage t+1 is in flight while stage t
-// is multiplied; one counted vmcnt + barrier before and one LDS barrier after each stage.
-// Epilogue and split-K semantics are those of igemm_kernel<MODE_WGRAD>.
-template <int COLS>
-__device__ __forceinline__ int tr_chunk_of_pos(int row, int pos) {   // inverse of tr_off's chunk swizzle
-  constexpr int RB = COLS * 2;
-  int f;
-  if constexpr (RB >= 256) f = (row & 3) | (((row >> 3) & 1) << 2);
-  else if constexpr (RB == 128) f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
-  else f = 0;
-  return pos ^ (2 * f);
-}
-
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(NT, 2) igemm_wgrad_dma_kernel(const IgemmParams p) {
-  constexpr int NW = NT / 64;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int RBA = BM * 2, RBB = BN * 2;
-  constexpr int A_BYTES = BK * RBA, B_BYTES = BK * RBB, STAGE = A_BYTES + B_BYTES;
-  constexpr int NIA = A_BYTES / 1024 / NW, NIB = B_BYTES / 1024 / NW;
-  constexpr int CPR_A = RBA / 16, CPR_B = RBB / 16;
-  static_assert(WM * WN == NW && NIA >= 1 && NIB >= 1 && NIA * NW * 1024 == A_BYTES && NIB * NW * 1024 == B_BYTES,
-                "wgrad_dma geometry");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid / WN, wc = wid % WN;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int tiles_mn = p.tiles_m * p.tiles_n;
-  const int split = lin / tiles_mn;
-  const int tl = lin - split * tiles_mn;
-  const int tile_n = tl % p.tiles_n, tile_m = tl / p.tiles_n;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int kbeg = split * p.ksplit;
-  const int kend = min(p.gk, kbeg + p.ksplit);
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
-  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
-
-  // ---- A slots: dy rows (reduction index m), output-channel chunk
-  int a_off[NIA], a_row[NIA];
-  bool a_cok[NIA];
-#pragma unroll
-  for (int i = 0; i < NIA; ++i) {
-    const int P = (i * NW + wid) * 64 + lane;
-    const int row = P / CPR_A;
-    const int col = tr_chunk_of_pos<BM>(row, P % CPR_A) * 8;
-    a_row[i] = row;
-    a_cok[i] = m0 + col < p.gm;
-    a_off[i] = (kbeg + row) * p.K + m0 + col;
-  }
-  // ---- B slots: im2col rows, column chunk j = (r, s, c)
-  const int st = p.stride;
-  const int dq = BK % p.Q, dp = (BK / p.Q) % p.P, dn = BK / (p.P * p.Q);
-  const int WC = p.W * p.C;
-  const int g_dqs = dq * st, g_Qs = p.Q * st, g_dps = dp * st, g_Ps = p.P * st;
-  const int g_A0 = dq * st * p.C + dp * st * WC + dn * p.H * WC;
-  const int g_A1 = st * WC - p.Q * st * p.C;
-  const int g_A2 = p.H * WC - p.P * st * WC;
-  int b_off[NIB], b_ps[NIB], b_qs[NIB], b_row[NIB], b_r[NIB], b_s[NIB], b_col[NIB];
-  bool b_cok[NIB];
-#pragma unroll
-  for (int i = 0; i < NIB; ++i) {
-    const int P = (i * NW + wid) * 64 + lane;
-    const int row = P / CPR_B;
-    const int j = n0 + tr_chunk_of_pos<BN>(row, P % CPR_B) * 8;
-    b_row[i] = row;
-    b_cok[i] = j < p.gn;
-    const int jj = b_cok[i] ? j : 0;
-    const int c = jj % p.C, rs = jj / p.C;
-    b_s[i] = rs % p.S - p.pad;
-    b_r[i] = rs / p.S - p.pad;
-    b_col[i] = (b_r[i] * p.W + b_s[i]) * p.C + c;
-    const int m = min(kbeg + row, p.gk);
-    const int n = fdiv(m, p.fd_PQ);
-    const int rem = m - n * p.P * p.Q;
-    const int pp = fdiv(rem, p.fd_Q);
-    const int qq = rem - pp * p.Q;
-    b_ps[i] = pp * st;
-    b_qs[i] = qq * st;
-    b_off[i] = ((n * p.H + pp * st) * p.W + qq * st) * p.C;
-  }
-  int k0 = kbeg;
-  auto issue = [&](int buf) {
-    char* sA = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < NIA; ++i) {
-      const bool ok = a_cok[i] && k0 + a_row[i] < kend;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(sA + (i * NW + wid) * 1024),
-                                               16, ok ? (unsigned)a_off[i] * 2u : kOOB, 0, 0, 0);
-      a_off[i] += BK * p.K;
-    }
-#pragma unroll
-    for (int i = 0; i < NIB; ++i) {
-      const int yy = b_ps[i] + b_r[i], xx = b_qs[i] + b_s[i];
-      const bool ok = b_cok[i] && k0 + b_row[i] < kend && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB,
-                                               (__attribute__((address_space(3))) void*)(sA + A_BYTES + (i * NW + wid) * 1024),
-                                               16, ok ? (unsigned)(b_off[i] + b_col[i]) * 2u : kOOB, 0, 0, 0);
-      int qs = b_qs[i] + g_dqs;
-      const bool c1 = qs >= g_Qs;
-      qs -= c1 ? g_Qs : 0;
-      int ps = b_ps[i] + g_dps + (c1 ? st : 0);
-      const bool c2 = ps >= g_Ps;
-      ps -= c2 ? g_Ps : 0;
-      b_qs[i] = qs;
-      b_ps[i] = ps;
-      b_off[i] += g_A0 + (c1 ? g_A1 : 0) + (c2 ? g_A2 : 0);
-    }
-    k0 += BK;
-  };
-
-  typedef short s16x4 __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
-  auto compute = [&](int buf) {
-    const char* sA = smem + buf * STAGE;
-    const char* sB = sA + A_BYTES;
-    const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      const int rowb = kk * 32 + 8 * g + q;
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int col = wr * WTM + i * 16 + pc;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
-        fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wc * WTN + j * 16 + pc;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
-        fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  if (nk > 0) {
-    issue(0);
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < nk) { issue(buf ^ 1); wait_vm<NIA + NIB>(); } else wait_vm<0>();
-      lds_barrier();          // stage t landed in LDS for every wave
-      compute(buf);
-      lds_sync();             // WAR: every wave's ds_reads of buf retire before it is re-filled
-    }
-  }
-
-  const int fr = lane & 15, fq = lane >> 4;
-  float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wc * WTN + j * 16 + fr;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wr * WTM + i * 16 + fq * 4 + e;
-        if (row < p.gm && col < p.gn) {
-          float v = acc[i][j][e] * p.alpha;
-          float* dst = out + (size_t)row * p.gn + col;
-          if (p.accumulate) v += *dst;
-          *dst = v;
-        }
-      }
-    }
-}
-
-
-// ------------------------------------------------------------------------------------------------
 // LDS-DMA kernel for FWD/DGRAD GEMMs with the block-uniform tap walk.  Two instantiations:
 //   8 waves, BM = 256 x BN = 256 (2x4 waves, 128x64 wave tiles), 1 block per CU -- large grids;
 //   4 waves, BM x BN = 128x128 / 256x64 (64x64 wave tiles), 2 blocks per CU -- everything else.
@@ -1507,13 +981,12 @@ constexpr int NT8 = 512;
 constexpr int BM8 = 256;
 
 
-// SCHED: 0 = lock-step 4-phase schedule (DMA of tile t+1 issued during tile t), 1 = wave-row
-// staggered READ / MFMA slots (8 waves), 2 = early prefetch (each half-tile of tile t+2 is DMA'd
-// into the buffer being read as soon as its tile-t half has been consumed: 4-7 phases of lead
-// instead of 3, one counted vmcnt per K-tile)
-template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI, int EPD = 2, int SCHED = 0>
+// Schedule: early prefetch -- each half-tile of tile t+2 is DMA'd into the buffer being read as soon
+// as its tile-t half has been consumed (4-7 phases of lead, one counted vmcnt per K-tile; +0.7 % on
+// the ResNet-50 step over the lock-step 4-phase schedule, profiles/r3_prio_pf2_ab.txt; the lock-step
+// and wave-row-staggered schedules were removed in round 4)
+template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB, int EPI, int EPD = 2>
 __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams p) {
-  constexpr bool STAG = SCHED == 1;
   constexpr int NW = NTHR / 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1669,225 +1142,154 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nh][j][kk], fa[i][kk], acc[nh * TNH + j][mh * TMH + i], 0, 0, 0);
   };
 
-  if constexpr (SCHED == 2) {
-    // per-tile tap state (the halves of tiles t+1 and t+2 are in flight together)
-    struct KS { int k0, kc, ks, kr; };
-    auto adv = [&](KS st) {
-      st.k0 += BK; st.kc += BK;
-      if (st.kc >= CIN) { st.kc = 0; if (++st.ks == p.S) { st.ks = 0; ++st.kr; } }
-      return st;
-    };
-    auto set_state = [&](const KS& st) { k0 = st.k0; kc = st.kc; ks = st.ks; kr = st.kr; };
-    const KS s0{k0, kc, ks, kr};
-    KS s1 = adv(s0), s2 = adv(s1);
-    // prologue: all of tile 0 (buffer 0), then A0, B1, A1 of tile 1 (buffer 1)
-    issue_a(0, 0); issue_b(0, 0); issue_b(1, 0); issue_a(1, 0);
-    if (nk > 1) {
-      set_state(s1);
-      issue_a(0, 1); issue_b(1, 1); issue_a(1, 1);
-      wait_vm<2 * NA + NB>();
-    } else {
-      wait_vm<0>();
-    }
-    lds_barrier();
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1, nb = buf ^ 1;
-      const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
-      // P0: quadrant (0,0); DMA B0(t+1) into nb (its tile t-1 B0 was last read in P3(t-1))
-      read_a(0, buf); read_b(0, buf);
-      if (has1) { set_state(s1); issue_b(0, nb); }
-      mma(0, 0);
-      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
-      // P1: quadrant (0,1); DMA A0(t+2) into buf (A0(t) read in P0)
-      read_b(1, buf);
-      if (has2) { set_state(s2); issue_a(0, buf); }
-      mma(0, 1);
-      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
-      // P2: quadrant (1,1); DMA B1(t+2) into buf (B1(t) read in P1)
-      read_a(1, buf);
-      if (has2) issue_b(1, buf);
-      mma(1, 1);
-      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
-      // P3: quadrant (1,0); DMA A1(t+2) into buf (A1(t) read in P2); retire all of tile t+1
-      read_b(0, buf);
-      if (has2) issue_a(1, buf);
-      mma(1, 0);
-      if (has2) wait_vm<2 * NA + NB>(); else wait_vm<0>();
-      lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
-      s1 = s2;
-      s2 = adv(s2);
-    }
-    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
-    return;
-  }
-
-  // ---- prologue: tile 0 complete in buffer 0
+  // per-tile tap state (the halves of tiles t+1 and t+2 are in flight together)
+  struct KS { int k0, kc, ks, kr; };
+  auto adv = [&](KS st) {
+    st.k0 += BK; st.kc += BK;
+    if (st.kc >= CIN) { st.kc = 0; if (++st.ks == p.S) { st.ks = 0; ++st.kr; } }
+    return st;
+  };
+  auto set_state = [&](const KS& st) { k0 = st.k0; kc = st.kc; ks = st.ks; kr = st.kr; };
+  const KS s0{k0, kc, ks, kr};
+  KS s1 = adv(s0), s2 = adv(s1);
+  // prologue: all of tile 0 (buffer 0), then A0, B1, A1 of tile 1 (buffer 1)
   issue_a(0, 0); issue_b(0, 0); issue_b(1, 0); issue_a(1, 0);
-  advance();
-  wait_vm<0>();
-  lds_barrier();
-
-  if constexpr (STAG) {
-    // Wave-row-staggered schedule (8 waves, 1 block per CU; cdna_hip_programming.md §5 "the 256^2
-    // 8-phase template").  Every quadrant phase q is split into a READ slot (its LDS fragment reads,
-    // the LDS-DMA of one half-tile of tile t+1, the counted vmcnt wait) and an MFMA slot, each
-    // closed by a workgroup barrier.  Wave row 1 starts one barrier late, so on every SIMD (one wave
-    // of each row) one wave issues its LDS reads / DMA while the other runs its 16 MFMAs: the matrix
-    // pipe no longer idles while both lock-stepped waves wait for their fragments.
-    //   slot s: row 0 runs its program slot s, row 1 its slot s-1.  Reads of half H(t) by row 0 in
-    //   READ_q come after barrier 8t+2q-1, which both rows pass only after the wait retiring H(t)
-    //   that sits in their READ_{q-1}: the retire point is one phase ahead of the first read, for
-    //   either row (hazard table in docs/PERF_NOTES.md, round 3).  The DMA of tile t+1 into buffer
-    //   nb starts at READ_0(t) of row 0, after row 1 has finished reading tile t-1 (its last reads,
-    //   READ_3(t-1), complete before its MFMA slot and the barrier that closes it).
-    const bool row1 = (__builtin_amdgcn_readfirstlane(tid >> 6) / WN) == 1;   // wave-uniform (SGPR) branch
-    auto mma_slot = [&](int mh, int nh) {
-      lds_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-      mma(mh, nh);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      lds_barrier();
-    };
-    if (row1) lds_barrier();
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1, nb = buf ^ 1;
-      const bool nxt = t + 1 < nk;
-      // READ_0: A0, B0 of t; DMA A0(t+1); retire B1(t)
-      read_a(0, buf); read_b(0, buf);
-      if (nxt) { issue_a(0, nb); wait_vm<2 * NA>(); } else wait_vm<NA>();
-      mma_slot(0, 0);
-      // READ_1: B1 of t; DMA B0(t+1); retire A1(t)
-      read_b(1, buf);
-      if (nxt) { issue_b(0, nb); wait_vm<NA + NB>(); } else wait_vm<0>();
-      mma_slot(0, 1);
-      // READ_2: A1 of t; DMA B1(t+1)
-      read_a(1, buf);
-      if (nxt) issue_b(1, nb);
-      mma_slot(1, 1);
-      // READ_3: B0 of t (again); DMA A1(t+1); retire A0(t+1), B0(t+1) for READ_0(t+1)
-      read_b(0, buf);
-      if (nxt) { issue_a(1, nb); advance(); wait_vm<NA + NB>(); }
-      mma_slot(1, 0);
-    }
-    if (!row1) lds_barrier();   // re-align the rows: every wave's LDS reads are done past here
-    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
-    return;
+  if (nk > 1) {
+    set_state(s1);
+    issue_a(0, 1); issue_b(1, 1); issue_a(1, 1);
+    wait_vm<2 * NA + NB>();
+  } else {
+    wait_vm<0>();
   }
-
+  lds_barrier();
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1, nb = buf ^ 1;
-    const bool nxt = t + 1 < nk;
-    // phase 0: quadrant (0,0); DMA A0 of t+1
+    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+    // P0: quadrant (0,0); DMA B0(t+1) into nb (its tile t-1 B0 was last read in P3(t-1))
     read_a(0, buf); read_b(0, buf);
-    if (nxt) issue_a(0, nb);
+    if (has1) { set_state(s1); issue_b(0, nb); }
     mma(0, 0);
-    if (nxt) wait_vm<2 * NA>(); else wait_vm<NA>();     // retire B1(t)
-    lds_barrier();
-    // phase 1: quadrant (0,1); DMA B0 of t+1
+    lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+    // P1: quadrant (0,1); DMA A0(t+2) into buf (A0(t) read in P0)
     read_b(1, buf);
-    if (nxt) issue_b(0, nb);
+    if (has2) { set_state(s2); issue_a(0, buf); }
     mma(0, 1);
-    if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A1(t)
-    lds_barrier();
-    // phase 2: quadrant (1,1); DMA B1 of t+1 (nothing to retire: phase 3 re-reads B0(t))
+    lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+    // P2: quadrant (1,1); DMA B1(t+2) into buf (B1(t) read in P1)
     read_a(1, buf);
-    if (nxt) issue_b(1, nb);
+    if (has2) issue_b(1, buf);
     mma(1, 1);
-    // phase 3: quadrant (1,0); DMA A1 of t+1
+    lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+    // P3: quadrant (1,0); DMA A1(t+2) into buf (A1(t) read in P2); retire all of tile t+1
     read_b(0, buf);
-    if (nxt) { issue_a(1, nb); advance(); }
+    if (has2) issue_a(1, buf);
     mma(1, 0);
-    if (nxt) wait_vm<NA + NB>(); else wait_vm<0>();     // retire A0(t+1), B0(t+1)
-    lds_barrier();
+    if (has2) wait_vm<2 * NA + NB>(); else wait_vm<0>();
+    lds_sync();   // WAR: this phase's ds_reads retire before another wave re-DMAs the region
+    s1 = s2;
+    s2 = adv(s2);
   }
   igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Persistent streaming kernel for the memory-bound FWD / DGRAD GEMMs (short reductions with
-// write-heavy epilogues: the 1x1 convolutions of ResNet-50 whose outputs and BN operands are
-// 100-400 MB).  The one-tile-per-block kernels expose a full HBM round trip per tile (operand load
-// -> MFMA -> epilogue loads -> stores) at 2-3 resident blocks per CU (tools/dgrad_probe.py: the
-// layer-1 1x1 DGRAD ran at 3.6 TB/s).  Here each block loops over tiles t, t + grid, ... and, as
-// soon as a tile's last K-step has been read from LDS, issues the LDS-DMA loads of the NEXT tile's
-// first two K-steps, which then land while the current tile's epilogue runs.  The epilogue's LDS
-// scratch (BN coefficients + DPP-reduced column partials, SHRED) sits after the two stage buffers,
-// so it never aliases the prefetch.  4 waves (2x2), BK = 64, 2 blocks per CU.
-// K-loop per tile: stage kt lives in buffer kt & 1; s_waitcnt vmcnt counts retire exactly the
-// stage about to be read (NA + NB DMA instructions per stage per wave), then a barrier.
-template <int MODE, int BM, int BN, int WM, int WN, int EPI>
-__global__ void __launch_bounds__(NT, 2) igemm_stream_kernel(const IgemmParams p) {
-  constexpr int NW = NT / 64;
+// "Big" LDS-DMA kernel for the compute-bound FWD/DGRAD GEMMs (round 4 main loop): 4 waves (2x2) of
+// 128 x BN/2 wave tiles -- BM = 256 x BN = 256 (128x128 per wave, 256 fp32 accumulators per lane in
+// AGPRs) or 256 x 128 -- one block per CU, the shape hipBLASLt's fastest gfx950 bf16 kernels use
+// (profiles/r4_blas_kernels.txt: MT256x256x64 / MT256x128x64, MI16x16, 256 threads).  Per K-tile
+// (BK = 64) each wave issues 2 x TM x TN MFMAs; the LDS images hold 2 stages; the fragments are
+// double-buffered over the two 32-deep halves of the K-tile, so the LDS reads of one half run under
+// the MFMAs of the other, and there is ONE workgroup barrier per K-tile:
+//   half 0: read frags(t, 1)          | MFMA frags(t, 0)
+//           vmcnt(0) [stage t+1 landed] + lgkmcnt(0) + barrier [every wave done reading stage t]
+//   half 1: DMA stage t+2 into stage t's buffer; read frags(t+1, 0) | MFMA frags(t, 1)
+// The DMA of stage t+2 therefore has a whole K-tile of MFMAs (plus half of the next) to land.
+// Waits use the s_waitcnt builtin (not inline asm), so the compiler's own waitcnt pass sees them and
+// adds no conservative lgkmcnt waits of its own in front of the half-1 MFMAs (tools/gemm_lab).
+// Operand staging, swizzle, channel permutation and epilogue are those of igemm_dma_kernel.
+template <int N>
+__device__ __forceinline__ void wait_vm_b() {   // vmcnt(N) through the builtin (gfx9 simm16 encoding)
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void lds_sync_b() {   // lgkmcnt(0) + s_barrier, both visible to the compiler
+  __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));
+  __builtin_amdgcn_s_barrier();
+}
+constexpr int BIG_BM = 256;
+
+template <int MODE, int BN, int EPI, int EPD = 2>
+__global__ void __launch_bounds__(NT, 1) igemm_big_kernel(const IgemmParams p) {
+  constexpr int BM = BIG_BM, WM = 2, WN = 2, NW = 4;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int NA = BM / 8 / NW;   // DMA instructions (8 rows each) per wave per A stage
-  constexpr int NB = BN / 8 / NW;
-  constexpr int PER = NA + NB;      // per wave per stage
+  constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;   // LDS-DMA instructions (8 rows each) per wave
   static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
-  static_assert(WM * WN == NW && NA >= 1 && NB >= 1, "tiling");
-  static_assert(WTN % 32 == 0, "PAIR channel permutation works on 32-row groups");
+  static_assert(WTN % 32 == 0 && TN % 2 == 0, "PAIR channel permutation");
+
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* scratch = smem + 2 * STAGE;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid / WN, wc = wid % WN;
-  const int tiles = p.tiles_m * p.tiles_n;
-  const int nk = p.gk / BK;
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = lin / tiles_mn;
+  const int tl = lin - split * tiles_mn;
+  const int tile_n = tl % p.tiles_n;
+  const int tile_m = tl / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = split * p.ksplit;
+  const int nk = (min(p.gk, kbeg + p.ksplit) - kbeg) / BK;
+
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+  // loader slots: DMA instruction i of wave w fills LDS rows (w*NA + i)*8 .. +7; lane -> row
+  // + lane/8, position lane%8, loading global chunk (lane%8) ^ (row & 7)
+  const int gch = (lane & 7) ^ (lane >> 3);
+  int a_off[NA], a_y[NA], a_x[NA];
+  int b_off[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row0 = (wid * NA + i) * 8;
+    const int m = m0 + row0 + (lane >> 3);
+    const bool v = m < p.gm;
+    const int mm = v ? m : 0;
+    if constexpr (MODE == MODE_FWD) {
+      const int n = fdiv(mm, p.fd_PQ);
+      const int rem = mm - n * p.P * p.Q;
+      const int pp = fdiv(rem, p.fd_Q);
+      const int qq = rem - pp * p.Q;
+      const int yv = pp * p.stride - p.pad;
+      a_y[i] = v ? yv : -(1 << 28);
+      a_x[i] = qq * p.stride - p.pad;
+      a_off[i] = ((n * p.H + yv) * p.W + a_x[i]) * p.C + gch * 8;
+    } else {
+      const int n = fdiv(mm, p.fd_HW);
+      const int rem = mm - n * p.dH * p.dW;
+      const int hh = fdiv(rem, p.fd_W);
+      const int ww = rem - hh * p.dW;
+      const int yv = hh + p.offy;
+      a_y[i] = v ? yv : -(1 << 28);
+      a_x[i] = ww + p.offx;
+      a_off[i] = ((n * p.P + yv) * p.Q + a_x[i]) * p.K + gch * 8;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int rho = (wid * NB + i) * 8 + (lane >> 3);
+    const int n = n0 + chan_perm<true>(rho);
+    b_off[i] = n < p.gn ? n * p.gk + gch * 8 : -1;
+  }
+  // block-uniform tap / channel walk (C or K a multiple of BK)
   const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
-  const int gch = (lane & 7) ^ (lane >> 3);   // source chunk of this lane (XOR-swizzled image)
-
-  // per-tile loader state (rows of this wave's DMA instructions)
-  int a_off[NA], a_y[NA], a_x[NA], b_off[NB];
-  int kr = 0, ks = 0, kc = 0, k0 = 0;      // tap / channel walk of the next stage to issue
-  int ld_tile = -1, ld_k = 0;             // (tile, K-step) of the next stage to issue
-  auto setup = [&](int t) {
-    const int tile_n = t % p.tiles_n, tile_m = t / p.tiles_n;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int m = m0 + (wid * NA + i) * 8 + (lane >> 3);
-      const bool v = m < p.gm;
-      const int mm = v ? m : 0;
-      if constexpr (MODE == MODE_FWD) {
-        const int n = fdiv(mm, p.fd_PQ);
-        const int rem = mm - n * p.P * p.Q;
-        const int pp = fdiv(rem, p.fd_Q);
-        const int qq = rem - pp * p.Q;
-        const int yv = pp * p.stride - p.pad;
-        a_y[i] = v ? yv : -(1 << 28);
-        a_x[i] = qq * p.stride - p.pad;
-        a_off[i] = ((n * p.H + yv) * p.W + a_x[i]) * p.C + gch * 8;
-      } else {
-        const int n = fdiv(mm, p.fd_HW);
-        const int rem = mm - n * p.dH * p.dW;
-        const int hh = fdiv(rem, p.fd_W);
-        const int ww = rem - hh * p.dW;
-        const int yv = hh + p.offy;
-        a_y[i] = v ? yv : -(1 << 28);
-        a_x[i] = ww + p.offx;
-        a_off[i] = ((n * p.P + yv) * p.Q + a_x[i]) * p.K + gch * 8;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int n = n0 + chan_perm<true>((wid * NB + i) * 8 + (lane >> 3));
-      b_off[i] = n < p.gn ? n * p.gk + gch * 8 : -1;
-    }
-    kr = ks = kc = k0 = 0;
-    ld_tile = t;
-    ld_k = 0;
-  };
-  auto issue = [&](int buf) {   // DMA the stage (ld_tile, ld_k) into buffer buf, advance the walk
-    char* sA = smem + buf * STAGE;
-    char* sB = sA + A_BYTES;
+  int kc = kbeg % CIN, k0 = kbeg;
+  int ks = (kbeg / CIN) % p.S, kr = (kbeg / CIN) / p.S;
+  auto issue = [&](int s) {   // DMA of the K-tile at (k0, kr, ks, kc) into stage s, then advance
     int tap;
     if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
     else tap = -(kr * p.Q + ks) * p.K + kc;
+    char* dst = smem + s * STAGE;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       bool ok;
@@ -1895,15 +1297,15 @@ __global__ void __launch_bounds__(NT, 2) igemm_stream_kernel(const IgemmParams p
         ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
       else
         ok = (unsigned)(a_y[i] - kr) < (unsigned)p.P && (unsigned)(a_x[i] - ks) < (unsigned)p.Q;
-      const unsigned voff = ok ? (unsigned)(a_off[i] + tap) * 2u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(sA + (wid * NA + i) * 1024),
+      const int voff = ok ? (a_off[i] + tap) * 2 : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(dst + (wid * NA + i) * 1024),
                                                16, voff, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const unsigned voff = b_off[i] >= 0 ? (unsigned)(b_off[i] + k0) * 2u : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(sB + (wid * NB + i) * 1024),
-                                               16, voff, 0, 0, 0);
+      const int voff = b_off[i] >= 0 ? (b_off[i] + k0) * 2 : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsB, (__attribute__((address_space(3))) void*)(dst + A_BYTES + (wid * NB + i) * 1024), 16, voff, 0, 0, 0);
     }
     k0 += BK;
     kc += BK;
@@ -1911,60 +1313,53 @@ __global__ void __launch_bounds__(NT, 2) igemm_stream_kernel(const IgemmParams p
       kc = 0;
       if (++ks == p.S) { ks = 0; ++kr; }
     }
-    ++ld_k;
   };
 
   f32x4 acc[TN][TM];
-  int t = blockIdx.x;
-  if (t < tiles) {
-    setup(t);
-    issue(0);
-    if (nk > 1) issue(1);
-  }
-  for (; t < tiles; t += gridDim.x) {
-    const int tile_n = t % p.tiles_n, tile_m = t / p.tiles_n;
-    const int m0 = tile_m * BM, n0 = tile_n * BN;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  auto rd = [&](bf16x8(&fa)[TM], bf16x8(&fb)[TN], int kk, int s) {
+    const char* sA = smem + s * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      fa[i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      fb[j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+  };
+  auto mma = [&](bf16x8(&fa)[TM], bf16x8(&fb)[TN]) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-      const int buf = kt & 1;
-      // retire stage kt: the stage issued after it (kt + 1), if any, may stay in flight
-      if (kt + 1 < nk) wait_vm<PER>(); else wait_vm<0>();
-      lds_barrier();
-      const char* sA = smem + buf * STAGE;
-      const char* sB = sA + A_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        bf16x8 fa[TM], fb[TN];
-        const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 16 + (lane & 15), chunk));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 16 + (lane & 15), chunk));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      lds_barrier();   // every wave is done reading buffer buf
-      if (kt + 2 < nk) issue(buf);                  // stage kt + 2 of this tile
+      for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+  };
+
+  if (nk > 0) {
+    issue(0);
+    if (nk > 1) {
+      issue(1);
+      wait_vm_b<NA + NB>();
+    } else {
+      wait_vm_b<0>();
     }
-    // next tile's first stages land while this tile's epilogue runs
-    const int tn = t + gridDim.x;
-    if (tn < tiles) {
-      setup(tn);
-      issue(0);
-      if (nk > 1) issue(1);
+    lds_sync_b();
+    rd(fa0, fb0, 0, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int s = t & 1;
+      rd(fa1, fb1, 1, s);
+      mma(fa0, fb0);
+      if (t + 1 < nk) wait_vm_b<0>();
+      lds_sync_b();   // every wave's reads of stage s retired; stage t+1 landed for every wave
+      if (t + 2 < nk) issue(s);
+      if (t + 1 < nk) rd(fa0, fb0, 0, s ^ 1);
+      mma(fa1, fb1);
     }
-    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, 2, true>(p, acc, scratch, tid, m0, n0, tile_m, 0);
   }
-  wait_vm<0>();
+  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2339,23 +1734,10 @@ __global__ void __launch_bounds__(NT, 2) skinny_fwd_kernel(const IgemmParams p) 
       const int m = m0 + 16 * i + fr;
       if (nok && m < p.gm) *reinterpret_cast<f32x4*>(ws + (size_t)m * p.gn + n) = acc[i];
     }
-    if constexpr (!kSkFixup) return;
-    __shared__ int sk_flag;   // this kernel has no dynamic LDS
-    if (p.sk_cnt == nullptr || !splitk_ticket(p, tile_m * p.tiles_n + tile_n, &sk_flag)) return;
-    const float* ws0 = reinterpret_cast<const float*>(p.out);
-    const size_t slab = (size_t)p.gm * p.gn;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + 16 * i + fr;
-      if (!nok || m >= p.gm) continue;
-      f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < p.nsplit; ++sp)
-        t += sp == split ? acc[i] : *reinterpret_cast<const f32x4*>(ws0 + sp * slab + (size_t)m * p.gn + n);
-      acc[i] = t;
-    }
+    return;
   }
   if (!nok) return;
-  __bf16* out = reinterpret_cast<__bf16*>(p.nsplit > 1 ? p.sk_out : p.out);
+  __bf16* out = reinterpret_cast<__bf16*>(p.out);
   float bias[4] = {0.f, 0.f, 0.f, 0.f};
   if (p.bias) {
 #pragma unroll
@@ -2583,20 +1965,6 @@ __global__ void wt_transpose_multi_kernel(const unsigned short* __restrict__ src
 
 // ------------------------------------------------------------------------------------------------
 // host side
-// coalesced epilogue (igemm_epilogue_coal) for the 4-wave BM = 128 FWD / DGRAD kernels: A/B knob
-static Knob kn_epi_coal("epi_coal", 0);   // measured slower: profiles/r3_epi_coal_*.txt
-template <int MODE, int BM, int BN, int NTHR>
-static size_t coal_setup(IgemmParams& p, size_t smem) {
-  p.coal = 0;
-  if constexpr (MODE != MODE_WGRAD && NTHR == NT && BM == 128 && (BN == 128 || BN == 64)) {
-    if (kEpiCoal && kn_epi_coal.get() && p.nsplit == 1 && p.grp == 0 && p.gn % 8 == 0 && p.relu < 2) {
-      p.coal = 1;
-      smem = std::max(smem, (size_t)(BM * (BN + 4) + 7 * BN) * sizeof(float));
-    }
-  }
-  return smem;
-}
-
 template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
@@ -2611,7 +1979,6 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
     const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
     smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
   }
-  smem = coal_setup<MODE, BM, BN, NT>(p, smem);
   const int cin = MODE == MODE_FWD ? p.C : p.K;
   const bool unif = MODE != MODE_WGRAD && cin % BK == 0 && p.ksplit % BK == 0;
   int epi = EPI_PLAIN;
@@ -2669,77 +2036,8 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
 }
 
 // A/B knobs (torch.ops.pcmp.set_knob; tools/gemm_knob_ab.py)
-static Knob kn_splitk_red("splitk_red_v", 2);   // WGRAD split-K reduction: 1 = v1 column-only grid, 2 = split lanes
-static Knob kn_shortk_bm64("shortk_bm64", 0);   // FWD/DGRAD with gk <= N: 64x128 register-staged tiles (0 = off)
 
-// 8-wave (512-thread) register-staged WGRAD with 256x256 tiles (2x4 waves of 128x64): half the
-// operand bytes per MFMA of the 4-wave 128x128 tile.  Measured (profiles/r2_wgrad8_ab.txt): layer-3
-// 3x3 (256 filters x 2304 columns) 95 -> 86 us, layer-4 3x3 unchanged, the 1x1 filters 12-19 %
-// slower (short per-block reductions after the split), so it runs the 3x3 filters with 256 output
-// channels.  Knob wgrad8: 0 off, 1 that policy, 2 every filter with >= 256 x 256 (A/B).
-// In the whole step, where WGRAD shares the CUs with the DGRAD chain on the other stream, the
-// 4-wave kernel wins instead: wgrad8=0 ahead in 8 of 8 interleaved rounds (+0.2-0.9 %,
-// profiles/r2_knob_sweep.txt), so the 8-wave WGRAD is off by default.
-static Knob kn_wgrad8("wgrad8", 0);
 static Knob kn_wgrad_wgs("wgrad_wgs", 0);   // > 0: fixed split-K workgroup target (side-stream WGRADs)
-// dual BN-reduce DGRADs (EPI_BNR2) on the register-staged kernel: 128x128 tiles need 256 VGPRs and
-// spill 72 B per lane with that epilogue (48 B with the BatchNorm-backward fold); 128x64 tiles fit in
-// 192 VGPRs at the cost of one more read of the (short) A operand per extra column tile.  A/B knob.
-static Knob kn_bnr2_n64("bnr2_n64", 0);
-static bool use_bnr2_n64(int mode, const IgemmParams& p) {
-  return mode == MODE_DGRAD && p.bn_x2 && kn_bnr2_n64.get() && p.gm > 64 && p.gn > 64;
-}
-
-static bool use_wgrad8(const IgemmParams& p) {
-  const int k = kn_wgrad8.get();
-  if (!k || p.gm < 256 || p.gn < 256) return false;
-  return k == 2 || (p.R * p.S > 1 && p.gm <= 256);
-}
-
-// LDS-DMA WGRAD (igemm_wgrad_dma_kernel) for the 4-wave tiles; knob wgrad_dma: 0 = register-staged
-// igemm_kernel<MODE_WGRAD> (round 2), 1 = DMA kernel
-// 2 = per-shape policy: the DMA kernel for the filters it wins in isolation (profiles/r3_wgrad_dma_shape_ab.txt:
-// every 3x3, 6-10 %, and the 1x1s with <= 64k reduction rows -- layers 3-4 at B=256 -- 4-8 %), the
-// register-staged one for the long-reduction 1x1s of layers 1-2 (1-6 % faster there)
-static Knob kn_wgrad_dma("wgrad_dma", 0);   // 1 (all) in the whole step: 0.1-0.3 % slower in 3/3 rounds (profiles/r3_wgrad_dma_step_ab.txt)
-template <int BM, int BN>
-static bool launch_wgrad_dma(IgemmParams& p, hipStream_t st) {
-  const int mode = kn_wgrad_dma.get();
-  if (!mode || p.C % 8 != 0 || p.K % 8 != 0) return false;
-  if (mode == 2 && p.R * p.S == 1 && p.gk > 65536) return false;
-  p.tiles_m = ceil_div(p.gm, BM);
-  p.tiles_n = ceil_div(p.gn, BN);
-  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
-  const size_t smem = (size_t)2 * (BM + BN) * BK * 2;
-  auto kfn = &igemm_wgrad_dma_kernel<BM, BN, 2, 2>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024));
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p);
-  PCMP_LAUNCH_CHECK();
-  return true;
-}
-
-static void launch_wgrad8(IgemmParams& p, hipStream_t st) {
-  p.tiles_m = ceil_div(p.gm, 256);
-  p.tiles_n = ceil_div(p.gn, 256);
-  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
-  const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
-  const size_t smem = (size_t)(nk > 1 ? 2 : 1) * (256 + 256) * BK * 2;
-  auto kfn = &igemm_kernel<MODE_WGRAD, 256, 256, 2, 4, false, EPI_PLAIN, 2, 512>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024));
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kfn, dim3(grid), dim3(512), smem, st, p);
-  PCMP_LAUNCH_CHECK();
-}
-
 static int igemm8_mode() {
   static const int v = [] {
     const char* e = std::getenv("PCMP_IGEMM8");
@@ -2757,12 +2055,6 @@ static int igemm8_min_tiles() {
   return v;
 }
 
-// 8-wave LDS-DMA kernel with the wave-row-staggered READ / MFMA schedule (STAG): A/B knob
-static Knob kn_dma8_stag("dma8_stag", 0);   // measured null (profiles/r3_stagger_ab.txt)
-// early-prefetch schedule (SCHED 2): bit 0 the 4-wave kernels, bit 1 the 8-wave kernel.  Whole-step
-// A/B (profiles/r3_prio_pf2_ab.txt, 3 interleaved rounds): 12,213-12,283 -> 12,346-12,360 img/s
-static Knob kn_dma_pf2("dma_pf2", 3);
-
 template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB>
 static void launch_dma(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
@@ -2778,29 +2070,19 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
     const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
     smem = std::max(smem, (size_t)((NTHR / 64) * 16 * (NS * (BN / WN) + 4) + WM * NS * BN) * sizeof(float));
   }
-  smem = coal_setup<MODE, BM, BN, NTHR>(p, smem);
   int epi = EPI_PLAIN;
   if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
 #define PCMP_DMA_LAUNCH(E)                                                                              \
   do {                                                                                                \
-    constexpr bool can_deep = (E == EPI_BNR || E == EPI_BNR2) && NTHR == 256;                                        \
-    constexpr bool can_stag = NTHR == NT8 && WM == 2;                                                 \
-    auto kfn = (can_deep && (E == EPI_BNR2 ? kn_epi_depth_bnr2 : kn_epi_depth).get() >= 4)                         \
-                   ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>                                     \
-                                                     : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>; \
-    if (can_stag && kn_dma8_stag.get()) kfn = &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, can_stag ? 1 : 0>; \
-    if (kn_dma_pf2.get() & (NTHR == NT8 ? 2 : 1))                                                     \
-      kfn = (can_deep && (E == EPI_BNR2 ? kn_epi_depth_bnr2 : kn_epi_depth).get() >= 4)              \
-                ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4, 2>                        \
-                : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, 2>;                       \
+    constexpr bool can_deep = (E == EPI_BNR || E == EPI_BNR2) && NTHR == 256;                        \
+    auto kfn = (can_deep && (E == EPI_BNR2 ? kn_epi_depth_bnr2 : kn_epi_depth).get() >= 4)              \
+                   ? &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>                        \
+                   : &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>;                       \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
       for (auto f : {&igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2>,                       \
-                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>,                       \
-                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, can_stag ? 1 : 0>,       \
-                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 2, 2>,                    \
-                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4, 2>})                   \
+                     &igemm_dma_kernel<MODE, BM, BN, WM, WN, NTHR, MINB, E, 4>})                      \
         PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f),                          \
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
       attr_set = true;                                                                                \
@@ -2819,6 +2101,71 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
   }
 #undef PCMP_DMA_LAUNCH
   PCMP_LAUNCH_CHECK();
+}
+
+// Round-4 "big" kernel (igemm_big_kernel: 4 waves, 256 x 256 or 256 x 128 tiles, 1 block per CU).
+// Knob big (bitmask): 1 = 256x256 tiles for FWD/DGRAD grids of >= big_min256 such tiles, 2 = 256x128
+// tiles where 256x256 would leave too many CUs idle (>= big_min128 tiles).  Both need the
+// block-uniform tap walk (source channels % 64) and >= big_mink K-tiles.
+static Knob kn_big("big", 0);
+static Knob kn_big_min256("big_min256", 192);
+static Knob kn_big_min128("big_min128", 160);
+static Knob kn_big_mink("big_mink", 4);
+
+template <int MODE, int BN>
+static void launch_big(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, BIG_BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_big: partial-stats buffer too small");
+  TORCH_CHECK(p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0 && p.ksplit % BK == 0,
+              "igemm_big: needs the block-uniform tap walk");
+  TORCH_CHECK(p.nsplit == 1 || (!p.stats && !p.bn_x), "igemm_big: split-K only with the plain epilogue");
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  size_t smem = (size_t)2 * (BIG_BM + BN) * BK * 2;
+  const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
+  if (epi_red) {
+    const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
+    smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / 2) + 4) + 2 * NS * BN) * sizeof(float));
+  }
+  TORCH_CHECK(smem <= 160 * 1024, "igemm_big: LDS budget");
+  int epi = EPI_PLAIN;
+  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
+  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
+#define PCMP_BIG_LAUNCH(E, D)                                                                         \
+  do {                                                                                                \
+    auto kfn = &igemm_big_kernel<MODE, BN, E, D>;                                                     \
+    static bool attr_set = false;                                                                     \
+    if (!attr_set) {                                                                                  \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
+      attr_set = true;                                                                                \
+    }                                                                                                 \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p);                                       \
+  } while (0)
+  if constexpr (MODE == MODE_FWD) {
+    if (epi == EPI_STATS) PCMP_BIG_LAUNCH(EPI_STATS, 2);
+    else if (p.relu >= 2) PCMP_BIG_LAUNCH(EPI_GELU, 2);
+    else PCMP_BIG_LAUNCH(EPI_PLAIN, 2);
+  } else {
+    if (epi == EPI_BNR) PCMP_BIG_LAUNCH(EPI_BNR, 2);
+    else if (epi == EPI_BNR2) PCMP_BIG_LAUNCH(EPI_BNR2, 2);
+    else if (p.relu >= 2) PCMP_BIG_LAUNCH(EPI_GELU, 2);
+    else PCMP_BIG_LAUNCH(EPI_PLAIN, 2);
+  }
+#undef PCMP_BIG_LAUNCH
+  PCMP_LAUNCH_CHECK();
+}
+
+// 0: not used; 256 / 128: the tile width of the big kernel for this GEMM
+static int use_big(int mode, const IgemmParams& p) {
+  const int kb = kn_big.get();
+  if (!kb || mode == MODE_WGRAD || p.nsplit != 1 || p.fold_x || p.act_sc) return 0;
+  const int cin = mode == MODE_FWD ? p.C : p.K;
+  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < kn_big_mink.get()) return 0;
+  const int tm = ceil_div(p.gm, BIG_BM);
+  if ((kb & 1) && p.gn >= 256 && tm * ceil_div(p.gn, 256) >= kn_big_min256.get()) return 256;
+  if ((kb & 2) && p.gn >= 128 && tm * ceil_div(p.gn, 128) >= kn_big_min128.get()) return 128;
+  return 0;
 }
 
 // 4-wave LDS-DMA kernel (2 blocks per CU) in place of the register-staged 4-wave kernel for the
@@ -2853,57 +2200,6 @@ static int use_dma4(int mode, const IgemmParams& p) {
   return 1;
 }
 
-// persistent streaming kernel (FWD/DGRAD, short reductions): grid = min(tiles, kn_stream_grid)
-// Measured (tools/gemm_knob_ab.py, profiles/r2_stream_kernel_ab.txt): the streaming kernel wins only
-// on the wide short-K DGRAD + BN-backward GEMMs (layer-1 256->64 351 -> 343 us, layer-2 512->128
-// 209 -> 203, layer-3 1024->256 130 -> 122) and loses on the FWD + statistics ones (layer-1 64->256
-// 153 -> 185 us), so by default it runs DGRAD with >= 256 output channels and <= 4 K-steps.
-// Whole-step A/B on the round-2 build (profiles/r2_knob_sweep.txt): with the BNR2 DGRADs moved to
-// the one-tile kernels, the streaming kernel no longer pays on the remaining BNR shapes either
-// (stream_maxk=0 ahead of 4 in 5 of 5 interleaved rounds, +0.7 % mean), so it is off by default.
-static Knob kn_stream_maxk("stream_maxk", 0);     // use it for gk/BK <= N K-steps (0 = off)
-static Knob kn_stream_fwd("stream_fwd", 0);       // 1: also for FWD
-static Knob kn_stream_grid("stream_grid", 512);   // resident blocks (2 per CU)
-// dual BN-reduce DGRADs (EPI_BNR2): the streaming kernel spills with that epilogue (256 VGPRs +
-// 112 B scratch per lane) and runs 19-29 % slower than the one-tile kernels: off by default
-// (profiles/r2_bnr2_ab.txt)
-static Knob kn_stream_bnr2("stream_bnr2", 0);
-
-template <int MODE, int BM, int BN, int WM, int WN>
-static void launch_stream(IgemmParams& p, hipStream_t st) {
-  p.tiles_m = ceil_div(p.gm, BM);
-  p.tiles_n = ceil_div(p.gn, BN);
-  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_stream: partial-stats buffer too small");
-  TORCH_CHECK(p.nsplit == 1 && p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0,
-              "igemm_stream: needs the block-uniform tap walk and no split-K");
-  const int tiles = p.tiles_m * p.tiles_n;
-  const int grid = std::max(1, std::min(tiles, kn_stream_grid.get()));
-  const size_t smem = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
-  int epi = EPI_PLAIN;
-  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
-  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
-#define PCMP_STREAM_LAUNCH(E)                                                                          \
-  do {                                                                                                 \
-    auto kfn = &igemm_stream_kernel<MODE, BM, BN, WM, WN, E>;                                          \
-    static bool attr_set = false;                                                                      \
-    if (!attr_set) {                                                                                   \
-      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                           \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));     \
-      attr_set = true;                                                                                 \
-    }                                                                                                  \
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p);                                        \
-  } while (0)
-  if constexpr (MODE == MODE_FWD) {
-    if (epi == EPI_STATS) PCMP_STREAM_LAUNCH(EPI_STATS); else PCMP_STREAM_LAUNCH(EPI_PLAIN);
-  } else {
-    if (epi == EPI_BNR) PCMP_STREAM_LAUNCH(EPI_BNR);
-    else if (epi == EPI_BNR2) PCMP_STREAM_LAUNCH(EPI_BNR2);
-    else PCMP_STREAM_LAUNCH(EPI_PLAIN);
-  }
-#undef PCMP_STREAM_LAUNCH
-  PCMP_LAUNCH_CHECK();
-}
-
 // halo-tiled direct conv for the layer-1 3x3 / stem shapes: bit 0 FWD, bit 1 every DGRAD variant,
 // bit 2 the overlapped BN-backward DGRAD.  DGRAD is off by default: its BN-backward epilogue loads
 // stall the one wave per SIMD (profiles/r2_halo_conv.txt)
@@ -2921,7 +2217,7 @@ static bool halo_dgrad_ovl(const IgemmParams& p) {
 static bool halo_geom(int mode, const IgemmParams& p, HaloGeom& g) {
   const int hk = kn_halo.get();
   if ((mode == MODE_FWD && !(hk & 1)) || (mode == MODE_DGRAD && !(hk & 6)) || mode == MODE_WGRAD || p.nsplit != 1 || p.stride != 1 || p.R != p.S || p.gn != 64 ||
-      p.grp != 0 || p.sub || p.relu >= 2)
+      p.sub || p.relu >= 2)
     return false;
   int CS, pad;
   if (mode == MODE_FWD) {
@@ -3011,18 +2307,6 @@ static void launch_halo(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
-// 0: not used; 1: 128x128; 2: 128x64 (narrow outputs)
-static int use_stream(int mode, const IgemmParams& p) {
-  const int mk = kn_stream_maxk.get();
-  if (mk <= 0 || mode == MODE_WGRAD || p.nsplit != 1 || p.relu >= 2) return 0;   // no GELU epilogue there
-  if (mode == MODE_FWD && !kn_stream_fwd.get()) return 0;
-  const int cin = mode == MODE_FWD ? p.C : p.K;
-  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK > mk || p.gm < 4096) return 0;
-  if (mode == MODE_DGRAD && !kn_stream_fwd.get() && p.gn < 256) return 0;
-  if (mode == MODE_DGRAD && p.bn_x2 && !kn_stream_bnr2.get()) return 0;
-  return p.gn <= 64 ? 2 : 1;
-}
-
 // 8-wave LDS-DMA kernel eligibility: FWD/DGRAD with the block-uniform tap walk (source channels a
 // multiple of BK), no split-K, enough K-tiles for the phase pipeline, and a grid that still covers
 // most CUs with BM = 256 tiles: >= 160 tiles (ResNet-50 layer3 at B=256 has 196 and runs 20-28 %
@@ -3064,7 +2348,6 @@ static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
     BN = p.gn <= 64 ? 64 : 128;
     return;
   }
-  if (use_wgrad8(p)) { BM = 256; BN = 256; return; }
   const int w = wgrad_wide(p);
   if (w == 1) { BM = 64; BN = 256; return; }
   if (w == 2) { BM = 256; BN = 64; return; }
@@ -3081,7 +2364,6 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
     return e ? std::atoi(e) : 1;
   }();
   if (!(mode != MODE_WGRAD && p.nsplit == 1 && p.gm > 64 && p.gn > 64)) return false;
-  if (kn_shortk_bm64.get() > 0 && p.gk <= kn_shortk_bm64.get()) return true;
   return v && ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
 }
 
@@ -3089,7 +2371,7 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 static int igemm_bm(int mode, const IgemmParams& p) {
   if (p.fold_x || p.act_sc) return 128;
   if (use_halo(mode, p)) return HALO_BM;
-  if (use_stream(mode, p)) return 128;
+  if (use_big(mode, p)) return BIG_BM;
   if (use_igemm8(mode, p)) return BM8;
   if (use_bm64_smallgrid(mode, p)) return 64;
   if (use_dma4(mode, p) == 3) return 256;
@@ -3102,7 +2384,6 @@ template <int MODE, int BM, int BN, int WM, int WN, int FOLD>
 static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
   p.tiles_m = ceil_div(p.gm, BM);
   p.tiles_n = ceil_div(p.gn, BN);
-  p.coal = 0;
   TORCH_CHECK(MODE == MODE_WGRAD || !p.stats || p.tiles_m <= p.stats_cap, "igemm fold: partial-stats buffer too small");
   const int grid = p.tiles_m * p.tiles_n * p.nsplit;
   const int nk = ceil_div(std::min(p.ksplit, p.gk), BK);
@@ -3149,7 +2430,7 @@ static void launch_fold(IgemmParams& p, hipStream_t st) {
     TORCH_CHECK(p.fold_x && !p.act_sc, "igemm fold: DGRAD folds only the BatchNorm-backward dz");
     TORCH_CHECK(p.R == 1 && p.S == 1 && p.stride == 1 && p.K % BK == 0 && p.nsplit == 1 && p.ksplit % BK == 0,
                 "igemm fold: DGRAD of a 1x1 stride-1 conv with K % 64 == 0, no split");
-    if (p.gn <= 64 || use_bnr2_n64(MODE, p)) launch_fold_cfg<MODE, 128, 64, 2, 2, 1>(p, st);
+    if (p.gn <= 64) launch_fold_cfg<MODE, 128, 64, 2, 2, 1>(p, st);
     else launch_fold_cfg<MODE, 128, 128, 2, 2, 1>(p, st);
   } else if constexpr (MODE == MODE_FWD) {
     TORCH_CHECK(p.act_sc && p.act_sh && !p.fold_x, "igemm fold: FWD folds only the BatchNorm-forward activation");
@@ -3184,15 +2465,14 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
   if (p.fold_x || p.act_sc) { launch_fold<MODE>(p, st); return; }
   if constexpr (MODE != MODE_WGRAD) {
     if (use_halo(MODE, p)) { launch_halo<MODE>(p, st); return; }
-    switch (use_stream(MODE, p)) {
-      case 1: launch_stream<MODE, 128, 128, 2, 2>(p, st); return;
-      case 2: launch_stream<MODE, 128, 64, 2, 2>(p, st); return;
+    switch (use_big(MODE, p)) {
+      case 256: launch_big<MODE, 256>(p, st); return;
+      case 128: launch_big<MODE, 128>(p, st); return;
       default: break;
     }
     if (use_igemm8(MODE, p) == 256) { launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st); return; }
   }
   if constexpr (MODE == MODE_WGRAD) {
-    if (use_wgrad8(p)) { launch_wgrad8(p, st); return; }
     const int w = wgrad_wide(p);
     if (w == 1) { launch_cfg<MODE, 64, 256, 1, 4>(p, st); return; }
     if (w == 2) { launch_cfg<MODE, 256, 64, 4, 1>(p, st); return; }
@@ -3206,14 +2486,6 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
       default: break;
     }
   }
-  if constexpr (MODE == MODE_WGRAD) {
-    if (p.gm > 32) {
-      bool done;
-      if (p.gm <= 64) done = p.gn <= 64 ? launch_wgrad_dma<64, 64>(p, st) : launch_wgrad_dma<64, 128>(p, st);
-      else done = p.gn <= 64 ? launch_wgrad_dma<128, 64>(p, st) : launch_wgrad_dma<128, 128>(p, st);
-      if (done) return;
-    }
-  }
   // tile choice: BN=64 for narrow outputs, BM=32/64 for short M (linear at small batch)
   if (p.gm <= 32) {
     if (p.gn <= 64) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
@@ -3222,7 +2494,7 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
     if (p.gn <= 64) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
     else launch_cfg<MODE, 64, 128, 2, 2>(p, st);
   } else {
-    if (p.gn <= 64 || use_bnr2_n64(MODE, p)) launch_cfg<MODE, 128, 64, 2, 2>(p, st);
+    if (p.gn <= 64) launch_cfg<MODE, 128, 64, 2, 2>(p, st);
     else launch_cfg<MODE, 128, 128, 2, 2>(p, st);
   }
 }
@@ -3243,7 +2515,8 @@ static Knob kn_plan_nsplit("plan_nsplit", 0); // tests: >= 1 (with plan_force) a
 
 struct GemmPlan {
   int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves),
-                // 3 = register-staged 64x64, 4 = register-staged 32x64, 5 = DMA 128x64 (small-M inference convs)
+                // 3 = register-staged 64x64, 4 = register-staged 32x64, 5 = DMA 128x64 (small-M inference convs),
+                // 6 = skinny FWD, 7 / 8 = big 256x256 / 256x128 (4 waves, 1 block per CU)
   int nsplit;
 };
 static const char* plan_kind_name(int k) {
@@ -3254,30 +2527,13 @@ static const char* plan_kind_name(int k) {
     case 4: return "reg32x64";
     case 5: return "dma128x64";
     case 6: return "skinny64x64";
+    case 7: return "big256x256";
+    case 8: return "big256x128";
     default: return "default";
   }
 }
 
 int* counter_slots(int n, int device);
-// in-kernel split-K fixup (IgemmParams::sk_cnt) instead of the splitk_epilogue launch: 1 = on.
-// Measured off (profiles/r3_sk_fixup_ab.txt, 2 interleaved rounds): batch-1 inference p50 0.549-0.554
-// -> 0.659-0.672 ms, BERT-base 3,691-3,739 -> 3,615-3,644 samples/s, ResNet-50 unchanged.  The tile's
-// last arriver reads every other split's fp32 slab serially (up to 32 splits at batch 1), which the
-// separate epilogue launch spreads over the whole chip.
-static Knob kn_sk_fixup("sk_fixup", 0);
-
-// arm the fixup for a FWD/DGRAD split launch writing bf16 `out`; false: use splitk_epilogue_kernel
-static bool arm_splitk_fixup(IgemmParams& p, void* out, int device) {
-  if (!kSkFixup || !kn_sk_fixup.get() || p.nsplit <= 1) return false;
-  // counter index = tile_m * tiles_n + tile_n over the launched kernel's tiles; the smallest tiles
-  // any FWD/DGRAD kernel uses are 32 x 64
-  int* cnt = counter_slots(ceil_div(p.gm, 32) * ceil_div(p.gn, 64), device);
-  if (!cnt) return false;
-  p.sk_cnt = cnt;
-  p.sk_out = out;
-  return true;
-}
-
 template <int MODE>
 static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
   const int kq = pl.kind == 6 ? 32 : BK;   // K granularity of the kernel
@@ -3289,11 +2545,9 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   p.ksplit = steps_per * kq;
   const __bf16* resid = p.resid;
   at::Tensor ws;
-  bool fixup = false;
   if (nsplit > 1) {
     ws = at::empty({(int64_t)nsplit, (int64_t)p.gm * p.gn}, fopts);
     p.out = ws.data_ptr();
-    fixup = arm_splitk_fixup(p, out, ws.get_device());
   } else {
     p.out = out;
   }
@@ -3302,11 +2556,13 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   else if (pl.kind == 3) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
   else if (pl.kind == 4) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
   else if (pl.kind == 5) launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st);
+  else if (pl.kind == 7) launch_big<MODE, 256>(p, st);
+  else if (pl.kind == 8) launch_big<MODE, 128>(p, st);
   else if (pl.kind == 6) {
     if constexpr (MODE == MODE_FWD) launch_skinny(p, st);
     else TORCH_CHECK(false, "skinny kernel is FWD only");
   } else dispatch<MODE>(p, st);
-  if (nsplit > 1 && !fixup) {
+  if (nsplit > 1) {
     const int64_t n = (int64_t)p.gm * p.gn;
     const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out,
@@ -3384,6 +2640,8 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
       if (ns > 1 && ksteps / ns < 4) continue;
       cands.push_back({1, ns});
       if (p.gn >= 256) cands.push_back({2, ns});
+      if (kn_big.get() & 1 && p.gn >= 256) cands.push_back({7, ns});
+      if (kn_big.get() & 2 && p.gn >= 128) cands.push_back({8, ns});
     }
   }
   if (force >= 0) {
@@ -3425,16 +2683,9 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
 
 
 // ------------------------------------------------------------------------------------------------
-// In-kernel BN-statistics group reduction (IgemmParams::grp): arrival counters come from a
-// per-device ring over one persistent zero-initialised int32 buffer (the last arriver of each group
-// resets its counter, so a slot is zero again once the kernel that used it has finished; the ring
-// holds 2^20 slots, a ResNet-50 step uses ~6,000, and the host runs at most a couple of steps
-// ahead).  Knob bn_group: 0 = off (per-tile rows + partials_reduce launch, round 1; the default).
-// Measured (profiles/r2_bn_group_ab.txt): correct and bitwise reproducible, but ResNet-50 fell from
-// 11,750 to 6,720 img/s -- each last arriver walks up to 98 rows per (channel, sum) at one dependent
-// L2 round trip per row, which lengthens every statistics-producing conv by far more than the
-// ~5 us partials_reduce launch it removes (the round-1 single-launch finalize failed the same way).
-static Knob kn_bn_group("bn_group", 0);
+// Zero-initialised int32 ticket counters for in-launch hand-offs (bn.hip's one-launch finalize,
+// knob bn_fused_fin): a per-device ring over one persistent buffer; the last user of a slot resets
+// it, so a slot is zero again once the kernel that used it has finished.
 constexpr int kCounterSlots = 1 << 20;
 
 int* counter_slots(int n, int device) {
@@ -3457,29 +2708,6 @@ int* counter_slots(int n, int device) {
   int* r = e.first + e.second;
   e.second += n;
   return r;
-}
-
-// group size for T row tiles: <= 64 reduced rows, >= 16 tiles per group
-static int bn_group_size(int T) { return std::max(16, ceil_div(T, 64)); }
-
-// set up the group reduction for a single-launch statistics producer; returns the reduced [G][2][gn]
-// fp64 tensor(s) (undefined when grouping is off or not worth it)
-static void setup_bn_group(IgemmParams& p, int T, const at::Tensor& like, at::Tensor& red, at::Tensor* red2) {
-  if (!kBnGroup || !kn_bn_group.get() || T <= 64) return;
-  const int grp = bn_group_size(T);
-  const int G = ceil_div(T, grp);
-  const int tiles_n_max = ceil_div(p.gn, 64);   // every kernel's column tile is >= 64 wide
-  int* cnt = counter_slots(G * tiles_n_max, like.get_device());
-  if (!cnt) return;
-  auto dopts = like.options().dtype(at::kDouble);
-  red = at::empty({G, 2, (int64_t)p.gn}, dopts);
-  p.grp = grp;
-  p.grp_cnt = cnt;
-  p.grp_red = red.data_ptr<double>();
-  if (red2) {
-    *red2 = at::empty({G, 2, (int64_t)p.gn}, dopts);
-    p.grp_red2 = red2->data_ptr<double>();
-  }
 }
 
 static unsigned tensor_bytes(const at::Tensor& t);
@@ -3530,9 +2758,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.bn_x2 = nullptr; p.bn_mean2 = nullptr; p.bn_istd2 = nullptr; p.bn_msc = nullptr; p.bn_msh = nullptr;
   p.bn_mbits = nullptr;
   p.stats_cap = 0;
-  p.grp = 0; p.grp_cnt = nullptr; p.grp_red = nullptr; p.grp_red2 = nullptr;
-  p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1; p.coal = 0;
-  p.sk_cnt = nullptr; p.sk_out = nullptr;
+  p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
   p.fold_x = nullptr; p.fold_coef = nullptr; p.fold_lds = 0;
   p.act_sc = nullptr; p.act_sh = nullptr;
 }
@@ -3584,17 +2810,16 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
   }
   const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
   const int BNsel = p.gn <= 64 ? 64 : 128;
-  at::Tensor stats, stats_red;
+  at::Tensor stats;
   if (want_stats) {
     p.stats_cap = ceil_div(p.gm, igemm_bm(MODE_FWD, p));
     stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
     p.stats = ptr<float>(stats);
-    setup_bn_group(p, p.stats_cap, x, stats_red, nullptr);
   }
   auto st = cur_stream();
   if (in_scale) {   // BatchNorm-forward fold (act_sc / act_sh set above)
     dispatch<MODE_FWD>(p, st);
-    if (want_stats) return {y, stats_red.defined() ? stats_red : stats};
+    if (want_stats) return {y, stats};
     return {y};
   }
   if (plain_gemm_eligible<MODE_FWD>(p)) {
@@ -3626,9 +2851,7 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
     const int64_t n = (int64_t)p.gm * p.gn;
     auto ws = at::empty({(int64_t)nsplit, n}, x.options().dtype(at::kFloat));
     p.out = ws.data_ptr();
-    const bool fixup = arm_splitk_fixup(p, y.data_ptr(), x.get_device());
     dispatch<MODE_FWD>(p, st);
-    if (fixup) return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
     const int blocks = (int)((n / 4 + 255) / 256);
     hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<__bf16>(y),
                        p.bias, p.resid, n, p.gn, nsplit, p.relu, p.aux);
@@ -3636,7 +2859,7 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
     return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
   }
   dispatch<MODE_FWD>(p, st);
-  if (want_stats) return {y, stats_red.defined() ? stats_red : stats};
+  if (want_stats) return {y, stats};
   return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
 }
 
@@ -3839,7 +3062,7 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     run_plan<MODE_DGRAD>(p, pl, ptr<__bf16>(dx), fopts, st);
     return {dx};
   }
-  at::Tensor part, part2, red, red2;
+  at::Tensor part, part2;
   if (bn) {
     set_bn(p);   // before igemm_bm: the kernel choice depends on the epilogue variant
     const int T = ceil_div(p.gm, igemm_bm(MODE_DGRAD, p));
@@ -3847,14 +3070,9 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
     p.stats_cap = T;
     p.stats = ptr<float>(part);
     if (two) { part2 = at::empty({T, 2, C}, fopts); p.stats2 = ptr<float>(part2); }
-    setup_bn_group(p, T, dy, red, two ? &red2 : nullptr);
   }
   dispatch<MODE_DGRAD>(p, st);
   if (!bn) return {dx};
-  if (red.defined()) {
-    if (two) return {dx, red, red2};
-    return {dx, red};
-  }
   if (two) return {dx, part, part2};
   return {dx, part};
 }
@@ -3957,7 +3175,7 @@ static void wgrad_run(IgemmParams p, int nsplit, float* out, bool accumulate, co
   auto ws = at::empty({(int64_t)nsplit, n}, fopts);
   p.out = ws.data_ptr();
   dispatch<MODE_WGRAD>(p, st);
-  if (kn_splitk_red.get() == 2 && n / 4 < (1ll << 31)) {
+  if (n / 4 < (1ll << 31)) {
     const int n4 = (int)(n / 4);
     const int SL = nsplit <= 8 ? 1 : (nsplit <= 32 ? 4 : 16);
     const int cols = 256 / SL;
@@ -4002,7 +3220,7 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   auto& cache = g_wsplit_cache;
   char key[160];
   snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
-           (int)use_wgrad8(p));
+           0);
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
@@ -4133,14 +3351,9 @@ int64_t autotune_load(std::vector<std::string> entries) {
   return n;
 }
 
-// epilogue variants compiled into this build (PCMP_SK_FIXUP / PCMP_EPI_COAL / PCMP_BN_GROUP)
-std::vector<std::string> build_features() {
-  std::vector<std::string> f;
-  if (kSkFixup) f.push_back("sk_fixup");
-  if (kEpiCoal) f.push_back("epi_coal");
-  if (kBnGroup) f.push_back("bn_group");
-  return f;
-}
+// optional compiled-in kernel variants of this build (none since round 4: the measured-losing
+// epilogue variants sk_fixup / epi_coal / bn_group were removed, docs/PERF_NOTES.md)
+std::vector<std::string> build_features() { return {}; }
 
 }  // namespace pcmp
 

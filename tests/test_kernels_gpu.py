@@ -589,161 +589,10 @@ def test_small_m_plan_kinds_match_reference(gpu, kind):
         ops.set_knob("plan_force", -1)
 
 
-@pytest.mark.parametrize("kind", [1, 3, 4, 5, 6])
-def test_splitk_in_kernel_fixup(gpu, kind):
-    """Split-K GEMMs whose last-arriving split sums the partial tiles in split order and runs the
-    epilogue (knob sk_fixup=1; compiled in only with -DPCMP_SK_FIXUP=1, otherwise the knob falls back
-    to the separate launch) == the separate splitk_epilogue launch (sk_fixup=0, default) == the fp32
-    reference, bitwise repeatable; FWD (bias / residual / ReLU) and a plain Linear DGRAD."""
-    torch.manual_seed(5)
-    ops = _ops()
-    prev_force = ops.set_knob("plan_force", kind)
-    # forced plans are re-autotuned on every call: pin the split count too, or two calls may pick
-    # different splits (different fp32 summation order) and the repeatability check is meaningless
-    prev_ns = ops.set_knob("plan_nsplit", 4)
-    try:
-        for (H, C, K, R, s, use_res) in [(7, 2048, 512, 1, 1, False), (7, 512, 2048, 1, 1, True),
-                                         (1, 2048, 1000, 1, 1, False), (14, 256, 256, 3, 1, False)]:
-            if kind in (1, 5) and R > 1:
-                continue
-            p = R // 2
-            x = rnd(1, H, H, C, dev=gpu)
-            w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
-            bias = torch.randn(K, device=gpu)
-            Ho = (H + 2 * p - R) // s + 1
-            res = rnd(1, Ho, Ho, K, dev=gpu) if use_res else None
-            yr = ref.conv_fwd(x, w, s, p, bias, res, True, False)[0]
-            ys = {}
-            for fx in (0, 1):
-                prev = ops.set_knob("sk_fixup", fx)
-                try:
-                    ys[fx] = ops.conv_fwd(x, w, s, p, bias, res, True, False)[0]
-                    if fx:
-                        assert torch.equal(ys[fx], ops.conv_fwd(x, w, s, p, bias, res, True, False)[0])
-                finally:
-                    ops.set_knob("sk_fixup", prev)
-                close(ys[fx], yr)
-            close(ys[1], ys[0], 1e-2, 1e-2)
-    finally:
-        ops.set_knob("plan_force", prev_force)
-        ops.set_knob("plan_nsplit", prev_ns)
-    # Linear DGRAD through the plain-GEMM planner (K-splits for the N = 768 outputs)
-    dy = rnd(4096, 1, 1, 768, dev=gpu)
-    wl = rnd(768, 1, 1, 3072, dev=gpu, scale=0.02)
-    dres = rnd(4096, 1, 1, 3072, dev=gpu)
-    close(ops.conv_dgrad(dy, wl, 1, 1, 1, 0, dres), ref.conv_dgrad(dy, wl, 1, 1, 1, 0, dres))
-
-
-@pytest.mark.parametrize("mode", ["fwd", "dgrad_bnr", "dgrad_bnr2"])
-def test_bn_group_reduction_in_kernel(gpu, mode):
-    """The last-arriving block of each row-tile group sums the group's BN-statistics rows in fixed
-    order (fp64 [G,2,C] out, no partials_reduce launch): equal to the per-tile rows' sum, bitwise
-    reproducible, and identical in the finalize result.  (Compiled in only with -DPCMP_BN_GROUP=1:
-    the knob measured slower and stays off, and unused epilogue code costs the other kernels.)"""
-    torch.manual_seed(3)
-    ops = _ops()
-    if "bn_group" not in ops.build_features():
-        pytest.skip("BN group reduction not compiled into this build (PCMP_BN_GROUP=0)")
-    N, H, C, K = 32, 56, 64, 256   # 100,352 rows -> 784 tiles of 128 -> 49 groups of 16
-    x = rnd(N, H, H, C, dev=gpu)
-    w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
-    dy = rnd(N, H, H, K, dev=gpu)
-    xb = rnd(N, H, H, C, dev=gpu)
-
-    def run(group):
-        ops.set_knob("bn_group", group)
-        try:
-            if mode == "fwd":
-                return ops.conv_fwd(x, w, 1, 0, None, None, False, True)[1:]
-            mean = torch.zeros(C, device=gpu)
-            istd = torch.ones(C, device=gpu)
-            two = mode == "dgrad_bnr2"
-            out = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, None, None, xb, mean, istd,
-                                     x if two else None, mean if two else None, istd if two else None, None, None)
-            return out[1:]
-        finally:
-            ops.set_knob("bn_group", 0)
-
-    a, b, c = run(1), run(1), run(0)   # (knob default is 0; the path stays tested)
-    for pa, pb, pc in zip(a, b, c):
-        assert pa.dtype == torch.float64 and pa.shape[0] <= 64 and pc.dtype == torch.float32
-        assert torch.equal(pa, pb)
-        torch.testing.assert_close(pa.sum(0), pc.double().sum(0), rtol=1e-5, atol=1e-3)
-
-
-@pytest.mark.parametrize("shape", [(4, 14, 14, 64, 96, 3, 1, 1), (2, 28, 28, 128, 256, 1, 2, 0),
-                                   (8, 7, 7, 512, 2048, 1, 1, 0), (3, 9, 9, 40, 72, 3, 2, 1),
-                                   (16, 8, 8, 64, 48, 1, 1, 0)])
-def test_wgrad_dma_kernel_matches_register_kernel(gpu, shape):
-    """LDS-DMA WGRAD (knob wgrad_dma, default on) == register-staged WGRAD == fp32 reference,
-    including tile tails, stride 2, 3x3 padding, split-K and accumulate."""
-    N, H, W, C, K, R, s, p = shape
-    torch.manual_seed(11)
-    ops = _ops()
-    P, Q = (H + 2 * p - R) // s + 1, (W + 2 * p - R) // s + 1
-    dy = rnd(N, P, Q, K, dev=gpu)
-    x = rnd(N, H, W, C, dev=gpu)
-    outs = {}
-    for v in (0, 1):
-        out = torch.full((K, R, R, C), 0.25, device=gpu)
-        prev = ops.set_knob("wgrad_dma", v)
-        try:
-            ops.conv_wgrad(dy, x, out, R, R, s, p, True)
-        finally:
-            ops.set_knob("wgrad_dma", prev)
-        outs[v] = out
-    outr = torch.full((K, R, R, C), 0.25, device=gpu)
-    ref.conv_wgrad(dy, x, outr, R, R, s, p, True)
-    close(outs[1], outr, rtol=1e-2, atol=5e-2)
-    close(outs[1], outs[0], rtol=1e-3, atol=1e-2)
-
-
-@pytest.mark.parametrize("v", [1, 2])
-def test_wgrad8_kernel_knob(gpu, v):
-    """The 8-wave 256x256 WGRAD kernel (off by default, knob wgrad8) == the fp32 reference."""
-    torch.manual_seed(7 + v)
-    ops = _ops()
-    N, H, C, K, R = 8, 14, 256, 256, 3 if v == 1 else 1
-    x = rnd(N, H, H, C, dev=gpu)
-    dy = rnd(N, H, H, K, dev=gpu)
-    out = torch.empty(K, R, R, C, device=gpu)
-    outr = torch.empty_like(out)
-    try:
-        ops.set_knob("wgrad8", v)
-        ops.conv_wgrad(dy, x, out, R, R, 1, R // 2, False)
-    finally:
-        ops.set_knob("wgrad8", 0)
-    ref.conv_wgrad(dy, x, outr, R, R, 1, R // 2, False)
-    close(out, outr, rtol=1e-2, atol=1e-1)
-
-
-def test_dgrad_bnr_stream_kernel_knob(gpu):
-    """The persistent streaming kernel (off by default, knob stream_maxk) == the one-tile kernel on a
-    wide short-K DGRAD + BN-backward reduction with residual and mask bits."""
-    torch.manual_seed(6)
-    ops = _ops()
-    N, H, C, K = 16, 28, 256, 64
-    w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
-    dy = rnd(N, H, H, K, dev=gpu)
-    xb, res = rnd(N, H, H, C, dev=gpu), rnd(N, H, H, C, dev=gpu)
-    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
-    bits = torch.randint(0, 256, (N * H * H * C // 8,), device=gpu, dtype=torch.uint8)
-    outs = []
-    try:
-        for v in (0, 4):
-            ops.set_knob("stream_maxk", v)
-            r = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, res, None, xb, mean, istd, None, None, None, None, None, None, bits)
-            outs.append([t.clone() for t in r])
-    finally:
-        ops.set_knob("stream_maxk", 0)
-    assert torch.equal(outs[0][0], outs[1][0])
-    torch.testing.assert_close(outs[0][1].double().sum(0), outs[1][1].double().sum(0), rtol=1e-5, atol=1e-3)
-
-
 def test_dgrad_bnr2_kernel_variants(gpu):
     """Dual BN-reduce DGRAD (the DGRAD into a block tail with a downsample BN): the one-tile kernel at
-    epilogue depth 2 (default), at depth 4, and the streaming kernel (knobs stream_maxk, stream_bnr2;
-    off by default) give the same masked gradient bitwise and the same BN-backward sums."""
+    epilogue depth 2 (default) and at depth 4 give the same masked gradient bitwise and the same
+    BN-backward sums."""
     torch.manual_seed(5)
     ops = _ops()
     N, H, C, K = 16, 28, 256, 64          # 12,544 rows: wide short-K GEMM (gk = 64, gn = 256)
@@ -755,18 +604,14 @@ def test_dgrad_bnr2_kernel_variants(gpu):
     bits = torch.randint(0, 256, (N * H * H * C // 8,), device=gpu, dtype=torch.uint8)
     outs = []
     try:
-        for knobs in ({}, {"epi_depth_bnr2": 4}, {"stream_maxk": 4, "stream_bnr2": 1}):
+        for knobs in ({}, {"epi_depth_bnr2": 4}):
             for k, v in knobs.items():
                 ops.set_knob(k, v)
             r = ops.conv_dgrad_bnr(dy, w, H, H, 1, 0, res, None, xb, mean, istd, x2, mean2, istd2, None, None, None, bits)
             outs.append([t.clone() for t in r])
             ops.set_knob("epi_depth_bnr2", 2)
-            ops.set_knob("stream_bnr2", 0)
-            ops.set_knob("stream_maxk", 0)
     finally:
         ops.set_knob("epi_depth_bnr2", 2)
-        ops.set_knob("stream_bnr2", 0)
-        ops.set_knob("stream_maxk", 0)
     for o in outs[1:]:
         assert torch.equal(o[0], outs[0][0])
         for pa, pb in zip(o[1:], outs[0][1:]):
@@ -878,90 +723,6 @@ def test_halo_conv_dgrad_matches_igemm(gpu, bnr):
         close(got[0], outr[0])
     else:
         close(got[0], ref.conv_dgrad(dy, w, H, H, 1, 1, None))
-
-
-@pytest.mark.parametrize("mode", ["fwd_stats", "dgrad_bnr", "plain_gemm"])
-def test_dma8_staggered_schedule_bitwise(gpu, mode):
-    """The 8-wave LDS-DMA kernel's wave-row-staggered READ / MFMA schedule (knob dma8_stag) gives the
-    lock-step schedule's outputs bitwise (same MFMA order per accumulator) and matches the fp32
-    reference, on shapes that select the 256x256 kernel (>= 160 tiles, >= 8 K-tiles)."""
-    torch.manual_seed(11)
-    ops = _ops()
-    N, H, C, K, R = 210, 14, 256, 256, 3          # 41,160 rows x 256: 161 tiles, 36 K-tiles
-    x = rnd(N, H, H, C, dev=gpu)
-    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
-    dy = rnd(N, H, H, K, dev=gpu)
-    xb = rnd(N, H, H, C, dev=gpu)
-    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
-    msc, msh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
-    A = (torch.rand(40960, 2048, device=gpu) * 2 - 1).to(torch.bfloat16)
-    B = (torch.rand(256, 2048, device=gpu) * 2 - 1).to(torch.bfloat16)
-
-    def run():
-        if mode == "fwd_stats":
-            return [t.clone() for t in ops.conv_fwd(x, w, 1, 1, None, None, False, True)]
-        if mode == "dgrad_bnr":
-            return [t.clone() for t in ops.conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, xb, mean, istd,
-                                                          None, None, None, msc, msh)]
-        return [ops.conv_fwd(A.view(40960, 1, 1, 2048), B.view(256, 1, 1, 2048), 1, 0, None, None, False,
-                             False)[0].clone()]
-    outs = []
-    if mode == "plain_gemm":
-        ops.set_knob("plan_force", 2)             # the 8-wave 256x256 DMA kernel
-    old = {k.split("=")[0]: int(k.split("=")[1]) for k in ops.list_knobs()}
-    try:
-        # lock-step, staggered, early-prefetch (8-wave and 4-wave kernels)
-        for stag, pf2 in ((0, 0), (1, 0), (0, 3)):
-            ops.set_knob("dma8_stag", stag)
-            ops.set_knob("dma_pf2", pf2)
-            outs.append(run())
-    finally:
-        ops.set_knob("dma8_stag", old["dma8_stag"])
-        ops.set_knob("dma_pf2", old["dma_pf2"])
-        ops.set_knob("plan_force", -1)
-    for o in outs[1:]:
-        assert torch.equal(outs[0][0], o[0])
-        for pa, pb in zip(outs[0][1:], o[1:]):
-            assert torch.equal(pa, pb)
-    if mode == "fwd_stats":
-        yr = ref.conv_fwd(x, w, 1, 1, None, None, False, True)[0]
-        close(outs[1][0], yr)
-        close_el(outs[1][0], yr)
-    elif mode == "dgrad_bnr":
-        gr = ref.conv_dgrad_bnr(dy, w, H, H, 1, 1, None, None, xb, mean, istd, None, None, None, msc, msh)[0]
-        close(outs[1][0], gr)
-    else:
-        refm = (A.float() @ B.float().t())
-        close(outs[1][0].view(40960, 256), refm, 1e-2, 1e-2)
-
-
-@pytest.mark.parametrize("shape", [(16, 28, 28, 128, 128, 3), (8, 28, 28, 512, 128, 1), (8, 56, 56, 64, 64, 3)])
-def test_dma4_early_prefetch_bitwise(gpu, shape):
-    """Early-prefetch schedule (knob dma_pf2 bit 0) of the 4-wave LDS-DMA kernels (128x128, 128x64):
-    FWD+stats and DGRAD+BN-reduce outputs bitwise equal to the lock-step schedule."""
-    torch.manual_seed(12)
-    ops = _ops()
-    N, H, W, C, K, R = shape
-    x = rnd(N, H, W, C, dev=gpu)
-    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
-    dy = rnd(N, H, W, K, dev=gpu)
-    xb = rnd(N, H, W, C, dev=gpu)
-    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
-    msc, msh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.1
-    outs = []
-    old = ops.set_knob("dma_pf2", 0)
-    try:
-        for v in (0, 1):
-            ops.set_knob("dma_pf2", v)
-            f = [t.clone() for t in ops.conv_fwd(x, w, 1, R // 2, None, None, False, True)]
-            d = [t.clone() for t in ops.conv_dgrad_bnr(dy, w, H, W, 1, R // 2, None, None, xb, mean, istd,
-                                                       None, None, None, msc, msh)]
-            outs.append(f + d)
-    finally:
-        ops.set_knob("dma_pf2", old)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
-    close(outs[1][0], ref.conv_fwd(x, w, 1, R // 2, None, None, False, True)[0])
 
 
 @pytest.mark.parametrize("hw,out", [((375, 500), (224, 224)), ((224, 224), (224, 224)), ((100, 77), (224, 224)),

@@ -59,7 +59,7 @@ __device__ __forceinline__ float bf2f(__bf16 v) { return (float)v; }
 // V1: one block per CU, WM x WN waves, 2 LDS stages, fragments double-buffered over the two
 // 32-deep halves of each 64-deep K-tile, ONE barrier per K-tile; the DMA of tile t+2 is issued
 // right after the barrier that retires the reads of tile t.
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool INPLACE_B = false>
 __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_v1(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
                                                          __bf16* __restrict__ C, int M, int N, int K, unsigned a_bytes,
                                                          unsigned b_bytes) {
@@ -135,16 +135,54 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_v1(const __bf16* __restr
     wait_vm<0>();
   }
   lds_sync();
-  rd(fa0, fb0, 0, 0);
-  for (int t = 0; t < nk; ++t) {
-    const int s = t & 1;
-    rd(fa1, fb1, 1, s);
-    mma(fa0, fb0);
-    if (t + 1 < nk) wait_vm<0>();
-    lds_sync();   // every wave's reads of stage s retired; stage t+1 landed for every wave
-    if (t + 2 < nk) issue(s, (t + 2) * BK);
-    if (t + 1 < nk) rd(fa0, fb0, 0, s ^ 1);
-    mma(fa1, fb1);
+  if constexpr (!INPLACE_B) {
+    rd(fa0, fb0, 0, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int s = t & 1;
+      rd(fa1, fb1, 1, s);
+      mma(fa0, fb0);
+      if (t + 1 < nk) wait_vm<0>();
+      lds_sync();   // every wave's reads of stage s retired; stage t+1 landed for every wave
+      if (t + 2 < nk) issue(s, (t + 2) * BK);
+      if (t + 1 < nk) rd(fa0, fb0, 0, s ^ 1);
+      mma(fa1, fb1);
+    }
+  } else {
+    // B fragments reloaded in place column by column (96 fragment VGPRs instead of 128)
+    auto rd_a = [&](bf16x8(&fa)[TM], int kk, int s) {
+      const char* sA = smem + s * STAGE;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+    };
+    auto rd_b1 = [&](int j, int kk, int s) {
+      return *reinterpret_cast<const bf16x8*>(smem + s * STAGE + A_BYTES +
+                                             rr_off(wc * WTN + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+    };
+    rd_a(fa0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb0[j] = rd_b1(j, 0, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int s = t & 1;
+      rd_a(fa1, 1, s);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j], fa0[i], acc[j][i], 0, 0, 0);
+        fb0[j] = rd_b1(j, 1, s);
+      }
+      if (t + 1 < nk) wait_vm<0>();
+      lds_sync();
+      if (t + 2 < nk) issue(s, (t + 2) * BK);
+      const bool nx = t + 1 < nk;
+      if (nx) rd_a(fa0, 0, s ^ 1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j], fa1[i], acc[j][i], 0, 0, 0);
+        if (nx) fb0[j] = rd_b1(j, 0, s ^ 1);
+      }
+    }
   }
   // epilogue: lane holds C[m][n..n+3] of each fragment
 #pragma unroll
@@ -185,11 +223,11 @@ struct Variant {
   int bm, bn;
 };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool IB = false>
 void launch_v1(const __bf16* A, const __bf16* B, __bf16* C, int M, int N, int K, hipStream_t st) {
   static bool attr = false;
   constexpr size_t smem = 2 * (BM + BN) * BK * 2;
-  auto kfn = &gemm_v1<BM, BN, WM, WN>;
+  auto kfn = &gemm_v1<BM, BN, WM, WN, IB>;
   if (!attr) {
     CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
@@ -205,6 +243,8 @@ int main(int argc, char** argv) {
       {"v1_256x256_w4", launch_v1<256, 256, 2, 2>, 256, 256},
       {"v1_256x256_w8", launch_v1<256, 256, 2, 4>, 256, 256},
       {"v1_256x128_w4", launch_v1<256, 128, 2, 2>, 256, 128},
+      {"v2_256x256_w4", launch_v1<256, 256, 2, 2, true>, 256, 256},
+      {"v2_256x128_w4", launch_v1<256, 128, 2, 2, true>, 256, 128},
   };
   struct Shape { int M, N, K; };
   std::vector<Shape> shapes = {{4096, 4096, 4096}, {8192, 8192, 8192}, {50176, 256, 2304}, {12544, 512, 4608},
