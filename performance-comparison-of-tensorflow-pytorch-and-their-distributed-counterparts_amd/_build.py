@@ -52,16 +52,26 @@ def _common_flags(inc, abi):
     return flags
 
 
+def _local_includes(path: pathlib.Path, seen=None) -> set:
+    """Local headers (``#include "x.h"``) a source includes, transitively."""
+    seen = set() if seen is None else seen
+    for line in path.read_text(errors="ignore").splitlines():
+        line = line.strip()
+        if line.startswith("#include \""):
+            h = (path.parent / line.split('"')[1]).resolve()
+            if h.exists() and h not in seen:
+                seen.add(h)
+                _local_includes(h, seen)
+    return seen
+
+
 def _deps_newer(obj: pathlib.Path, src: pathlib.Path) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
     if src.stat().st_mtime > t:
         return True
-    for h in list(CSRC.glob("*.h")) + list((CSRC / "runtime").glob("*.h")):
-        if h.stat().st_mtime > t:
-            return True
-    return False
+    return any(h.stat().st_mtime > t for h in _local_includes(src))
 
 
 def _compile(cmd, src):

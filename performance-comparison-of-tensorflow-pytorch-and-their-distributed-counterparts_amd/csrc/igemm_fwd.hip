@@ -1,0 +1,152 @@
+// Implicit-GEMM convolution / Linear: forward (FWD) entry points.
+// Kernels, launchers, dispatch and the GEMM planner live in igemm.h; this translation unit holds the
+// FWD entry points (split from igemm.hip in round 4 so the three modes compile in parallel).
+#include "igemm.h"
+
+namespace pcmp {
+
+// x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
+// (bf16 [N,P,Q,K]) and activation (act: IgemmParams::relu) fused; optional stats output
+// [tiles_m,2,K] f32 (returned).  act 2 (GELU) also returns the pre-activation u.
+static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                             const c10::optional<at::Tensor>& bias,
+                                             const c10::optional<at::Tensor>& resid, int act, bool want_stats,
+                                             const at::Tensor* in_scale = nullptr, const at::Tensor* in_shift = nullptr) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_BF16(x); PCMP_CHECK_BF16(w);
+  PCMP_CHECK_CONTIG(x); PCMP_CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv_fwd: NHWC x and KRSC w expected");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "conv_fwd: channel mismatch");
+  TORCH_CHECK(C % 8 == 0 && K % 8 == 0, "conv_fwd: C and K must be multiples of 8");
+  IgemmParams p;
+  fill_geometry(p, N, H, W, C, K, R, S, stride, pad);
+  p.gm = N * p.P * p.Q; p.gn = K; p.gk = R * S * C;
+  TORCH_CHECK((int64_t)N * H * W * C < (1ll << 31) && (int64_t)p.gm * K < (1ll << 31), "conv_fwd: tensor too large");
+  auto y = at::empty({N, p.P, p.Q, K}, x.options());
+  p.a = ptr<__bf16>(x); p.b = ptr<__bf16>(w); p.out = y.data_ptr();
+  p.a_bytes = tensor_bytes(x); p.b_bytes = tensor_bytes(w);
+  if (bias.has_value() && bias->defined()) { PCMP_CHECK_F32(*bias); p.bias = ptr<float>(*bias); }
+  if (resid.has_value() && resid->defined()) {
+    PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
+    TORCH_CHECK(resid->numel() == y.numel(), "conv_fwd: residual shape");
+    p.resid = ptr<__bf16>(*resid);
+  }
+  p.relu = act;
+  at::Tensor u;
+  if (act == 2) {
+    TORCH_CHECK(!want_stats, "conv_fwd: GELU epilogue without statistics");
+    u = at::empty_like(y);
+    p.aux = ptr<__bf16>(u);
+  }
+  p.ksplit = p.gk; p.nsplit = 1;
+  if (in_scale) {   // BatchNorm-forward fold: the operand is relu(in_scale * x + in_shift); set before
+                    // igemm_bm sizes the statistics rows (the fold picks its own tile)
+    TORCH_CHECK(in_shift && R == 1 && S == 1 && stride == 1 && C % BK == 0 && act != 2,
+                "conv_fwd: the input activation fold needs a 1x1 stride-1 conv with C % 64 == 0");
+    for (const at::Tensor* t : {in_scale, in_shift}) {
+      PCMP_CHECK_F32(*t); PCMP_CHECK_CONTIG(*t);
+      TORCH_CHECK(t->numel() == C, "conv_fwd: in_scale / in_shift must hold C values");
+    }
+    p.act_sc = ptr<float>(*in_scale); p.act_sh = ptr<float>(*in_shift);
+  }
+  const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
+  const int BNsel = p.gn <= 64 ? 64 : 128;
+  at::Tensor stats;
+  if (want_stats) {
+    p.stats_cap = ceil_div(p.gm, igemm_bm(MODE_FWD, p));
+    stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
+    p.stats = ptr<float>(stats);
+  }
+  auto st = cur_stream();
+  if (in_scale) {   // BatchNorm-forward fold (act_sc / act_sh set above)
+    dispatch<MODE_FWD>(p, st);
+    if (want_stats) return {y, stats};
+    return {y};
+  }
+  if (plain_gemm_eligible<MODE_FWD>(p)) {
+    const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
+    run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
+    return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
+  }
+  // Small-M shapes (batch-1 inference: 49..3136 pixels) leave most of the 256 CUs idle; split the
+  // reduction so the grid reaches ~256 workgroups, then reduce + epilogue in one pass.
+  const int tiles = ceil_div(p.gm, BMsel) * ceil_div(p.gn, BNsel);
+  const int ksteps = ceil_div(p.gk, BK);
+  int nsplit = 1;
+  // PCMP_FWD_SPLIT_TARGET / PCMP_FWD_SPLIT_MINK: grid target and minimum K-steps per split (A/B-only knobs of
+  // the round-1 heuristic; numerics at high split counts are covered by the plan_force small-M tests)
+  static const int split_target = [] { const char* e = getenv("PCMP_FWD_SPLIT_TARGET"); return e ? std::max(1, atoi(e)) : 256; }();
+  static const int split_mink = [] { const char* e = getenv("PCMP_FWD_SPLIT_MINK"); return e ? std::max(1, atoi(e)) : 4; }();
+  if (!want_stats && tiles < 128 && ksteps >= 8)
+    nsplit = std::max(1, std::min({ceil_div(split_target, tiles), ksteps / split_mink, 32}));
+  if (!want_stats && tiles < 128 && ksteps >= 8 && kn_gemm_plan.get()) {
+    const GemmPlan pl = plan_gemm<MODE_FWD>(p, ptr<__bf16>(y), x.options().dtype(at::kFloat), st, true, nsplit);
+    run_plan<MODE_FWD>(p, pl, ptr<__bf16>(y), x.options().dtype(at::kFloat), st);
+    return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
+  }
+  if (nsplit > 1) {
+    const int steps_per = ceil_div(ksteps, nsplit);
+    nsplit = ceil_div(ksteps, steps_per);
+    p.ksplit = steps_per * BK;
+    p.nsplit = nsplit;
+    const int64_t n = (int64_t)p.gm * p.gn;
+    auto ws = at::empty({(int64_t)nsplit, n}, x.options().dtype(at::kFloat));
+    p.out = ws.data_ptr();
+    dispatch<MODE_FWD>(p, st);
+    const int blocks = (int)((n / 4 + 255) / 256);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), ptr<__bf16>(y),
+                       p.bias, p.resid, n, p.gn, nsplit, p.relu, p.aux);
+    PCMP_LAUNCH_CHECK();
+    return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
+  }
+  dispatch<MODE_FWD>(p, st);
+  if (want_stats) return {y, stats};
+  return act == 2 ? std::vector<at::Tensor>{y, u} : std::vector<at::Tensor>{y};
+}
+
+
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias,
+                                 const c10::optional<at::Tensor>& resid, bool relu, bool want_stats,
+                                 const c10::optional<at::Tensor>& in_scale, const c10::optional<at::Tensor>& in_shift) {
+  const bool fold = in_scale.has_value() && in_scale->defined();
+  TORCH_CHECK(!fold || (in_shift.has_value() && in_shift->defined()), "conv_fwd: in_shift required with in_scale");
+  TORCH_CHECK(!fold || x.scalar_type() != at::kFloat, "conv_fwd: the input activation fold is bf16 only");
+  if (x.scalar_type() == at::kFloat) return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats);
+  return conv_fwd_impl(x, w, stride, pad, bias, resid, relu ? 1 : 0, want_stats, fold ? &*in_scale : nullptr,
+                       fold ? &*in_shift : nullptr);
+}
+
+// Linear y = gelu(x W^T + b) with the GELU fused into the GEMM epilogue: x [M, C], w [N, C] bf16
+// -> [gelu(u), u] (u = x W^T + b, kept for the backward).  BERT's FFN up-projection
+// (pytorch_on_language_distr.py:151-161 via BertIntermediate).
+std::vector<at::Tensor> linear_gelu_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias) {
+  if (x.scalar_type() == at::kFloat) return f32::linear_gelu_fwd(x, w, bias);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "linear_gelu_fwd: x [M, C], w [N, C]");
+  const int64_t M = x.size(0), C = x.size(1), N = w.size(0);
+  auto r = conv_fwd_impl(x.view({M, 1, 1, C}), w.view({N, 1, 1, C}), 1, 0, bias, c10::nullopt, 2, false);
+  return {r[0].view({M, N}), r[1].view({M, N})};
+}
+
+// Timings of every planner candidate for one conv_fwd call (reports / kernel tuning): runs the
+// planner uncached with its log enabled.
+std::vector<std::string> plan_candidates(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                         const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
+                                         bool relu) {
+  std::vector<std::string> log;
+  const int old = kn_plan_force.value.exchange(99);   // 99: no such kind -> every candidate, uncached
+  g_plan_log = &log;
+  try {
+    conv_fwd(x, w, stride, pad, bias, resid, relu, false, c10::nullopt, c10::nullopt);
+  } catch (...) {
+    g_plan_log = nullptr;
+    kn_plan_force.value.store(old);
+    throw;
+  }
+  g_plan_log = nullptr;
+  kn_plan_force.value.store(old);
+  return log;
+}
+
+}  // namespace pcmp

@@ -1,0 +1,154 @@
+// Implicit-GEMM convolution / Linear: weight-gradient (WGRAD) entry points.
+// Kernels, launchers, dispatch and the GEMM planner live in igemm.h; this translation unit holds the
+// WGRAD entry points (split from igemm.hip in round 4 so the three modes compile in parallel).
+#include "igemm.h"
+
+namespace pcmp {
+
+// split-K WGRAD: partial dW per split into a workspace, then one deterministic reduction pass
+static void wgrad_run(IgemmParams p, int nsplit, float* out, bool accumulate, const at::TensorOptions& fopts,
+                      hipStream_t st) {
+  const int ksteps = ceil_div(p.gk, BK);
+  const int steps_per = ceil_div(ksteps, nsplit);
+  nsplit = ceil_div(ksteps, steps_per);
+  p.ksplit = steps_per * BK;
+  p.nsplit = nsplit;
+  if (nsplit == 1) {
+    p.out = out;
+    p.accumulate = accumulate;
+    dispatch<MODE_WGRAD>(p, st);
+    return;
+  }
+  const int64_t n = (int64_t)p.gm * p.gn;
+  TORCH_CHECK(n % 4 == 0, "conv_wgrad: numel % 4");
+  auto ws = at::empty({(int64_t)nsplit, n}, fopts);
+  p.out = ws.data_ptr();
+  dispatch<MODE_WGRAD>(p, st);
+  if (n / 4 < (1ll << 31)) {
+    const int n4 = (int)(n / 4);
+    const int SL = nsplit <= 8 ? 1 : (nsplit <= 32 ? 4 : 16);
+    const int cols = 256 / SL;
+    const dim3 grid(ceil_div(n4, cols));
+    if (SL == 1) hipLaunchKernelGGL(splitk_reduce2_kernel<1>, grid, dim3(256), 0, st, ptr<float>(ws), out, n4, nsplit, (int)accumulate);
+    else if (SL == 4) hipLaunchKernelGGL(splitk_reduce2_kernel<4>, grid, dim3(256), 0, st, ptr<float>(ws), out, n4, nsplit, (int)accumulate);
+    else hipLaunchKernelGGL(splitk_reduce2_kernel<16>, grid, dim3(256), 0, st, ptr<float>(ws), out, n4, nsplit, (int)accumulate);
+    PCMP_LAUNCH_CHECK();
+    return;
+  }
+  const int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, st, ptr<float>(ws), out, n, nsplit,
+                     (int)accumulate);
+  PCMP_LAUNCH_CHECK();
+}
+
+// WGRAD split-K autotuning (cudnn.benchmark-style): the best split count of a shape depends on tile
+// quantisation against 256 CUs and on the workspace traffic of the reduction, and measured
+// non-monotonically (profiles/r1_wgrad_splitk_ab.txt), so the first call of each shape times a few
+// grid targets on a scratch output and caches the fastest.  Never while a graph is being captured.
+// PCMP_AUTOTUNE=0 (or an explicit PCMP_WGRAD_WGS) keeps the static 1024-workgroup target, which
+// also keeps runs bitwise reproducible (a tuned split count changes the summation order).
+static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions& fopts, hipStream_t st) {
+  const int ksteps = ceil_div(p.gk, BK);
+  auto nsplit_for = [&](int target) { return std::max(1, std::min(std::min(ceil_div(target, tiles), ksteps / 8), 256)); };
+  static const int fixed_target = [] {
+    const char* e = std::getenv("PCMP_WGRAD_WGS");
+    return e ? std::max(64, std::atoi(e)) : 0;
+  }();
+  static const bool tune = [] {
+    const char* e = std::getenv("PCMP_AUTOTUNE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (fixed_target) return nsplit_for(fixed_target);
+  // WGRADs launched on the side stream (ops/params.py run_on_side sets the knob around them) share
+  // the CUs with the DGRAD chain: there a fixed 384-workgroup target beats the isolated autotune
+  // (ResNet-50 step +0.5-0.7 %, 3 of 3 interleaved rounds, profiles/r2_knob_sweep.txt sweep 6)
+  if (kn_wgrad_wgs.get() > 0) return nsplit_for(std::max(64, kn_wgrad_wgs.get()));
+  const int dflt = nsplit_for(1024);
+  if (!tune) return dflt;
+  auto& mu = g_plan_mu;
+  auto& cache = g_wsplit_cache;
+  char key[160];
+  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
+           0);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;   // a graph captured after warm-up keeps the tuned split
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
+  std::vector<int> cands;
+  for (int t : {64, 128, 256, 512, 768, 1024, 1536, 2048}) {
+    const int ns = nsplit_for(t);
+    if (std::find(cands.begin(), cands.end(), ns) == cands.end()) cands.push_back(ns);
+  }
+  int best = dflt;
+  if (cands.size() > 1) {
+    auto scratch = at::empty({(int64_t)p.gm * p.gn}, fopts);
+    hipEvent_t e0, e1;
+    PCMP_HIP_CHECK(hipEventCreate(&e0));
+    PCMP_HIP_CHECK(hipEventCreate(&e1));
+    float best_ms = 1e30f;
+    for (int ns : cands) {
+      wgrad_run(p, ns, ptr<float>(scratch), false, fopts, st);   // warm (workspace allocation, caches)
+      PCMP_HIP_CHECK(hipEventRecord(e0, st));
+      for (int r = 0; r < 3; ++r) wgrad_run(p, ns, ptr<float>(scratch), false, fopts, st);
+      PCMP_HIP_CHECK(hipEventRecord(e1, st));
+      PCMP_HIP_CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      PCMP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best_ms) { best_ms = ms; best = ns; }
+    }
+    PCMP_HIP_CHECK(hipEventDestroy(e0));
+    PCMP_HIP_CHECK(hipEventDestroy(e1));
+  }
+  std::lock_guard<std::mutex> g(mu);
+  cache.emplace(key, best);
+  return best;
+}
+
+// dy: [N,P,Q,K], x: [N,H,W,C] -> writes dW (f32, [K,R,S,C]) into `out` (accumulate optional).
+void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
+                int64_t stride, int64_t pad, bool accumulate, const c10::optional<at::Tensor>& fold_x,
+                const c10::optional<at::Tensor>& fold_coef, const c10::optional<at::Tensor>& in_scale,
+                const c10::optional<at::Tensor>& in_shift) {
+  const bool fold = fold_x.has_value() && fold_x->defined();
+  const bool afold = in_scale.has_value() && in_scale->defined();
+  TORCH_CHECK(!afold || dy.scalar_type() != at::kFloat, "conv_wgrad: the input activation fold is bf16 only");
+  TORCH_CHECK(!fold || dy.scalar_type() != at::kFloat, "conv_wgrad: the BatchNorm-backward fold is bf16 only");
+  if (dy.scalar_type() == at::kFloat) return f32::conv_wgrad(dy, x, out, R, S, stride, pad, accumulate);
+  PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(x);
+  PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = dy.size(3);
+  IgemmParams p;
+  fill_geometry(p, N, H, W, C, K, R, S, stride, pad);
+  TORCH_CHECK(dy.size(1) == p.P && dy.size(2) == p.Q, "conv_wgrad: dy shape");
+  TORCH_CHECK(out.numel() == (int64_t)K * R * S * C, "conv_wgrad: out numel");
+  p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
+  p.a = ptr<__bf16>(dy); p.b = ptr<__bf16>(x);
+  p.a_bytes = tensor_bytes(dy); p.b_bytes = tensor_bytes(x);
+  if (fold) {   // dy operand = k1*g + k2*fold_x + k3 (dy passed as g)
+    PCMP_CHECK_BF16(*fold_x); PCMP_CHECK_CONTIG(*fold_x);
+    TORCH_CHECK(fold_x->numel() == dy.numel(), "conv_wgrad: fold_x must have dy's shape");
+    TORCH_CHECK(fold_coef.has_value() && fold_coef->defined(), "conv_wgrad: fold_coef required with fold_x");
+    PCMP_CHECK_F32(*fold_coef); PCMP_CHECK_CONTIG(*fold_coef);
+    TORCH_CHECK(fold_coef->numel() == 3 * (int64_t)K, "conv_wgrad: fold_coef must be [3, K]");
+    p.fold_x = ptr<__bf16>(*fold_x); p.fold_coef = ptr<float>(*fold_coef);
+  }
+  if (afold) {   // x operand = relu(in_scale * x + in_shift) (x passed as the pre-BN tensor)
+    TORCH_CHECK(in_shift.has_value() && in_shift->defined(), "conv_wgrad: in_shift required with in_scale");
+    for (const at::Tensor* t : {&*in_scale, &*in_shift}) {
+      PCMP_CHECK_F32(*t); PCMP_CHECK_CONTIG(*t);
+      TORCH_CHECK(t->numel() == C, "conv_wgrad: in_scale / in_shift must hold C values");
+    }
+    p.act_sc = ptr<float>(*in_scale); p.act_sh = ptr<float>(*in_shift);
+  }
+  int BM, BN;
+  wgrad_tile(p, BM, BN);
+  const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
+  auto st = cur_stream();
+  const int nsplit = wgrad_nsplit(p, tiles, out.options(), st);
+  wgrad_run(p, nsplit, ptr<float>(out), accumulate, out.options(), st);
+}
+
+}  // namespace pcmp
