@@ -1194,20 +1194,25 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
 }
 
 // ------------------------------------------------------------------------------------------------
-// "Big" LDS-DMA kernel for the compute-bound FWD/DGRAD GEMMs (round 4 main loop): 4 waves (2x2) of
-// 128 x BN/2 wave tiles -- BM = 256 x BN = 256 (128x128 per wave, 256 fp32 accumulators per lane in
-// AGPRs) or 256 x 128 -- one block per CU, the shape hipBLASLt's fastest gfx950 bf16 kernels use
-// (profiles/r4_blas_kernels.txt: MT256x256x64 / MT256x128x64, MI16x16, 256 threads).  Per K-tile
-// (BK = 64) each wave issues 2 x TM x TN MFMAs; the LDS images hold 2 stages; the fragments are
-// double-buffered over the two 32-deep halves of the K-tile, so the LDS reads of one half run under
-// the MFMAs of the other, and there is ONE workgroup barrier per K-tile:
-//   half 0: read frags(t, 1)          | MFMA frags(t, 0)
+// "Big" LDS-DMA kernel for the compute-bound FWD/DGRAD GEMMs (round 4 main loop).  BM = 256 rows,
+// BN = 256 (8 waves, 2x4, 128x64 wave tiles) or 128 (4 waves, 2x2, 128x64), one block per CU, two LDS
+// stages.  The fragments are double-buffered over the two 32-deep halves of each 64-deep K-tile, so
+// there is ONE workgroup barrier per K-tile:
+//   half 0: ds_read frags(t, 1)  || MFMA frags(t, 0)
 //           vmcnt(0) [stage t+1 landed] + lgkmcnt(0) + barrier [every wave done reading stage t]
-//   half 1: DMA stage t+2 into stage t's buffer; read frags(t+1, 0) | MFMA frags(t, 1)
-// The DMA of stage t+2 therefore has a whole K-tile of MFMAs (plus half of the next) to land.
-// Waits use the s_waitcnt builtin (not inline asm), so the compiler's own waitcnt pass sees them and
-// adds no conservative lgkmcnt waits of its own in front of the half-1 MFMAs (tools/gemm_lab).
-// Operand staging, swizzle, channel permutation and epilogue are those of igemm_dma_kernel.
+//   half 1: DMA stage t+2 into stage t's buffer, ds_read frags(t+1, 0)  || MFMA frags(t, 1)
+// The DMA of stage t+2 has a whole K-tile of MFMAs to land.  The loop body is branch-free (the DMA of
+// the last two iterations reads out of range and zero-fills a dead stage; their fragment reads hit a
+// dead stage), so each half is one scheduling region: sched_group_barrier spreads the DMA issues and
+// ds_reads between the MFMAs (an LDS-DMA issue costs ~60 cycles of the issuing wave), and SG = 2 adds
+// sched_barrier fences so hipcc keeps each half's MFMAs on its side of the workgroup barrier.  Waits
+// use the s_waitcnt builtin (not inline asm), so hipcc's waitcnt pass sees them and adds no
+// conservative lgkmcnt waits in front of the half-1 MFMAs.
+// Measured in tools/gemm_lab (profiles/r4_gemm_lab.txt, same box, uniform random operands):
+// 8 waves + fences 1,283 TF at 4096^3 and 953 TF at 50176x256x2304 (the layer-3 3x3 GEMM) against
+// 1,249 / 898 for the same loop without interleave and fences; 4-wave 256x256 variants (256 fp32
+// accumulators per lane) lose 10-25 % to hipcc's AGPR copies.  Operand staging, swizzle, channel
+// permutation and epilogue are those of igemm_dma_kernel.
 template <int N>
 __device__ __forceinline__ void wait_vm_b() {   // vmcnt(N) through the builtin (gfx9 simm16 encoding)
   static_assert(N >= 0 && N < 64, "vmcnt");
@@ -1218,16 +1223,20 @@ __device__ __forceinline__ void lds_sync_b() {   // lgkmcnt(0) + s_barrier, both
   __builtin_amdgcn_s_barrier();
 }
 constexpr int BIG_BM = 256;
+template <int BN>
+constexpr int big_waves() { return BN == 256 ? 8 : 4; }
 
 template <int MODE, int BN, int EPI, int EPD = 2>
-__global__ void __launch_bounds__(NT, 1) igemm_big_kernel(const IgemmParams p) {
-  constexpr int BM = BIG_BM, WM = 2, WN = 2, NW = 4;
+__global__ void __launch_bounds__(big_waves<BN>() * 64, 1) igemm_big_kernel(const IgemmParams p) {
+  constexpr int BM = BIG_BM, NW = big_waves<BN>(), NTHR = NW * 64, WM = 2, WN = NW / 2;
+  constexpr int SG = NW == 8 ? 2 : 1;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
   constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;   // LDS-DMA instructions (8 rows each) per wave
   static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
   static_assert(WTN % 32 == 0 && TN % 2 == 0, "PAIR channel permutation");
+  static_assert(NA >= 1 && NB >= 1, "loader");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1286,7 +1295,8 @@ __global__ void __launch_bounds__(NT, 1) igemm_big_kernel(const IgemmParams p) {
   const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
   int kc = kbeg % CIN, k0 = kbeg;
   int ks = (kbeg / CIN) % p.S, kr = (kbeg / CIN) / p.S;
-  auto issue = [&](int s) {   // DMA of the K-tile at (k0, kr, ks, kc) into stage s, then advance
+  // DMA of the K-tile at (k0, kr, ks, kc) into stage s, then advance; !live: zero-fill (tail)
+  auto issue = [&](int s, bool live) {
     int tap;
     if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
     else tap = -(kr * p.Q + ks) * p.K + kc;
@@ -1298,13 +1308,13 @@ __global__ void __launch_bounds__(NT, 1) igemm_big_kernel(const IgemmParams p) {
         ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
       else
         ok = (unsigned)(a_y[i] - kr) < (unsigned)p.P && (unsigned)(a_x[i] - ks) < (unsigned)p.Q;
-      const int voff = ok ? (a_off[i] + tap) * 2 : (int)kOOB;
+      const int voff = (ok && live) ? (a_off[i] + tap) * 2 : (int)kOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(dst + (wid * NA + i) * 1024),
                                                16, voff, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int voff = b_off[i] >= 0 ? (b_off[i] + k0) * 2 : (int)kOOB;
+      const int voff = (b_off[i] >= 0 && live) ? (b_off[i] + k0) * 2 : (int)kOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsB, (__attribute__((address_space(3))) void*)(dst + A_BYTES + (wid * NB + i) * 1024), 16, voff, 0, 0, 0);
     }
@@ -1338,29 +1348,41 @@ __global__ void __launch_bounds__(NT, 1) igemm_big_kernel(const IgemmParams p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
   };
+  constexpr int NMF = TM * TN, NDS = TM + TN, NVM = NA + NB;
 
   if (nk > 0) {
-    issue(0);
-    if (nk > 1) {
-      issue(1);
-      wait_vm_b<NA + NB>();
-    } else {
-      wait_vm_b<0>();
-    }
+    issue(0, true);
+    issue(1, nk > 1);
+    wait_vm_b<NA + NB>();
     lds_sync_b();
     rd(fa0, fb0, 0, 0);
     for (int t = 0; t < nk; ++t) {
       const int s = t & 1;
       rd(fa1, fb1, 1, s);
       mma(fa0, fb0);
-      if (t + 1 < nk) wait_vm_b<0>();
+#pragma unroll
+      for (int g = 0; g < NDS; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);            // 1 DS_READ
+        __builtin_amdgcn_sched_group_barrier(0x8, NMF / NDS, 0);      // MFMAs
+      }
+      if constexpr (SG >= 2) __builtin_amdgcn_sched_barrier(0);
+      wait_vm_b<0>();
       lds_sync_b();   // every wave's reads of stage s retired; stage t+1 landed for every wave
-      if (t + 2 < nk) issue(s);
-      if (t + 1 < nk) rd(fa0, fb0, 0, s ^ 1);
+      if constexpr (SG >= 2) __builtin_amdgcn_sched_barrier(0);
+      issue(s, t + 2 < nk);
+      rd(fa0, fb0, 0, s ^ 1);
       mma(fa1, fb1);
+#pragma unroll
+      for (int g = 0; g < NDS; ++g) {
+        if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);  // 1 VMEM (LDS-DMA)
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x8, NMF / NDS, 1);
+      }
+      if constexpr (SG >= 2) __builtin_amdgcn_sched_barrier(0);
     }
+    wait_vm_b<0>();   // the tail zero-fill DMAs land before the epilogue reuses the LDS
   }
-  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NT, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
+  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2104,11 +2126,17 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
-// Round-4 "big" kernel (igemm_big_kernel: 4 waves, 256 x 256 or 256 x 128 tiles, 1 block per CU).
-// Knob big (bitmask): 1 = 256x256 tiles for FWD/DGRAD grids of >= big_min256 such tiles, 2 = 256x128
-// tiles where 256x256 would leave too many CUs idle (>= big_min128 tiles).  Both need the
-// block-uniform tap walk (source channels % 64) and >= big_mink K-tiles.
+// Round-4 "big" kernel (igemm_big_kernel: 256 x 256 tiles on 8 waves or 256 x 128 on 4, 1 block per CU).
+// Knob big (bitmask): 1 = 256x256 tiles for FWD/DGRAD grids of >= big_min256 such tiles and
+// N <= big_maxn, 2 = 256x128 tiles where 256x256 would leave too many CUs idle (>= big_min128 tiles).
+// Both need the block-uniform tap walk (source channels % 64) and >= big_mink K-tiles.
+// Default (profiles/r4_knob_ab_big.txt, in-process per-shape A/B on ResNet-50 B=256): the 8-wave
+// 256x256 path wins 2-5 % only on the N=256, >=196-tile layer-3 GEMMs (3x3 FWD/DGRAD, 1x1 to/from
+// 256 channels) and loses on N>=512 / fewer tiles; the 4-wave 256x128 path loses everywhere.  In the
+// whole training step (profiles/r4_bench_ab_big.txt) big=1 is still 0.3 % slower than big=0: its
+// 128 KB-LDS, 1-block-per-CU grid leaves no room for the side-stream WGRAD blocks, so it ships off.
 inline Knob kn_big("big", 0);
+inline Knob kn_big_maxn("big_maxn", 256);
 inline Knob kn_big_min256("big_min256", 192);
 inline Knob kn_big_min128("big_min128", 160);
 inline Knob kn_big_mink("big_mink", 4);
@@ -2126,7 +2154,8 @@ static void launch_big(IgemmParams& p, hipStream_t st) {
   const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
   if (epi_red) {
     const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
-    smem = std::max(smem, (size_t)(4 * 16 * (NS * (BN / 2) + 4) + 2 * NS * BN) * sizeof(float));
+    constexpr int NW = big_waves<BN>();
+    smem = std::max(smem, (size_t)(NW * 16 * (NS * (BN / (NW / 2)) + 4) + 2 * NS * BN) * sizeof(float));
   }
   TORCH_CHECK(smem <= 160 * 1024, "igemm_big: LDS budget");
   int epi = EPI_PLAIN;
@@ -2141,7 +2170,7 @@ static void launch_big(IgemmParams& p, hipStream_t st) {
                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
       attr_set = true;                                                                                \
     }                                                                                                 \
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(NT), smem, st, p);                                       \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(big_waves<BN>() * 64), smem, st, p);                     \
   } while (0)
   if constexpr (MODE == MODE_FWD) {
     if (epi == EPI_STATS) PCMP_BIG_LAUNCH(EPI_STATS, 2);
@@ -2149,7 +2178,10 @@ static void launch_big(IgemmParams& p, hipStream_t st) {
     else PCMP_BIG_LAUNCH(EPI_PLAIN, 2);
   } else {
     if (epi == EPI_BNR) PCMP_BIG_LAUNCH(EPI_BNR, 2);
-    else if (epi == EPI_BNR2) PCMP_BIG_LAUNCH(EPI_BNR2, 2);
+    else if (epi == EPI_BNR2) {
+      if constexpr (BN == 128) PCMP_BIG_LAUNCH(EPI_BNR2, 2);   // 8 waves: the dual-BN epilogue spills
+      else TORCH_CHECK(false, "igemm_big: dual BN-reduce epilogue is instantiated for 256x128 tiles only");
+    }
     else if (p.relu >= 2) PCMP_BIG_LAUNCH(EPI_GELU, 2);
     else PCMP_BIG_LAUNCH(EPI_PLAIN, 2);
   }
@@ -2164,7 +2196,9 @@ static int use_big(int mode, const IgemmParams& p) {
   const int cin = mode == MODE_FWD ? p.C : p.K;
   if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < kn_big_mink.get()) return 0;
   const int tm = ceil_div(p.gm, BIG_BM);
-  if ((kb & 1) && p.gn >= 256 && tm * ceil_div(p.gn, 256) >= kn_big_min256.get()) return 256;
+  if ((kb & 1) && p.gn >= 256 && p.gn <= kn_big_maxn.get() && !(mode == MODE_DGRAD && p.bn_x2) &&
+      tm * ceil_div(p.gn, 256) >= kn_big_min256.get())
+    return 256;
   if ((kb & 2) && p.gn >= 128 && tm * ceil_div(p.gn, 128) >= kn_big_min128.get()) return 128;
   return 0;
 }

@@ -44,7 +44,7 @@ class _Knobs:
             _ops().set_knob(k, v)
 
 
-BIG_ON = dict(big=3, big_min256=1, big_min128=1, big_mink=1)
+BIG_ON = dict(big=3, big_maxn=1 << 20, big_min256=1, big_min128=1, big_mink=1)
 
 SHAPES = [
     # N, H, W, C, K, R, stride, pad
@@ -114,3 +114,14 @@ def test_big_kernel_plain_gemm_plans(gpu, mnk):
             with _Knobs(big=3, plan_force=kind, plan_nsplit=ns):
                 got = _ops().conv_fwd(A.view(M, 1, 1, K), B.view(N, 1, 1, K), 1, 0, bias, None, True, False)[0]
             close(got, expect)
+
+
+def test_big_kernel_default_policy(gpu):
+    """Shipped policy: the 256x256 kernel runs for layer-3-sized N=256 convs only (plan log names it)."""
+    x = rnd(256, 14, 14, 256, dev=gpu)
+    w = rnd(256, 3, 3, 256, dev=gpu, scale=(2.0 / 2304) ** 0.5)
+    with _Knobs(big=0):
+        base = _ops().conv_fwd(x, w, 1, 1, None, None, False, True)[0]
+    with _Knobs(big=1, big_maxn=256, big_min256=192):
+        got = _ops().conv_fwd(x, w, 1, 1, None, None, False, True)[0]
+    assert torch.equal(got, base)
