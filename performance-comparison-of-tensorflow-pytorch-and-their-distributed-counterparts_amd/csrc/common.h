@@ -60,6 +60,31 @@ __device__ __forceinline__ float dgelu_erf(float x) {
   return cdf + x * pdf;
 }
 
+// bf16-epilogue GELU: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16
+// rounding of the stored value), branch-free: one reciprocal, one exp2, five FMAs -- the library
+// erff is ~45 instructions over two divergent branches.  The exp(-x^2/2) term is shared with the
+// derivative.  fp32 kernels (text_f32.hip) keep erff.
+__device__ __forceinline__ float erf_as_core(float a, float e) {   // a = |z|, e = exp(-z^2)
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  return 1.f - y * t * e;
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float e = __expf(-z * z);
+  const float er = copysignf(erf_as_core(fabsf(z), e), x);
+  return 0.5f * x * (1.f + er);
+}
+__device__ __forceinline__ float dgelu_fast(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float e = __expf(-z * z);   // = exp(-x^2 / 2)
+  const float er = copysignf(erf_as_core(fabsf(z), e), x);
+  return 0.5f * (1.f + er) + x * 0.3989422804014327f * e;
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -84,13 +109,19 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 }
 
 // Counter-based hash RNG (stateless): used for dropout so backward regenerates the mask
-// from (seed, offset, index) instead of storing it.
+// from (seed, offset, index) instead of storing it.  32-bit mixing ("lowbias32" finaliser) of the
+// index folded with the 64-bit seed: two 32-bit multiplies per element where the splitmix64 form
+// needed three 64-bit ones (~40 VALU ops; 30 % of the attention kernels' time at p = 0.1,
+// profiles/r4_attn_micro.txt).  ops/ref.py hash_uniform is the bit-exact torch port.
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed ^ (idx * 0x9E3779B97F4A7C15ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)z;
+  uint32_t x = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x85EBCA6Bu) ^ (uint32_t)seed ^
+               ((uint32_t)(seed >> 32) * 0x9E3779B9u);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
 }
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
   return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);

@@ -397,7 +397,7 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           float x1 = acc[j][i][e0 + 1] + bias[ce + 1];
           if (has_res) {
             const float r0 = __uint_as_float(rvA[b][q] << 16), r1 = __uint_as_float(rvA[b][q] & 0xffff0000u);
-            if (GELU && p.relu == 3) { x0 *= dgelu_erf(r0); x1 *= dgelu_erf(r1); }
+            if (GELU && p.relu == 3) { x0 *= dgelu_fast(r0); x1 *= dgelu_fast(r1); }
             else { x0 += r0; x1 += r1; }
           }
           if constexpr (GELU) {
@@ -405,8 +405,8 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
             else if (p.relu == 2) {   // u (bf16) -> aux; out = gelu(u) as the separate kernel would
               const unsigned uu = f2bf2(x0, x1);
               av[q] = uu;
-              x0 = gelu_erf(__uint_as_float(uu << 16));
-              x1 = gelu_erf(__uint_as_float(uu & 0xffff0000u));
+              x0 = gelu_fast(__uint_as_float(uu << 16));
+              x1 = gelu_fast(__uint_as_float(uu & 0xffff0000u));
             }
           } else if (p.relu) { x0 = fmaxf(x0, 0.f); x1 = fmaxf(x1, 0.f); }
           unsigned u = f2bf2(x0, x1);
@@ -1887,9 +1887,9 @@ static __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float x = s[e] + (bias ? bias[c + e] : 0.f);
-    if (resid) x = relu == 3 ? x * dgelu_erf(bf2f(rv[e])) : x + bf2f(rv[e]);
+    if (resid) x = relu == 3 ? x * dgelu_fast(bf2f(rv[e])) : x + bf2f(rv[e]);
     if (relu == 1) x = fmaxf(x, 0.f);
-    else if (relu == 2) { av[e] = f2bf(x); x = gelu_erf(bf2f(av[e])); }
+    else if (relu == 2) { av[e] = f2bf(x); x = gelu_fast(bf2f(av[e])); }
     ov[e] = f2bf(x);
   }
   reinterpret_cast<u16x4*>(out)[i] = ov;

@@ -390,7 +390,7 @@ __global__ void act_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict_
     float v[8];
     ldv8(x + i * 8, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = mode == 0 ? gelu_erf(v[e]) : tanhf(v[e]);
+    for (int e = 0; e < 8; ++e) v[e] = mode == 0 ? gelu_fast(v[e]) : tanhf(v[e]);
     stv8(y + i * 8, v);
   }
 }
@@ -402,7 +402,7 @@ __global__ void act_bwd_kernel(const __bf16* __restrict__ dy, const __bf16* __re
     ldv8(dy + i * 8, g);
     ldv8(xy + i * 8, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] *= mode == 0 ? dgelu_erf(v[e]) : (1.f - v[e] * v[e]);
+    for (int e = 0; e < 8; ++e) g[e] *= mode == 0 ? dgelu_fast(v[e]) : (1.f - v[e] * v[e]);
     stv8(dx + i * 8, g);
   }
 }

@@ -156,18 +156,13 @@ def join_side(result, ev):
     return result
 
 
-_SIDE_WGS = []
-
-
 def _side_wgrad_wgs() -> int:
     """Split-K workgroup target of side-stream WGRADs (``PCMP_SIDE_WGRAD_WGS``, default 384; 0 keeps
-    the per-shape autotune, which times each WGRAD alone)."""
-    if not _SIDE_WGS:
-        try:
-            _SIDE_WGS.append(max(0, int(os.environ.get("PCMP_SIDE_WGRAD_WGS", "384"))))
-        except ValueError:
-            _SIDE_WGS.append(384)
-    return _SIDE_WGS[0]
+    the per-shape autotune, which times each WGRAD alone).  Read per call so A/B runs can flip it."""
+    try:
+        return max(0, int(os.environ.get("PCMP_SIDE_WGRAD_WGS", "384")))
+    except ValueError:
+        return 384
 
 
 def run_on_side(fn: Callable[[], None], keep_alive) -> None:

@@ -321,14 +321,20 @@ def _lsr(z, k):
 
 
 def hash_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    """Bit-exact torch port of ``uniform01`` in csrc/common.h (splitmix64 finaliser)."""
-    z = torch.bitwise_xor(torch.tensor(_s64(seed), dtype=torch.int64, device=idx.device),
-                          idx.long() * _s64(0x9E3779B97F4A7C15))
-    z = torch.bitwise_xor(z, _lsr(z, 30)) * _s64(0xBF58476D1CE4E5B9)
-    z = torch.bitwise_xor(z, _lsr(z, 27)) * _s64(0x94D049BB133111EB)
-    z = torch.bitwise_xor(z, _lsr(z, 31))
-    u32 = z & 0xFFFFFFFF
-    return (u32 >> 8).float() * (1.0 / 16777216.0)
+    """Bit-exact torch port of ``uniform01`` in csrc/common.h (32-bit lowbias32 mixing of the index
+    folded with the 64-bit seed)."""
+    m32 = 0xFFFFFFFF
+    seed &= _M64
+    key = (seed & m32) ^ (((seed >> 32) * 0x9E3779B9) & m32)
+    i = idx.long()
+    x = torch.bitwise_xor(i & m32, (_lsr(i, 32) * 0x85EBCA6B) & m32)
+    x = torch.bitwise_xor(x, key)
+    x = torch.bitwise_xor(x, x >> 16)
+    x = (x * 0x7FEB352D) & m32
+    x = torch.bitwise_xor(x, x >> 15)
+    x = (x * 0x846CA68B) & m32
+    x = torch.bitwise_xor(x, x >> 16)
+    return (x >> 8).float() * (1.0 / 16777216.0)
 
 
 def _salted(seed, salt):

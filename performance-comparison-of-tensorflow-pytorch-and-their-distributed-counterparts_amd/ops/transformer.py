@@ -5,6 +5,7 @@ import torch
 
 from .functions import dropout_rng
 from .kernels import K
+from . import params as _params
 from .params import compute_weight, compute_weight_t, emit_grad, sink_or_temp
 
 
@@ -175,6 +176,28 @@ def _wgrad(p, dy, x):
                                                         acc))
 
 
+def _side_ok(p, t):
+    return (t.is_cuda and p.requires_grad and getattr(p, "main_grad", None) is not None and
+            _params.side_stream_enabled())
+
+
+def _wgrad_bias(p, bias, dy, x):
+    """Weight gradient dy^T x and bias gradient colsum(dy) of one Linear.  With flat gradient sinks
+    they run on the WGRAD side stream (ops/params.py run_on_side), concurrent with the DGRAD /
+    attention / LayerNorm-backward chain that only needs dy -- the same split as the conv blocks.
+    Returns (grad_w, grad_b) for autograd (None when written into a sink)."""
+    if _side_ok(p, dy) and (bias is None or _side_ok(bias, dy)):
+        def run():
+            _wgrad(p, dy, x)
+            if bias is not None:
+                emit_grad(bias, lambda o, acc: K.colsum(dy, o, acc))
+        _params.run_on_side(run, (dy, x))
+        return None, None
+    gw = _wgrad(p, dy, x)
+    gb = emit_grad(bias, lambda o, acc: K.colsum(dy, o, acc)) if bias is not None else None
+    return gw, gb
+
+
 def _ln_fwd(ctx, a, resid, gamma, beta, eps, p):
     seed, off = dropout_rng.next(a.numel()) if p > 0 else (0, 0)
     salt = dropout_rng.salt if p > 0 else None
@@ -224,11 +247,10 @@ class BertAttentionBlockFn(torch.autograd.Function):
         if dy.dtype != dt:
             dy = dy.to(dt)
         dres, da, (gg, gb, gbo) = _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, bo)
-        gwo = _wgrad(wo, da, out)
+        gwo, _ = _wgrad_bias(wo, None, da, out)
         dctx = _dgrad(da, compute_weight(wo, dt), compute_weight_t(wo, dt))
         dqkv = K.attention_bwd(dctx, qkv, out, lse, ids if has_ids else None, B, S, H, p, seed, off, salt)
-        gwq = _wgrad(wqkv, dqkv, h)
-        gbq = emit_grad(bqkv, lambda o, acc: K.colsum(dqkv, o, acc))
+        gwq, gbq = _wgrad_bias(wqkv, bqkv, dqkv, h)
         dh = _dgrad(dqkv, compute_weight(wqkv, dt), compute_weight_t(wqkv, dt), dres) if ctx.needs_input_grad[0] else None
         return dh, None, gwq, gbq, gwo, gbo, gg, gb, None, None, None, None, None, None
 
@@ -255,9 +277,8 @@ class BertFFNBlockFn(torch.autograd.Function):
         if dy.dtype != dt:
             dy = dy.to(dt)
         dres, df, (gg, gb, gb2) = _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, b2)
-        gw2 = _wgrad(w2, df, g)
+        gw2, _ = _wgrad_bias(w2, None, df, g)
         du = K.linear_dgrad_gelu(df, compute_weight(w2, dt), u, compute_weight_t(w2, dt))
-        gw1 = _wgrad(w1, du, h1)
-        gb1 = emit_grad(b1, lambda o, acc: K.colsum(du, o, acc))
+        gw1, gb1 = _wgrad_bias(w1, b1, du, h1)
         dh1 = _dgrad(du, compute_weight(w1, dt), compute_weight_t(w1, dt), dres) if ctx.needs_input_grad[0] else None
         return dh1, gw1, gb1, gw2, gb2, gg, gb, None, None

@@ -21,7 +21,7 @@ dev = torch.device("cuda")
 HIP_ONLY = os.environ.get("SUITE_HIP_ONLY") == "1"   # skip the stock-PyTorch comparators (clean profiles)
 
 
-def timeit(fn, warmup=3, iters=10):
+def timeit(fn, warmup=8, iters=30):
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()

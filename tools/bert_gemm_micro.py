@@ -52,12 +52,16 @@ for name, cin, cout in [("qkv", 768, 2304), ("attn_out", 768, 768), ("ffn1", 768
     if name == "ffn1":
         cases.append((f"{name}_fwd_gelu", fl, lambda x=x, w=w, b=b: ops.linear_gelu_fwd(x, w, b),
                       lambda x=x, w=w, bb=bb: torch.nn.functional.gelu(torch.addmm(bb, x, w.t()))))
+        cases.append((f"{name}_fwd_plain", fl, lambda x4=x4, w4=w4, b=b: ops.conv_fwd(x4, w4, 1, 0, b, None, False, False),
+                      lambda x=x, w=w, bb=bb: torch.addmm(bb, x, w.t())))
     else:
         cases.append((f"{name}_fwd", fl, lambda x4=x4, w4=w4, b=b: ops.conv_fwd(x4, w4, 1, 0, b, None, False, False),
                       lambda x=x, w=w, bb=bb: torch.addmm(bb, x, w.t())))
     if name == "ffn2":
         u = (torch.rand(M, cin, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         cases.append((f"{name}_dgrad_gelu", fl, lambda dy=dy, w=w, u=u, wt4=wt4: ops.linear_dgrad_gelu(dy, w, u, wt4.view(wt4.shape[0], -1)),
+                      lambda dy=dy, w=w: torch.mm(dy, w)))
+        cases.append((f"{name}_dgrad_plain", fl, lambda dy4=dy4, w4=w4, wt4=wt4: ops.conv_dgrad(dy4, w4, 1, 1, 1, 0, None, wt4),
                       lambda dy=dy, w=w: torch.mm(dy, w)))
     elif name in ("qkv", "ffn1"):
         cases.append((f"{name}_dgrad_res", fl,
