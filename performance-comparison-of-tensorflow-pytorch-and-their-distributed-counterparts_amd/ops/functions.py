@@ -129,9 +129,12 @@ class LogSoftmaxFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (logp,) = ctx.saved_tensors
-        if g.dtype != ctx.dtype:
-            g = g.to(ctx.dtype)
-        return K.log_softmax_bwd(g.contiguous(), logp)
+        # the g - exp(logp) * sum(g) math runs at g's precision (fp32 from an fp32 NLL); only the
+        # result is cast to the activation dtype
+        if g.dtype != ctx.dtype and g.dtype != torch.float32:
+            g = g.float()
+        dz = K.log_softmax_bwd(g.contiguous(), logp)
+        return dz if dz.dtype == ctx.dtype else dz.to(ctx.dtype)
 
 
 def linear(x, weight, bias=None, relu=False):

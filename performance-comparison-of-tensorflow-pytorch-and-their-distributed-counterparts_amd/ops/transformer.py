@@ -79,18 +79,14 @@ class AttentionFn(torch.autograd.Function):
 def _partial_rows_grad(p, src2d, n):
     """Gradient of a table parameter whose first ``n`` elements get the column sums of ``src2d``
     (``K.colsum``) and whose other rows get none (BERT's position rows past S, token-type rows > 0).
-    Those rows are zeroed only when they may hold something: a fresh temporary, the first write of
-    the flat slot, or a shorter S than the last write."""
+    Those rows are zeroed on every first write of an accumulation window (one small fill), so no
+    state carried across steps -- a shorter S, an in-place edit of the flat gradient, a loaded
+    gradient -- can leave a stale value there."""
     def compute(out, acc):
         flat = out.view(-1)
         K.colsum(src2d, flat[:n], acc)
         if flat.numel() > n and not acc:
-            own = out is getattr(p, "main_grad", None)
-            seen = getattr(p, "_pcmp_rows_written", None) if own else None
-            if seen is None or seen > n:
-                flat[n:].zero_()
-            if own:
-                p._pcmp_rows_written = n
+            flat[n:].zero_()
     return emit_grad(p, compute)
 
 

@@ -111,6 +111,26 @@ def test_bert_matches_hf():
     assert _rel(m.emb_ln.weight.grad, sd["bert.embeddings.LayerNorm.weight"].grad) < 1e-4
 
 
+def test_bert_position_grad_rows_past_s_stay_zero():
+    """Flat gradient sinks across windows with S1 < S2 > S3: the position rows no token of the
+    current window used hold zero (no stale rows from a longer earlier window)."""
+    from pcmp.models.bert import BertConfig, BertForSequenceClassification
+    from pcmp.utils.flat import FlatParams
+    torch.manual_seed(0)
+    m = BertForSequenceClassification(BertConfig(num_hidden_layers=1, hidden_size=64, num_attention_heads=1,
+                                                 intermediate_size=128, hidden_dropout_prob=0.0,
+                                                 attention_probs_dropout_prob=0.0))
+    flat = FlatParams(m.parameters())
+    for S in (16, 48, 16):
+        flat.zero_grad()
+        ids = torch.randint(1, 30522, (2, S))
+        m(ids, None, None, torch.tensor([0, 1]))[0].backward()
+        g = m.position.main_grad
+        assert float(g[:S].abs().max()) > 0
+        assert float(g[S:].abs().max()) == 0.0, S
+        assert float(m.token_type.main_grad[1:].abs().max()) == 0.0
+
+
 def test_bert_fused_sublayers_match_op_by_op(monkeypatch):
     """The fused sublayer nodes (dropout+residual+LayerNorm fwd/bwd kernels, GELU and residual-grad
     GEMM epilogues) give the op-by-op layer's loss and gradients, dropout ON (same RNG stream)."""
