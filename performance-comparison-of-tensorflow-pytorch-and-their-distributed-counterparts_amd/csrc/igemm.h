@@ -2667,6 +2667,8 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
     for (int ns : {1, 2, 3, 4, 6}) {
       if (ns > 1 && ksteps / ns < 4) continue;
       cands.push_back({1, ns});
+      // 128x64 tiles: twice the 128x128 grid for N <= 1024 (BERT's N = 768 GEMMs: 384 tiles, not 192)
+      if (p.gn <= 1024) cands.push_back({5, ns});
       if (p.gn >= 256) cands.push_back({2, ns});
       if (kn_big.get() & 1 && p.gn >= 256) cands.push_back({7, ns});
       if (kn_big.get() & 2 && p.gn >= 128) cands.push_back({8, ns});

@@ -28,6 +28,8 @@ _compute_dtype: torch.dtype | None = None   # None: bf16 on the GPU, fp32 on the
 def load(build_if_missing: bool = False) -> bool:
     """Load the native op library into ``torch.ops.pcmp``.  Returns True on success."""
     global _loaded, _load_error
+    if _loaded:
+        return True
     with _lock:
         if _loaded:
             return True

@@ -46,13 +46,17 @@ def _first_tensor(args):
 class _Dispatch:
     def __getattr__(self, name):
         refimpl = getattr(ref, name, None)
+        fp32_ref = name in FP32_REF_OPS
+        native = []   # the resolved torch.ops.pcmp.<name>.default overload (per-call host cost counts)
 
         def call(*args):
             t = _first_tensor(args)
             if TRACE is not None:
                 TRACE.append((name, [tuple(a.shape) if isinstance(a, torch.Tensor) else a for a in args]))
-            if _lib.use_native(t) and not (name in FP32_REF_OPS and _lib.precision() == "fp32"):
-                return getattr(torch.ops.pcmp, name)(*args)
+            if _lib.use_native(t) and not (fp32_ref and _lib.precision() == "fp32"):
+                if not native:
+                    native.append(getattr(torch.ops.pcmp, name).default)
+                return native[0](*args)
             if refimpl is None:
                 raise NotImplementedError(f"no reference implementation for {name}")
             return refimpl(*args)

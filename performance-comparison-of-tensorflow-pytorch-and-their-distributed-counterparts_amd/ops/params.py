@@ -108,10 +108,24 @@ def sink_or_temp(p: torch.Tensor | None):
 # PCMP_WGRAD_STREAM=0 keeps everything on one stream.
 _SIDE: dict = {}
 _JOIN_QUEUED = [False]
+_ENV: dict = {}
+
+
+def refresh_env() -> None:
+    """Re-read the side-stream switches (PCMP_WGRAD_STREAM, PCMP_SIDE_WGRAD_WGS); they are cached
+    because run_on_side is on the per-kernel host path (A/B tools call this after editing os.environ)."""
+    _ENV["side"] = os.environ.get("PCMP_WGRAD_STREAM", "1") != "0"
+    try:
+        _ENV["wgs"] = max(0, int(os.environ.get("PCMP_SIDE_WGRAD_WGS", "384")))
+    except ValueError:
+        _ENV["wgs"] = 384
+
+
+refresh_env()
 
 
 def side_stream_enabled() -> bool:
-    return os.environ.get("PCMP_WGRAD_STREAM", "1") != "0"
+    return _ENV["side"]
 
 
 def active_streams(device):
@@ -158,26 +172,49 @@ def join_side(result, ev):
 
 def _side_wgrad_wgs() -> int:
     """Split-K workgroup target of side-stream WGRADs (``PCMP_SIDE_WGRAD_WGS``, default 384; 0 keeps
-    the per-shape autotune, which times each WGRAD alone).  Read per call so A/B runs can flip it."""
-    try:
-        return max(0, int(os.environ.get("PCMP_SIDE_WGRAD_WGS", "384")))
-    except ValueError:
-        return 384
+    the per-shape autotune, which times each WGRAD alone)."""
+    return _ENV["wgs"]
+
+
+# per device: [side stream, ring of fork events, ring position].  run_on_side runs ~50 times per
+# training step, so its host cost counts (BERT-base's eager step is launch-bound on a slow host,
+# profiles/r4_bert_host_prof.txt): raw current-stream get / set instead of Stream objects and the
+# stream context manager, and recycled events instead of one new Event per fork.  A recycled
+# event is re-recorded only after 256 later forks -- the wait enqueued on it long since resolved.
+_SIDE_CTX: dict = {}
+_NEV = 256
+
+
+def _side_ctx(idx: int):
+    c = _SIDE_CTX.get(idx)
+    if c is None:
+        side = _SIDE.get(idx)
+        if side is None:
+            side = _SIDE[idx] = torch.cuda.Stream(idx)
+        c = _SIDE_CTX[idx] = [side, [torch.cuda.Event() for _ in range(_NEV)], 0]
+    return c
 
 
 def run_on_side(fn: Callable[[], None], keep_alive) -> None:
     """Run ``fn`` (kernel launches) on the device's WGRAD stream, ordered after the compute stream's
     work so far; ``keep_alive`` tensors are recorded on the side stream for the caching allocator."""
-    dev = keep_alive[0].device
-    main = torch.cuda.current_stream(dev)
-    side = _SIDE.get(dev.index)
-    if side is None:
-        side = _SIDE[dev.index] = torch.cuda.Stream(dev)
-    key = ("active", dev.index)
-    _SIDE[key] = (main, side)
-    side.wait_stream(main)
-    wgs = _side_wgrad_wgs()
-    with torch.cuda.stream(side):
+    idx = keep_alive[0].get_device()
+    c = _side_ctx(idx)
+    side = c[0]
+    cur = torch._C._cuda_getCurrentStream(idx)   # (stream id, device index, device type)
+    ev = c[1][c[2]]
+    c[2] = (c[2] + 1) % _NEV
+    ev.record()                                   # on the compute stream (current)
+    side.wait_event(ev)
+    if not _JOIN_QUEUED[0]:
+        main = torch.cuda.Stream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
+        key = ("active", idx)
+        _SIDE[key] = (main, side)
+        _JOIN_QUEUED[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(main, side, key))
+    wgs = _ENV["wgs"]
+    torch._C._cuda_setStream(stream_id=side.stream_id, device_index=idx, device_type=side.device_type)
+    try:
         if wgs:
             prev = torch.ops.pcmp.set_knob("wgrad_wgs", wgs)
             try:
@@ -186,8 +223,7 @@ def run_on_side(fn: Callable[[], None], keep_alive) -> None:
                 torch.ops.pcmp.set_knob("wgrad_wgs", prev)   # keep a PCMP_KNOBS=wgrad_wgs=N setting
         else:
             fn()
+    finally:
+        torch._C._cuda_setStream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
     for t in keep_alive:
         t.record_stream(side)
-    if not _JOIN_QUEUED[0]:
-        _JOIN_QUEUED[0] = True
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(main, side, key))

@@ -1,4 +1,5 @@
-"""Run N training steps of one secondary workload (for rocprofv3): python tools/prof_target.py bert|bilstm|resnet18"""
+"""Run N training steps of one secondary workload (for rocprofv3):
+python tools/prof_target.py bert|bert_graph|bilstm|resnet18 [steps]   (bert_graph: GraphedStep replays)"""
 import os
 import sys
 
@@ -14,9 +15,9 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 13
 from pcmp.engine.trainer import make_state  # noqa: E402
 from pcmp.data.synthetic import SyntheticIMDB  # noqa: E402
 
-if what in ("bert", "bilstm"):
+if what in ("bert", "bert_graph", "bilstm"):
     ids, mask, y = SyntheticIMDB(32, 128).get_batch(list(range(32)), dev)
-    if what == "bert":
+    if what in ("bert", "bert_graph"):
         from pcmp.models.bert import bert_base
         m = bert_base().to(dev)
         st = make_state(m, "adamw", lr=2e-5, eps=1e-8, clip=1.0)
@@ -33,8 +34,17 @@ else:
     y = torch.randint(0, 1000, (256,), device=dev)
     st = make_state(m, "sgd", lr=0.1, momentum=0.9)
     loss_fn = lambda: cross_entropy(m.forward_logits(x), y)  # noqa: E731
-for _ in range(steps):
-    st.zero_grad()
-    st.backward_step(loss_fn())
+if what == "bert_graph":
+    from pcmp.engine.graph import GraphedStep
+    for _ in range(4):
+        st.zero_grad()
+        st.backward_step(loss_fn())
+    g = GraphedStep(st, lambda a, b, c: m(a, None, b, c)[0], [ids, mask, y])
+    for _ in range(steps):
+        g(ids, mask, y)
+else:
+    for _ in range(steps):
+        st.zero_grad()
+        st.backward_step(loss_fn())
 torch.cuda.synchronize()
 print("done", what, steps)
