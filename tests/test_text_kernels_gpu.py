@@ -303,7 +303,7 @@ def test_graphed_bert_step_matches_eager_without_dropout(gpu):
                 st.zero_grad()
                 loss = fn(ids, mask, y)
                 st.backward_step(loss)
-                out.append(float(loss))
+                out.append(loss.detach().item())
         losses[mode] = out
     for a, b in zip(losses["eager"], losses["graph"]):
         assert abs(a - b) <= 1e-3 * max(1.0, abs(a)), losses
