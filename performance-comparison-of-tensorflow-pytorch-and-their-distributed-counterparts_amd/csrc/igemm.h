@@ -104,6 +104,9 @@ struct IgemmParams {
   // of the bn_apply pass that would write y (register-staged kernel; FWD: 1x1 stride-1 convs)
   const float* act_sc;
   const float* act_sh;
+  // DGRAD (stride 1): the residual is sub-sampled -- resid is [N][rs_H2][rs_W2][gn] and adds at
+  // output pixels (2i, 2j) only (a 1x1 stride-2 downsample's DGRAD, which is zero elsewhere)
+  int resid_sub, rs_H2, rs_W2;
 };
 
 // y = relu(a*z + b) of one 16-B chunk (8 channels), bf16-rounded as bn_apply rounds; 0 for an
@@ -284,19 +287,22 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
     const bool has_mb = bnr && p.bn_mbits != nullptr;
     const bool has_mk = bnr && !has_mb && p.bn_mask != nullptr;
     const bool mfx = bnr && !has_mb && !has_mk && p.bn_msc != nullptr;   // ReLU mask recomputed from x
-    // output row offsets of the TM pixel-row groups
+    // output row offsets of the TM pixel-row groups (rrows: the residual's, -1 = no residual term)
     size_t orows[TM];
+    int rrows[MODE == MODE_DGRAD ? TM : 1];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wr * WTM + i * 16 + fr;
       size_t orow = m < p.gm ? m : 0;
       if constexpr (MODE == MODE_DGRAD) {
-        if (p.sub && m < p.gm) {
+        rrows[i] = (int)orow;
+        if ((p.sub || p.resid_sub) && m < p.gm) {
           const int n = fdiv(m, p.fd_HW);
           const int rem = m - n * p.dH * p.dW;
           const int hh = fdiv(rem, p.fd_W);
           const int ww = rem - hh * p.dW;
-          orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
+          if (p.sub) orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
+          else rrows[i] = ((hh | ww) & 1) ? -1 : (n * p.rs_H2 + (hh >> 1)) * p.rs_W2 + (ww >> 1);
         }
       }
       orows[i] = orow;
@@ -321,7 +327,25 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
           d[0] = t2.x; d[1] = t2.y;
         }
       };
-      if (has_res) ldv(rvA[b], p.resid);
+      if (has_res) {
+        if constexpr (MODE == MODE_DGRAD) {
+          if (p.resid_sub) {   // sub-sampled residual: zero where rrows < 0
+            const bool okr = ok && rrows[i] >= 0;
+            const size_t ro = (size_t)(okr ? rrows[i] : 0) * p.gn + (ok ? n : 0);
+            if constexpr (VW == 8) {
+              const uint4 t4 = okr ? *reinterpret_cast<const uint4*>(p.resid + ro) : uint4{0, 0, 0, 0};
+              rvA[b][0] = t4.x; rvA[b][1] = t4.y; rvA[b][2] = t4.z; rvA[b][3] = t4.w;
+            } else {
+              const uint2 t2 = okr ? *reinterpret_cast<const uint2*>(p.resid + ro) : uint2{0, 0};
+              rvA[b][0] = t2.x; rvA[b][1] = t2.y;
+            }
+          } else {
+            ldv(rvA[b], p.resid);
+          }
+        } else {
+          ldv(rvA[b], p.resid);
+        }
+      }
       if constexpr (bnr) {
         if (has_mb) {   // o is a multiple of VW: the store's channels are bits (o & 7) .. +VW-1 of byte o/8
           const unsigned byte = ok ? p.bn_mbits[o >> 3] : 0u;
@@ -2742,6 +2766,7 @@ static void fill_geometry(IgemmParams& p, int N, int H, int W, int C, int K, int
   p.relu = 0; p.alpha = 1.f; p.accumulate = 0; p.nsplit = 1;
   p.fold_x = nullptr; p.fold_coef = nullptr; p.fold_lds = 0;
   p.act_sc = nullptr; p.act_sh = nullptr;
+  p.resid_sub = 0; p.rs_H2 = 0; p.rs_W2 = 0;
 }
 
 // ---- entry points (igemm_fwd.hip / igemm_dgrad.hip / igemm_wgrad.hip; registered in igemm.hip)
@@ -2766,7 +2791,7 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& mshift, const c10::optional<at::Tensor>& wt,
                                        const c10::optional<at::Tensor>& ymask_bits,
                                        const c10::optional<at::Tensor>& fold_x,
-                                       const c10::optional<at::Tensor>& fold_coef);
+                                       const c10::optional<at::Tensor>& fold_coef, bool resid_sub);
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S,
                 int64_t stride, int64_t pad, bool accumulate, const c10::optional<at::Tensor>& fold_x,
                 const c10::optional<at::Tensor>& fold_coef, const c10::optional<at::Tensor>& in_scale,

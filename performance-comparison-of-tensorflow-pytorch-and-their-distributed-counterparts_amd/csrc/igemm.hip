@@ -126,7 +126,8 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::conv_dgrad);
   m.def("conv_dgrad_bnr(Tensor dy, Tensor w, int H, int W, int stride, int pad, Tensor? resid, Tensor? ymask, "
         "Tensor x, Tensor mean, Tensor invstd, Tensor? x2, Tensor? mean2, Tensor? invstd2, Tensor? mscale, "
-        "Tensor? mshift, Tensor? wt=None, Tensor? ymask_bits=None, Tensor? fold_x=None, Tensor? fold_coef=None) -> Tensor[]",
+        "Tensor? mshift, Tensor? wt=None, Tensor? ymask_bits=None, Tensor? fold_x=None, Tensor? fold_coef=None, "
+        "bool resid_sub=False) -> Tensor[]",
         &pcmp::conv_dgrad_bnr);
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate, "
         "Tensor? fold_x=None, Tensor? fold_coef=None, Tensor? in_scale=None, Tensor? in_shift=None) -> ()",

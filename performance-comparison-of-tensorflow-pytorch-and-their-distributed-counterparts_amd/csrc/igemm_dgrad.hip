@@ -38,7 +38,7 @@ struct BnrArgs {  // fused BatchNorm-backward reduction in the dgrad epilogue (s
 static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
                                           int64_t stride, int64_t pad, const c10::optional<at::Tensor>& resid,
                                           const BnrArgs* bn, const c10::optional<at::Tensor>& wt_given,
-                                          const at::Tensor* dgelu_u = nullptr) {
+                                          const at::Tensor* dgelu_u = nullptr, bool resid_sub = false) {
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(w);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(w);
   const int N = dy.size(0), K = w.size(0), R = w.size(1), S = w.size(2), C = w.size(3);
@@ -48,7 +48,15 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   const bool has_res = resid.has_value() && resid->defined();
   if (has_res) {
     PCMP_CHECK_BF16(*resid); PCMP_CHECK_CONTIG(*resid);
-    TORCH_CHECK(resid->numel() == (int64_t)N * H * W * C, "conv_dgrad: residual shape");
+    if (resid_sub) {
+      TORCH_CHECK(stride == 1, "conv_dgrad: a sub-sampled residual needs a stride-1 DGRAD");
+      p.resid_sub = 1; p.rs_H2 = (int)(H + 1) / 2; p.rs_W2 = (int)(W + 1) / 2;
+      TORCH_CHECK(resid->numel() == (int64_t)N * p.rs_H2 * p.rs_W2 * C, "conv_dgrad: sub-sampled residual shape");
+    } else {
+      TORCH_CHECK(resid->numel() == (int64_t)N * H * W * C, "conv_dgrad: residual shape");
+    }
+  } else {
+    TORCH_CHECK(!resid_sub, "conv_dgrad: resid_sub without a residual");
   }
   auto set_bn = [&](IgemmParams& q) {
     if (!bn) return;
@@ -232,8 +240,9 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& wt,
                                        const c10::optional<at::Tensor>& ymask_bits,
                                        const c10::optional<at::Tensor>& fold_x,
-                                       const c10::optional<at::Tensor>& fold_coef) {
+                                       const c10::optional<at::Tensor>& fold_coef, bool resid_sub) {
   const bool fold = fold_x.has_value() && fold_x->defined();
+  TORCH_CHECK(!resid_sub || dy.scalar_type() != at::kFloat, "conv_dgrad_bnr: the sub-sampled residual is bf16 only");
   TORCH_CHECK(!fold || dy.scalar_type() != at::kFloat, "conv_dgrad_bnr: the BatchNorm-backward fold is bf16 only");
   if (dy.scalar_type() == at::kFloat)
     return f32::conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2, mean2, invstd2, mscale,
@@ -271,7 +280,7 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
     TORCH_CHECK(fold_coef->numel() == 3 * dy.size(-1), "conv_dgrad_bnr: fold_coef must be [3, K]");
     a.fold_x = ptr<__bf16>(*fold_x); a.fold_coef = ptr<float>(*fold_coef);
   }
-  return dgrad_impl(dy, w, H, W, stride, pad, resid, &a, wt);
+  return dgrad_impl(dy, w, H, W, stride, pad, resid, &a, wt, nullptr, resid_sub);
 }
 
 }  // namespace pcmp

@@ -18,6 +18,7 @@ stem conv7x7/2-bn-relu-maxpool3x3/2 (:455-458).
 """
 from __future__ import annotations
 
+import os
 import weakref
 
 import torch
@@ -342,16 +343,38 @@ def _link_prev_tail(x):
     return None
 
 
-def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev):
-    """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue."""
+def _dgrad_into_prev(dh, w, H, W, L, resid, x, prev, resid_sub=False):
+    """dx = dgrad(dh) + resid, masked by x > 0, with prev's BN reduction fused in the epilogue
+    (``resid_sub``: resid is a 1x1 stride-2 downsample's compact DGRAD, added at even pixels)."""
     mask = None if prev.mbits is not None else x
     g, fx, fc = _fold_args(dh)
     r = K.conv_dgrad_bnr(g, w, H, W, L.stride, L.pad, resid, mask, prev.c, prev.mean, prev.invstd,
                          prev.cd, prev.meand, prev.invstdd, None, None, compute_weight_t(L.weight, g.dtype),
-                         prev.mbits, fx, fc)
+                         prev.mbits, fx, fc, resid_sub)
     prev.parts = r[1:]
     prev.g_ptr = r[0].data_ptr()
     return r[0]
+
+
+# PCMP_COMPACT_DOWN=0: the downsample DGRAD writes the dense zero-filled [N, H, W, C] gradient (A/B)
+_COMPACT_DOWN = os.environ.get("PCMP_COMPACT_DOWN", "1") != "0"
+
+
+def _compact_down_dgrad_ok(dcd, down, H, W) -> bool:
+    return (down.R == 1 and down.S == 1 and down.stride == 2 and down.pad == 0 and H % 2 == 0 and W % 2 == 0
+            and dcd.dtype == torch.bfloat16 and dcd.shape[1] * 2 == H and dcd.shape[2] * 2 == W)
+
+
+def _compact_down_dgrad(dcd, down, H, W):
+    """A 1x1 stride-2 pad-0 downsample's DGRAD is nonzero only at the even pixels (2i, 2j) of its
+    [N, H, W, C] input gradient, where it is a plain stride-1 1x1 DGRAD of dcd: computed compact
+    ([N, H/2, W/2, C]) it needs no zero fill of the other 3/4, and the conv1 DGRAD that adds it
+    (``conv_dgrad_bnr(..., resid_sub=True)``) reads a quarter of the bytes."""
+    wd = compute_weight(down.weight, dcd.dtype)
+    wdt = compute_weight_t(down.weight, dcd.dtype)
+    if wdt is not None:   # 1x1 stride 2: the class-blocked layout holds class (0, 0) only = [C][1][1][K]
+        wdt = wdt.view(wd.shape[3], 1, 1, wd.shape[0])
+    return K.conv_dgrad(dcd, wd, dcd.shape[1], dcd.shape[2], 1, 0, None, wdt)
 
 
 def _side_branch_ok(t, L) -> bool:
@@ -487,11 +510,17 @@ class ResidualBlockFn(torch.autograd.Function):
         # stream, concurrently with the main branch's backward chain
         prev0 = ctx.prev_tail if (need_dx and _bnr_ok(main[0])) else None
         tfork = None
+        t_sub = False
         if down is not None and prev0 is not None and _side_branch_ok(dcd, down):
             wd = compute_weight(down.weight, dcd.dtype)
             wdt = compute_weight_t(down.weight, dcd.dtype)
-            tfork = _params.fork_side(lambda: K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt),
-                                      (dcd, wd, wdt))
+            # the consumer (the main branch's first DGRAD) takes the compact form only at stride 1
+            t_sub = _COMPACT_DOWN and main[0].stride == 1 and _compact_down_dgrad_ok(dcd, down, H, W)
+            if t_sub:
+                tfork = _params.fork_side(lambda: _compact_down_dgrad(dcd, down, H, W), (dcd, wd))
+            else:
+                tfork = _params.fork_side(lambda: K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt),
+                                          (dcd, wd, wdt))
         for i in range(len(main) - 1, -1, -1):
             L = main[i]
             _wgrad(L, dh, acts[i], grads)
@@ -533,7 +562,8 @@ class ResidualBlockFn(torch.autograd.Function):
                                 t = _params.join_side(*tfork)
                             else:
                                 t = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, None, wdt)
-                            dx = _dgrad_into_prev(dh, wcomp, H, W, L, t, x, prev)
+                                t_sub = False
+                            dx = _dgrad_into_prev(dh, wcomp, H, W, L, t, x, prev, t_sub)
                         else:
                             t = K.conv_dgrad(_mat(dh), wcomp, H, W, L.stride, L.pad, None, wt)
                             dx = K.conv_dgrad(dcd, wd, H, W, down.stride, down.pad, t, wdt)

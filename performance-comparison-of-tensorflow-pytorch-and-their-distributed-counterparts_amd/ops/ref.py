@@ -65,8 +65,17 @@ def fold_dz(g, x, coef):
     return (c[0] * g.float() + c[1] * x.float() + c[2]).to(g.dtype)
 
 
+def expand_sub_resid(r, H, W):
+    """[N, ceil(H/2), ceil(W/2), C] sub-sampled residual -> [N, H, W, C], zero off the (2i, 2j) pixels."""
+    full = torch.zeros(r.shape[0], H, W, r.shape[-1], dtype=r.dtype, device=r.device)
+    full[:, 0::2, 0::2] = r
+    return full
+
+
 def conv_dgrad_bnr(dy, w, H, W, stride, pad, resid, ymask, x, mean, invstd, x2=None, mean2=None, invstd2=None,
-                   mscale=None, mshift=None, wt=None, ymask_bits=None, fold_x=None, fold_coef=None):
+                   mscale=None, mshift=None, wt=None, ymask_bits=None, fold_x=None, fold_coef=None, resid_sub=False):
+    if resid_sub and resid is not None:
+        resid = expand_sub_resid(resid, H, W)
     if fold_x is not None:
         dy = fold_dz(dy, fold_x, fold_coef)
     if ymask_bits is not None:                    # mask as bits (bn_apply mbits)

@@ -865,3 +865,33 @@ def test_wgrad_act_fold(gpu, K, C, dzfold):
         ops.conv_wgrad(dz, z, of, 1, 1, 1, 0, False, None, None, sc, sh)
     ops.conv_wgrad(dz, y, ou, 1, 1, 1, 0, False)
     close_el(of, ou, rel=1e-3, abs_frac=1e-4)
+
+
+@pytest.mark.parametrize("two", [False, True])
+def test_dgrad_bnr_sub_sampled_residual(gpu, two):
+    """conv_dgrad_bnr with a compact 1x1 stride-2 downsample DGRAD as the residual (resid_sub: added at
+    the even pixels only) == the same call with that residual expanded dense (zeros elsewhere),
+    bitwise, including the fused BN-backward partial sums; the compact residual itself is the
+    stride-1 DGRAD of the downsample gradient on the half-resolution grid."""
+    torch.manual_seed(11)
+    ops = _ops()
+    N, H, C, K, Kd = 8, 28, 256, 128, 512
+    dh = rnd(N, H, H, K, dev=gpu)
+    w = rnd(K, 1, 1, C, dev=gpu, scale=0.1)
+    dcd = rnd(N, H // 2, H // 2, Kd, dev=gpu)
+    wd = rnd(Kd, 1, 1, C, dev=gpu, scale=0.05)
+    t_dense = ops.conv_dgrad(dcd, wd, H, H, 2, 0, None)
+    t_sub = ops.conv_dgrad(dcd, wd, H // 2, H // 2, 1, 0, None)
+    assert torch.equal(ref.expand_sub_resid(t_sub, H, H), t_dense)
+    x = rnd(N, H, H, C, dev=gpu)
+    mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    ymask = rnd(N, H, H, C, dev=gpu).relu()
+    extra = (x, mean, invstd) if two else (None, None, None)
+    a = ops.conv_dgrad_bnr(dh, w, H, H, 1, 0, t_dense, ymask, x, mean, invstd, *extra, None, None)
+    b = ops.conv_dgrad_bnr(dh, w, H, H, 1, 0, t_sub, ymask, x, mean, invstd, *extra, None, None, None, None,
+                           None, None, True)
+    assert len(a) == len(b)
+    for ta, tb in zip(a, b):
+        assert torch.equal(ta, tb)
+    r = ref.conv_dgrad_bnr(dh, w, H, H, 1, 0, t_sub, ymask, x, mean, invstd, *extra, resid_sub=True)
+    close(b[0], r[0])
