@@ -318,6 +318,129 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) gemm_v3(const __bf16* __restr
     }
 }
 
+// V4: V3 (fenced halves, one barrier per K-tile) on v_mfma_f32_32x32x16_bf16: 32x32 output tiles,
+// K = 16 per instruction (lane: row / column lane & 31, k-group (lane >> 5) * 8), half as many MFMA
+// instructions as 16x16x32 for the same wave tile and the same ds_read bytes.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64, 1) gemm_v4(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                         __bf16* __restrict__ C, int M, int N, int K, unsigned a_bytes,
+                                                         unsigned b_bytes) {
+  constexpr int NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_m = lin / tiles_n, tile_n = lin % tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk = K / BK;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(A, a_bytes), rsB = make_rsrc(B, b_bytes);
+  const int gch = (lane & 7) ^ (lane >> 3);
+  unsigned a_vo[NA], b_vo[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + (wid * NA + i) * 8 + (lane >> 3);
+    a_vo[i] = m < M ? (unsigned)(m * K + gch * 8) * 2u : kOOB;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + (wid * NB + i) * 8 + (lane >> 3);
+    b_vo[i] = n < N ? (unsigned)(n * K + gch * 8) * 2u : kOOB;
+  }
+  auto issue = [&](int s, int k0, bool live) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(smem + s * STAGE + (wid * NA + i) * 1024), 16,
+                                               (int)(live ? a_vo[i] + k0 * 2 : kOOB), 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(smem + s * STAGE + A_BYTES + (wid * NB + i) * 1024), 16,
+                                               (int)(live ? b_vo[i] + k0 * 2 : kOOB), 0, 0, 0);
+  };
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][i][r] = 0.f;
+  // a half = 32 of the tile's 64 K = two 16-deep MFMA steps; fragments of both steps read together
+  bf16x8 fa0[2][TM], fb0[2][TN], fa1[2][TM], fb1[2][TN];
+  auto rd = [&](bf16x8(&fa)[2][TM], bf16x8(&fb)[2][TN], int half, int s) {
+    const char* sA = smem + s * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ch = half * 4 + q * 2 + (lane >> 5);   // 16-B chunk (8 k) of this lane's k-group
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[q][i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[q][j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 32 + (lane & 31), ch));
+    }
+  };
+  auto mma = [&](bf16x8(&fa)[2][TM], bf16x8(&fb)[2][TN]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[q][j], fa[q][i], acc[j][i], 0, 0, 0);
+  };
+  constexpr int NMF = 2 * TM * TN, NDS = 2 * (TM + TN), NVM = NA + NB;
+  issue(0, 0, true);
+  issue(1, BK, nk > 1);
+  wait_vm<NA + NB>();
+  lds_sync();
+  rd(fa0, fb0, 0, 0);
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    rd(fa1, fb1, 1, s);
+    mma(fa0, fb0);
+#pragma unroll
+    for (int g = 0; g < NDS; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (g % (NDS / NMF > 0 ? NDS / NMF : 1) == 0) __builtin_amdgcn_sched_group_barrier(0x8, NMF >= NDS ? NMF / NDS : 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vm<0>();
+    lds_sync();
+    __builtin_amdgcn_sched_barrier(0);
+    issue(s, (t + 2) * BK, t + 2 < nk);
+    rd(fa0, fb0, 0, s ^ 1);
+    mma(fa1, fb1);
+#pragma unroll
+    for (int g = 0; g < NDS; ++g) {
+      if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+      if (g % (NDS / NMF > 0 ? NDS / NMF : 1) == 0) __builtin_amdgcn_sched_group_barrier(0x8, NMF >= NDS ? NMF / NDS : 1, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  wait_vm<0>();
+  // 32x32 accumulator: register r of lane l holds C[row][col], col = l & 31,
+  // row = 8 * (r / 4) + 4 * (l >> 5) + (r % 4); here the MFMA ran B (rows = n) x A (cols = m)
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + i * 32 + (lane & 31);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int n = n0 + wc * WTN + j * 32 + 8 * r4 + 4 * (lane >> 5);
+        if (m < M && n < N) {
+          uint2 w;
+          w.x = f2bf(acc[j][i][4 * r4]) | ((unsigned)f2bf(acc[j][i][4 * r4 + 1]) << 16);
+          w.y = f2bf(acc[j][i][4 * r4 + 2]) | ((unsigned)f2bf(acc[j][i][4 * r4 + 3]) << 16);
+          *reinterpret_cast<uint2*>(C + (size_t)m * N + n) = w;
+        }
+      }
+    }
+}
+
 __global__ void ref_gemm(const __bf16* A, const __bf16* B, float* C, int M, int N, int K) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x, m = blockIdx.y;
   if (n >= N) return;
@@ -369,18 +492,29 @@ void launch_v3(const __bf16* A, const __bf16* B, __bf16* C, int M, int N, int K,
                      (unsigned)((size_t)M * K * 2), (unsigned)((size_t)N * K * 2));
 }
 
+template <int BM, int BN, int WM, int WN>
+void launch_v4(const __bf16* A, const __bf16* B, __bf16* C, int M, int N, int K, hipStream_t st) {
+  static bool attr = false;
+  constexpr size_t smem = 2 * (BM + BN) * BK * 2;
+  auto kfn = &gemm_v4<BM, BN, WM, WN>;
+  if (!attr) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(WM * WN * 64), smem, st, A, B, C, M, N, K,
+                     (unsigned)((size_t)M * K * 2), (unsigned)((size_t)N * K * 2));
+}
+
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 3;
   std::vector<Variant> vars = {
-      {"v1_256x256_w4", launch_v1<256, 256, 2, 2>, 256, 256},
-      {"v1_256x256_w8", launch_v1<256, 256, 2, 4>, 256, 256},
-      {"v1_256x128_w4", launch_v1<256, 128, 2, 2>, 256, 128},
-      {"v3ns_256x256_w4", launch_v3<256, 256, 2, 2, 0>, 256, 256},
-      {"v3_256x256_w4", launch_v3<256, 256, 2, 2, 1>, 256, 256},
-      {"v3_256x256_w8", launch_v3<256, 256, 2, 4, 1>, 256, 256},
-      {"v3f_256x256_w4", launch_v3<256, 256, 2, 2, 2>, 256, 256},
       {"v3f_256x256_w8", launch_v3<256, 256, 2, 4, 2>, 256, 256},
-      {"v3_256x128_w4", launch_v3<256, 128, 2, 2, 1>, 256, 128},
+      {"v4_256x256_w8", launch_v4<256, 256, 2, 4>, 256, 256},
+      {"v3f_256x256_w4", launch_v3<256, 256, 2, 2, 2>, 256, 256},
+      {"v4_256x256_w4", launch_v4<256, 256, 2, 2>, 256, 256},
+      {"v3f_128x128_w4", launch_v3<128, 128, 2, 2, 2>, 128, 128},
+      {"v4_128x128_w4", launch_v4<128, 128, 2, 2>, 128, 128},
   };
   struct Shape { int M, N, K; };
   std::vector<Shape> shapes = {{4096, 4096, 4096}, {8192, 8192, 8192}, {50176, 256, 2304}, {12544, 512, 4608},
