@@ -2560,6 +2560,197 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
 
 
 // ------------------------------------------------------------------------------------------------
+// Plain-GEMM kernel on v_mfma_f32_32x32x16_bf16 (plan kinds 9 / 10): C[m][n] = sum_k A[m][k] B[n][k]
+// for the stride-1 1x1 FWD / DGRAD GEMMs the planner handles (Linear layers: A = x or dy, B = w or
+// the transposed weight, both K-contiguous), with the plain epilogue (bias, residual, ReLU, GELU
+// forward with the u side output, GELU backward through resid) or fp32 split-K partials.  Main loop:
+// the LDS-DMA double buffer with one barrier per 64-deep K-tile and fenced halves of
+// tools/gemm_lab (v4); 32x32x16 issues half the MFMA instructions of 16x16x32 for the same wave
+// tile and ds_read bytes: +5-12 % on 128x128 4-wave tiles in the lab (profiles/r4_gemm_lab_mfma32.txt).
+// Accumulator of lane l, 32x32 tile: C column (lane & 31) = row m of the output, register r holds
+// output channel 8 * (r / 4) + 4 * (l >> 5) + (r % 4) of the tile (the MFMA runs B x A).
+template <int BM, int BN, int WM, int WN, int MINB>
+__global__ void __launch_bounds__(WM * WN * 64, MINB) gemm32_kernel(const IgemmParams p) {
+  constexpr int NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;
+  static_assert(NA * 8 * NW == BM && NB * 8 * NW == BN && TM >= 1 && TN >= 1, "gemm32 tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int M = p.gm, N = p.gn, K = p.gk;
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / tiles_mn;
+  const int tt = lin - split * tiles_mn;
+  const int tile_m = tt / p.tiles_n, tile_n = tt - (tt / p.tiles_n) * p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = split * p.ksplit;
+  const int nk = (min(K, kbeg + p.ksplit) - kbeg) / BK;
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes), rsB = make_rsrc(p.b, p.b_bytes);
+  const int gch = (lane & 7) ^ (lane >> 3);
+  unsigned a_vo[NA], b_vo[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + (wid * NA + i) * 8 + (lane >> 3);
+    a_vo[i] = m < M ? (unsigned)((size_t)m * K + kbeg + gch * 8) * 2u : kOOB;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + (wid * NB + i) * 8 + (lane >> 3);
+    b_vo[i] = n < N ? (unsigned)((size_t)n * K + kbeg + gch * 8) * 2u : kOOB;
+  }
+  auto issue = [&](int s, int k0, bool live) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(smem + s * STAGE + (wid * NA + i) * 1024), 16,
+                                               (int)(live && a_vo[i] != kOOB ? a_vo[i] + k0 * 2 : kOOB), 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(smem + s * STAGE + A_BYTES + (wid * NB + i) * 1024), 16,
+                                               (int)(live && b_vo[i] != kOOB ? b_vo[i] + k0 * 2 : kOOB), 0, 0, 0);
+  };
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][i][r] = 0.f;
+  bf16x8 fa0[2][TM], fb0[2][TN], fa1[2][TM], fb1[2][TN];
+  auto rd = [&](bf16x8(&fa)[2][TM], bf16x8(&fb)[2][TN], int half, int s) {
+    const char* sA = smem + s * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ch = half * 4 + q * 2 + (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[q][i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[q][j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 32 + (lane & 31), ch));
+    }
+  };
+  auto mma = [&](bf16x8(&fa)[2][TM], bf16x8(&fb)[2][TN]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[q][j], fa[q][i], acc[j][i], 0, 0, 0);
+  };
+  constexpr int NMF = 2 * TM * TN, NDS = 2 * (TM + TN), NVM = NA + NB;
+  constexpr int DPM = NDS / NMF > 0 ? NDS / NMF : 1, MPD = NMF >= NDS ? NMF / NDS : 1;
+  if (nk > 0) {
+    issue(0, 0, true);
+    issue(1, BK, nk > 1);
+    wait_vm_b<NA + NB>();
+    lds_sync_b();
+    rd(fa0, fb0, 0, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int s = t & 1;
+      rd(fa1, fb1, 1, s);
+      mma(fa0, fb0);
+#pragma unroll
+      for (int g = 0; g < NDS; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      wait_vm_b<0>();
+      lds_sync_b();
+      __builtin_amdgcn_sched_barrier(0);
+      issue(s, (t + 2) * BK, t + 2 < nk);
+      rd(fa0, fb0, 0, s ^ 1);
+      mma(fa1, fb1);
+#pragma unroll
+      for (int g = 0; g < NDS; ++g) {
+        if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_vm_b<0>();
+  }
+  // ---- epilogue: lane = output row m, 4 groups of 4 consecutive channels per 32x32 tile ----------
+  if (p.nsplit > 1) {
+    float* ws = reinterpret_cast<float*>(p.out) + (size_t)split * M * N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wr * WTM + i * 32 + (lane & 31);
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int n = n0 + wc * WTN + j * 32 + 8 * r4 + 4 * (lane >> 5);
+          if (m < M && n < N)
+            *reinterpret_cast<f32x4*>(ws + (size_t)m * N + n) =
+                f32x4{acc[j][i][4 * r4], acc[j][i][4 * r4 + 1], acc[j][i][4 * r4 + 2], acc[j][i][4 * r4 + 3]};
+        }
+      }
+    return;
+  }
+  __bf16* out = reinterpret_cast<__bf16*>(p.out);
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + i * 32 + (lane & 31);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const int n = n0 + wc * WTN + j * 32 + 8 * r4 + 4 * (lane >> 5);
+        if (m >= M || n >= N) continue;
+        const size_t o = (size_t)m * N + n;
+        float x[4];
+        const f32x4 b4 = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = acc[j][i][4 * r4 + e] + b4[e];
+        if (p.resid) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(p.resid + o);
+          const float r[4] = {__uint_as_float(rv.x << 16), __uint_as_float(rv.x & 0xffff0000u),
+                              __uint_as_float(rv.y << 16), __uint_as_float(rv.y & 0xffff0000u)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = p.relu == 3 ? x[e] * dgelu_fast(r[e]) : x[e] + r[e];
+        }
+        if (p.relu == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
+        } else if (p.relu == 2) {   // u (bf16) -> aux; out = gelu(u)
+          const unsigned u0 = f2bf2(x[0], x[1]), u1 = f2bf2(x[2], x[3]);
+          *reinterpret_cast<uint2*>(p.aux + o) = uint2{u0, u1};
+          x[0] = gelu_fast(__uint_as_float(u0 << 16));
+          x[1] = gelu_fast(__uint_as_float(u0 & 0xffff0000u));
+          x[2] = gelu_fast(__uint_as_float(u1 << 16));
+          x[3] = gelu_fast(__uint_as_float(u1 & 0xffff0000u));
+        }
+        *reinterpret_cast<uint2*>(out + o) = uint2{f2bf2(x[0], x[1]), f2bf2(x[2], x[3])};
+      }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int MINB>
+static void launch_gemm32(IgemmParams& p, hipStream_t st) {
+  TORCH_CHECK(p.R == 1 && p.S == 1 && p.stride == 1 && p.pad == 0 && p.gk % BK == 0 && p.ksplit % BK == 0 &&
+                  !p.stats && !p.bn_x && !p.fold_x && !p.act_sc && p.gn % 4 == 0,
+              "gemm32: plain 1x1 GEMMs only");
+  p.tiles_m = ceil_div(p.gm, BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
+  constexpr size_t smem = (size_t)2 * (BM + BN) * BK * 2;
+  static_assert(smem <= 160 * 1024, "gemm32: LDS budget");
+  auto kfn = &gemm32_kernel<BM, BN, WM, WN, MINB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(WM * WN * 64), smem, st, p);
+  PCMP_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Plain-GEMM planner: a stride-1 1x1 convolution without a BatchNorm epilogue is a plain GEMM
 // (every Linear layer: BERT-base's M = 4096-token projections, the VGG16 classifier, the transfer
 // heads).  Those shapes have too few 128x128 / 256x256 tiles to fill 256 CUs (BERT's N = 768
@@ -2570,6 +2761,7 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
 // captured).  This replaces the round-1 hipBLASLt candidate for these GEMMs.
 inline Knob kn_gemm_plan("gemm_plan", 1);   // 0 = default dispatch only, 1 = autotuned plan
 inline Knob kn_plan_force("plan_force", -1); // tests: >= 0 restricts the candidates to that kind (uncached)
+inline Knob kn_gemm32("gemm32", 1);          // 32x32x16-MFMA plain-GEMM candidates (plan kinds 9 / 10)
 inline Knob kn_plan_nsplit("plan_nsplit", 0); // tests: >= 1 (with plan_force) also pins the split count
 
 struct GemmPlan {
@@ -2588,6 +2780,8 @@ static const char* plan_kind_name(int k) {
     case 6: return "skinny64x64";
     case 7: return "big256x256";
     case 8: return "big256x128";
+    case 9: return "m32_128x128";
+    case 10: return "m32_256x256";
     default: return "default";
   }
 }
@@ -2617,6 +2811,8 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   else if (pl.kind == 5) launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st);
   else if (pl.kind == 7) launch_big<MODE, 256>(p, st);
   else if (pl.kind == 8) launch_big<MODE, 128>(p, st);
+  else if (pl.kind == 9) launch_gemm32<128, 128, 2, 2, 2>(p, st);
+  else if (pl.kind == 10) launch_gemm32<256, 256, 2, 2, 1>(p, st);
   else if (pl.kind == 6) {
     if constexpr (MODE == MODE_FWD) launch_skinny(p, st);
     else TORCH_CHECK(false, "skinny kernel is FWD only");
@@ -2693,6 +2889,10 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
       cands.push_back({1, ns});
       // 128x64 tiles: twice the 128x128 grid for N <= 1024 (BERT's N = 768 GEMMs: 384 tiles, not 192)
       if (p.gn <= 1024) cands.push_back({5, ns});
+      if (kn_gemm32.get() && p.gn % 4 == 0) {   // 32x32x16 MFMA kernels
+        cands.push_back({9, ns});
+        if (p.gn >= 256) cands.push_back({10, ns});
+      }
       if (p.gn >= 256) cands.push_back({2, ns});
       if (kn_big.get() & 1 && p.gn >= 256) cands.push_back({7, ns});
       if (kn_big.get() & 2 && p.gn >= 128) cands.push_back({8, ns});
