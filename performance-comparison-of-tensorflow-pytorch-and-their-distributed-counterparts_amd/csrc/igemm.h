@@ -134,6 +134,7 @@ constexpr int NT = 256;
 
 // DGRAD + BN-backward-reduce epilogue: register-ring depth of its resid / x / mask loads (2 = one
 // step ahead, round 1; 4 = three steps ahead).  A/B knob (tools/gemm_knob_ab.py).
+inline Knob kn_wgrad_m32("wgrad_m32", 1);   // WGRAD on 32x32x16 MFMAs (igemm_kernel M32; profiles/r4_wgrad_m32_ab.txt)
 inline Knob kn_epi_depth("epi_depth", 4);   // measured: profiles/r2_epilogue_depth_ab.txt
 // the dual BN-reduce epilogue (EPI_BNR2) at depth 4 needs 256 VGPRs and spills; depth 2 fits and
 // is 0-6 % faster (profiles/r2_bnr2_ab.txt)
@@ -541,7 +542,11 @@ __device__ __forceinline__ void igemm_epilogue_fd(const IgemmParams& p, f32x4 (&
 // FOLD (bitmask): 1 = the A operand is formed while staging -- DGRAD / WGRAD: dz of the BatchNorm-
 // backward fold (fold_x, fold_coef); FWD: relu(a*z + b) of the BatchNorm-forward fold (act_sc/sh);
 // 2 = WGRAD's B operand (x) is relu(a*z + b) (act_sc / act_sh)
-template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT, int FOLD = 0>
+// M32 (WGRAD only): the MFMAs are v_mfma_f32_32x32x16_bf16 on 32x32 sub-tiles of the wave tile
+// (fragments from the same k-major LDS image through ds_read_b64_tr_b16, one 16-lane group per
+// (16-column half, 8-deep k half)): half the MFMA instructions, same LDS bytes (knob wgrad_m32)
+template <int MODE, int BM, int BN, int WM, int WN, bool UNIF, int EPI, int EPD = 2, int NTHR = NT, int FOLD = 0,
+          bool M32_ = false>
 __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const IgemmParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;   // 16x16 MFMA tiles per wave
@@ -587,6 +592,16 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   for (int i = 0; i < AT0; ++i)
 #pragma unroll
     for (int j = 0; j < AT1; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr bool M32 = M32_ && MODE == MODE_WGRAD;
+  static_assert(!M32 || (WTM % 32 == 0 && WTN % 32 == 0), "M32: 32-multiple wave tiles");
+  constexpr int TM32 = M32 ? WTM / 32 : 1, TN32 = M32 ? WTN / 32 : 1;
+  f32x16 acc32[TM32][TN32];
+#pragma unroll
+  for (int i = 0; i < TM32; ++i)
+#pragma unroll
+    for (int j = 0; j < TN32; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc32[i][j][r] = 0.f;
 
   uint4 ra[NVA], rb[NVB];
 
@@ -902,6 +917,36 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
   auto compute_stage = [&](int buf) {
     const char* sA = smem + buf * STAGE;
     const char* sB = sA + A_BYTES;
+    if constexpr (M32) {
+      // lane group g = lane >> 4 reads columns 16 * (g & 1) .. +15 of a 32-column slice at k rows
+      // 8 * (g >> 1) .. +7 of the 16-deep step: lane l ends with column (l & 31), k 8 * (l >> 5) .. +7
+      const int g = lane >> 4, q = (lane >> 2) & 3, pc = (lane & 3) * 4;
+#pragma unroll
+      for (int kq = 0; kq < BK / 16; ++kq) {
+        const int rowb = kq * 16 + 8 * (g >> 1) + q;
+        bf16x8 fa[TM32], fb[TN32];
+#pragma unroll
+        for (int i = 0; i < TM32; ++i) {
+          const int col = wr * WTM + i * 32 + 16 * (g & 1) + pc;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
+          fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int j = 0; j < TN32; ++j) {
+          const int col = wc * WTN + j * 32 + 16 * (g & 1) + pc;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
+          fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int i = 0; i < TM32; ++i)
+#pragma unroll
+          for (int j = 0; j < TN32; ++j)
+            acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc32[i][j], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8 fa[TM], fb[TN];
@@ -964,7 +1009,27 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
 
   // ---- epilogue -------------------------------------------------------------------------------
   const int fr = lane & 15, fq = lane >> 4;
-  if constexpr (MODE == MODE_WGRAD) {
+  if constexpr (M32) {
+    // 32x32 accumulator: column (lane & 31), register r -> row 8 * (r / 4) + 4 * (lane >> 5) + r % 4
+    float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
+#pragma unroll
+    for (int i = 0; i < TM32; ++i)
+#pragma unroll
+      for (int j = 0; j < TN32; ++j) {
+        const int col = n0 + wc * WTN + j * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wr * WTM + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+          if (row < p.gm && col < p.gn) {
+            float v = acc32[i][j][r] * p.alpha;
+            float* dst = out + (size_t)row * p.gn + col;
+            if (p.accumulate) v += *dst;
+            *dst = v;
+          }
+        }
+      }
+    return;
+  } else if constexpr (MODE == MODE_WGRAD) {
     float* out = reinterpret_cast<float*>(p.out) + (size_t)split * p.gm * p.gn;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -2076,7 +2141,21 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
       if (unif) PCMP_IGEMM_LAUNCH(true, EPI_PLAIN); else PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
     }
   } else {
-    PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
+    bool m32 = false;
+    if constexpr ((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0) {
+      if (kn_wgrad_m32.get()) {
+        auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, false, EPI_PLAIN, 2, NT, 0, true>;
+        static bool attr_ = false;
+        if (!attr_) {
+          PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf_),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+          attr_ = true;
+        }
+        hipLaunchKernelGGL(kf_, dim3(grid), dim3(NT), smem, st, p);
+        m32 = true;
+      }
+    }
+    if (!m32) PCMP_IGEMM_LAUNCH(false, EPI_PLAIN);
   }
 #undef PCMP_IGEMM_LAUNCH
   PCMP_LAUNCH_CHECK();
@@ -2477,7 +2556,21 @@ static void launch_fold_cfg(IgemmParams& p, hipStream_t st) {
   } else if constexpr (MODE == MODE_FWD) {
     if (p.stats) PCMP_FOLD_LAUNCH(true, EPI_STATS, 2); else PCMP_FOLD_LAUNCH(true, EPI_PLAIN, 2);
   } else {
-    PCMP_FOLD_LAUNCH(false, EPI_PLAIN, 2);
+    bool m32 = false;
+    if constexpr ((BM / WM) % 32 == 0 && (BN / WN) % 32 == 0) {
+      if (kn_wgrad_m32.get()) {
+        auto kf_ = &igemm_kernel<MODE, BM, BN, WM, WN, false, EPI_PLAIN, 2, NT, FOLD, true>;
+        static bool attr_ = false;
+        if (!attr_) {
+          PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf_),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+          attr_ = true;
+        }
+        hipLaunchKernelGGL(kf_, dim3(grid), dim3(NT), smem, st, p);
+        m32 = true;
+      }
+    }
+    if (!m32) PCMP_FOLD_LAUNCH(false, EPI_PLAIN, 2);
   }
 #undef PCMP_FOLD_LAUNCH
   PCMP_LAUNCH_CHECK();
