@@ -47,9 +47,14 @@ static void wgrad_run(IgemmParams p, int nsplit, float* out, bool accumulate, co
 // grid targets on a scratch output and caches the fastest.  Never while a graph is being captured.
 // PCMP_AUTOTUNE=0 (or an explicit PCMP_WGRAD_WGS) keeps the static 1024-workgroup target, which
 // also keeps runs bitwise reproducible (a tuned split count changes the summation order).
+static Knob kn_wgrad_cap_few("wgrad_cap_few", 1024);
 static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions& fopts, hipStream_t st) {
   const int ksteps = ceil_div(p.gk, BK);
-  auto nsplit_for = [&](int target) { return std::max(1, std::min(std::min(ceil_div(target, tiles), ksteps / 8), 256)); };
+  // split cap: 256, or wgrad_cap_few for GEMMs of <= 4 output tiles (the stem WGRAD: one 64x256 tile
+  // over 3.2 M reduction rows, alone on the chip at the end of backward -- 256 splits are one 4-wave
+  // workgroup per CU)
+  const int cap = tiles <= 4 ? std::max(256, kn_wgrad_cap_few.get()) : 256;
+  auto nsplit_for = [&](int target) { return std::max(1, std::min(std::min(ceil_div(target, tiles), ksteps / 8), cap)); };
   static const int fixed_target = [] {
     const char* e = std::getenv("PCMP_WGRAD_WGS");
     return e ? std::max(64, std::atoi(e)) : 0;
@@ -69,7 +74,7 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   auto& cache = g_wsplit_cache;
   char key[160];
   snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
-           0);
+           cap);
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
@@ -78,7 +83,7 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return dflt;
   std::vector<int> cands;
-  for (int t : {64, 128, 256, 512, 768, 1024, 1536, 2048}) {
+  for (int t : {64, 128, 256, 512, 768, 1024, 1536, 2048, 3072, 4096}) {
     const int ns = nsplit_for(t);
     if (std::find(cands.begin(), cands.end(), ns) == cands.end()) cands.push_back(ns);
   }
