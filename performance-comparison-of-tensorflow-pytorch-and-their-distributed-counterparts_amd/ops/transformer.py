@@ -194,6 +194,35 @@ def _wgrad_bias(p, bias, dy, x):
     return gw, gb
 
 
+class _SideBatch:
+    """The weight / bias gradients of one sublayer backward, issued to the WGRAD side stream as ONE
+    ``run_on_side`` fork (the host cost of a fork is on the eager step's critical path:
+    profiles/r4_bert_host_prof.txt); without flat sinks / side stream each runs inline at once."""
+
+    def __init__(self):
+        self.jobs, self.keep = [], []
+
+    def add(self, p, bias, dy, x):
+        if _side_ok(p, dy) and (bias is None or _side_ok(bias, dy)):
+            self.jobs.append((p, bias, dy, x))
+            self.keep += [dy, x]
+            return None, None
+        return _wgrad_bias(p, bias, dy, x)
+
+    def flush(self):
+        if not self.jobs:
+            return
+        jobs = self.jobs
+
+        def run():
+            for p, bias, dy, x in jobs:
+                _wgrad(p, dy, x)
+                if bias is not None:
+                    emit_grad(bias, lambda o, acc, dy=dy: K.colsum(dy, o, acc))
+        _params.run_on_side(run, tuple(self.keep))
+        self.jobs, self.keep = [], []
+
+
 def _ln_fwd(ctx, a, resid, gamma, beta, eps, p):
     seed, off = dropout_rng.next(a.numel()) if p > 0 else (0, 0)
     salt = dropout_rng.salt if p > 0 else None
@@ -243,10 +272,12 @@ class BertAttentionBlockFn(torch.autograd.Function):
         if dy.dtype != dt:
             dy = dy.to(dt)
         dres, da, (gg, gb, gbo) = _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, bo)
-        gwo, _ = _wgrad_bias(wo, None, da, out)
+        side = _SideBatch()
+        gwo, _ = side.add(wo, None, da, out)
         dctx = _dgrad(da, compute_weight(wo, dt), compute_weight_t(wo, dt))
         dqkv = K.attention_bwd(dctx, qkv, out, lse, ids if has_ids else None, B, S, H, p, seed, off, salt)
-        gwq, gbq = _wgrad_bias(wqkv, bqkv, dqkv, h)
+        gwq, gbq = side.add(wqkv, bqkv, dqkv, h)
+        side.flush()
         dh = _dgrad(dqkv, compute_weight(wqkv, dt), compute_weight_t(wqkv, dt), dres) if ctx.needs_input_grad[0] else None
         return dh, None, gwq, gbq, gwo, gbo, gg, gb, None, None, None, None, None, None
 
@@ -273,8 +304,10 @@ class BertFFNBlockFn(torch.autograd.Function):
         if dy.dtype != dt:
             dy = dy.to(dt)
         dres, df, (gg, gb, gb2) = _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, b2)
-        gw2, _ = _wgrad_bias(w2, None, df, g)
+        side = _SideBatch()
+        gw2, _ = side.add(w2, None, df, g)
         du = K.linear_dgrad_gelu(df, compute_weight(w2, dt), u, compute_weight_t(w2, dt))
-        gw1, gb1 = _wgrad_bias(w1, b1, du, h1)
+        gw1, gb1 = side.add(w1, b1, du, h1)
+        side.flush()
         dh1 = _dgrad(du, compute_weight(w1, dt), compute_weight_t(w1, dt), dres) if ctx.needs_input_grad[0] else None
         return dh1, gw1, gb1, gw2, gb2, gg, gb, None, None
