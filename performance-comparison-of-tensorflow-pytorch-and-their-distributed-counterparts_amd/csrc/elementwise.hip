@@ -289,6 +289,97 @@ __global__ void __launch_bounds__(256) maxpool_bwd_bnr_kernel(const __bf16* __re
   }
 }
 
+// Stem backward fused, 2x2-quad form (even H, W; 3x3 / stride-2 / pad-1 window): a thread owns the
+// input pixels (2a + dh, 2b + dw) of one quad x 8 channels.  The four pixels share the pooled
+// windows (a, b), (a, b+1), (a+1, b), (a+1, b+1), so those are loaded once per quad (4 dy + 4 argmax
+// loads for 4 pixels instead of 4 per pixel); each pixel folds its windows in the per-pixel kernel's
+// order, so g is bitwise that kernel's; the partial sums come in another order (knob pool_quad).
+__global__ void __launch_bounds__(256) maxpool_bwd_bnr_quad_kernel(
+    const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx, const __bf16* __restrict__ cx,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ sc,
+    const float* __restrict__ sh, __bf16* __restrict__ g_out, float* __restrict__ part, int N, int H, int W, int C,
+    int P, int Q, int quads_per_block) {
+  extern __shared__ float red[];   // [rpp][2][C]
+  const int CV = C / 8;
+  const int tpr = CV, rpp = 256 / CV;
+  const int tid = threadIdx.x;
+  const int tr = tid / tpr, cv = tid % tpr;
+  const int H2 = H >> 1, W2 = W >> 1;
+  const int MQ = N * H2 * W2;
+  const int r0 = blockIdx.x * quads_per_block, r1 = min(MQ, r0 + quads_per_block);
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], is[8], a[8], b[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[cv * 8 + e]; is[e] = invstd[cv * 8 + e];
+    a[e] = sc[cv * 8 + e]; b[e] = sh[cv * 8 + e];
+  }
+  if (tr < rpp) {
+    for (int qd = r0 + tr; qd < r1; qd += rpp) {
+      const int qb = (unsigned)qd % (unsigned)W2;
+      const int t = (unsigned)qd / (unsigned)W2;
+      const int qa = (unsigned)t % (unsigned)H2;
+      const int n = (unsigned)t / (unsigned)H2;
+      const int pa1 = min(P - 1, qa + 1), qb1 = min(Q - 1, qb + 1);
+      const int pp[4] = {qa, qa, pa1, pa1}, qq[4] = {qb, qb1, qb, qb1};
+      uint64_t pk[4];
+      u16x8 gv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const unsigned o = (((unsigned)n * P + pp[j]) * Q + qq[j]) * (unsigned)C + cv * 8;
+        pk[j] = *reinterpret_cast<const uint64_t*>(idx + o);
+        gv[j] = *reinterpret_cast<const u16x8*>(dy + o);
+      }
+      float xv[4][8];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int h = 2 * qa + (d >> 1), w = 2 * qb + (d & 1);
+        ld8(cx + ((size_t)((unsigned)n * H + h) * W + w) * C + cv * 8, xv[d]);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int dh = d >> 1, dw = d & 1;
+        const int h = 2 * qa + dh, w = 2 * qb + dw;
+        // this pixel's windows, in the per-pixel kernel's (p0, q0), (p0, q1), (p1, q0), (p1, q1) order:
+        // p1 = min(P-1, (h+1)/2) is qa+1 only for odd h, q1 likewise
+        const int p1 = dh ? pa1 : qa, q1 = dw ? qb1 : qb;
+        const bool use[4] = {true, q1 != qb, p1 != qa, p1 != qa && q1 != qb};
+        const int jj[4] = {0, dw ? 1 : 0, dh ? 2 : 0, (dh && dw) ? 3 : 0};
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!use[k]) continue;
+          const int j = jj[k];
+          const int pos = (h - (2 * pp[j] - 1)) * 3 + (w - (2 * qq[j] - 1));
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((int)((pk[j] >> (8 * e)) & 0xff) == pos) acc[e] += bf2f(gv[j][e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gr = bf2f(f2bf(acc[e]));
+          acc[e] = (xv[d][e] * a[e] + b[e] > 0.f) ? gr : 0.f;
+          sg[e] += acc[e];
+          sgx[e] += acc[e] * (xv[d][e] - mu[e]) * is[e];
+        }
+        st8(g_out + ((size_t)((unsigned)n * H + h) * W + w) * C + cv * 8, acc);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(tr * 2 + 0) * C + cv * 8 + e] = sg[e];
+      red[(tr * 2 + 1) * C + cv * 8 + e] = sgx[e];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * C; i += blockDim.x) {
+    const int which = i / C, c = i % C;
+    float t = 0.f;
+    for (int r = 0; r < rpp; ++r) t += red[(r * 2 + which) * C + c];
+    part[(size_t)blockIdx.x * 2 * C + i] = t;
+  }
+}
+
 // ---------------------------------------------------------------- global average pool ----------
 // x [N, HW, C] -> y [N, C]  (one block per (n, 64*8-channel slab))
 __global__ void gap_fwd_kernel(const __bf16* __restrict__ x, __bf16* __restrict__ y, int HW, int C) {
@@ -738,6 +829,7 @@ __global__ void image_to_s2d_kernel(const T* __restrict__ x, __bf16* __restrict_
 // specialised 3x3 / stride-2 / pad-1 pooling kernels (32-bit indexing); knob pool3s2=0 -> generic
 static Knob kn_pool3s2("pool3s2", 1);
 
+static Knob kn_pool_quad("pool_quad", 1);   // stem pooling backward over 2x2 input quads
 static bool pool3s2_ok(const at::Tensor& x, int64_t k, int64_t s, int64_t pad) {
   return kn_pool3s2.get() && k == 3 && s == 2 && pad == 1 && x.numel() < (int64_t)INT_MAX;
 }
@@ -801,10 +893,23 @@ std::vector<at::Tensor> maxpool_bwd_bnr(const at::Tensor& dy, const at::Tensor& 
     TORCH_CHECK(t->numel() == C, "maxpool_bwd_bnr: per-channel vectors");
   }
   const int M = N * H * W, rpp = 256 / (C / 8);
+  auto g = at::empty_like(cx);
+  if (kn_pool_quad.get() && pool3s2_ok(cx, k, s, pad) && H % 2 == 0 && W % 2 == 0 && P == H / 2 && Q == W / 2) {
+    const int MQ = M / 4;
+    int qpb = std::max(rpp, ceil_div(MQ, 2048));
+    qpb = ceil_div(qpb, rpp) * rpp;
+    const int T = ceil_div(MQ, qpb);
+    auto part = at::empty({T, 2, C}, cx.options().dtype(at::kFloat));
+    hipLaunchKernelGGL(maxpool_bwd_bnr_quad_kernel, dim3(T), dim3(256), (size_t)rpp * 2 * C * sizeof(float),
+                       cur_stream(), ptr<__bf16>(dy), ptr<uint8_t>(idx), ptr<__bf16>(cx), ptr<float>(mean),
+                       ptr<float>(invstd), ptr<float>(scale), ptr<float>(shift), ptr<__bf16>(g), ptr<float>(part), N,
+                       H, W, C, P, Q, qpb);
+    PCMP_LAUNCH_CHECK();
+    return {g, part};
+  }
   int rpb = std::max(rpp, ceil_div(M, 2048));
   rpb = ceil_div(rpb, rpp) * rpp;
   const int T = ceil_div(M, rpb);
-  auto g = at::empty_like(cx);
   auto part = at::empty({T, 2, C}, cx.options().dtype(at::kFloat));
   auto kfn = pool3s2_ok(cx, k, s, pad) && P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1 ? &maxpool_bwd_bnr_kernel<true>
                                                                                      : &maxpool_bwd_bnr_kernel<false>;

@@ -488,6 +488,7 @@ def test_pool3s2_specialised(gpu, H, W):
     sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.3
     mean, invstd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
     res = {}
+    prev_quad = ops.set_knob("pool_quad", 0)   # the 2x2-quad backward sums its partials in another order
     try:
         for v in (0, 1):
             ops.set_knob("pool3s2", v)
@@ -497,10 +498,17 @@ def test_pool3s2_specialised(gpu, H, W):
             dy = torch.randn(yb.shape, device=gpu, generator=dy).to(torch.bfloat16)
             g, part = ops.maxpool_bwd_bnr(dy, ib, c, mean, invstd, sc, sh, 3, 2, 1)
             res[v] = (y, i, yb, ib, g, part)
+        ops.set_knob("pool_quad", 1)
+        gq, partq = ops.maxpool_bwd_bnr(dy, ib, c, mean, invstd, sc, sh, 3, 2, 1)
     finally:
         ops.set_knob("pool3s2", 1)
+        ops.set_knob("pool_quad", prev_quad)
     for a, b in zip(res[0], res[1]):
         assert torch.equal(a, b) or (a.is_floating_point() and torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0)))
+    # the quad kernel (even H, W): g bitwise; the per-channel sums equal up to fp32 summation order
+    g1, part1 = res[1][4], res[1][5]
+    assert torch.equal(gq.nan_to_num(7.0), g1.nan_to_num(7.0))
+    close(partq.sum(0).nan_to_num(0.0), part1.sum(0).nan_to_num(0.0), rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("src", ["f32", "u8", "nhwc"])
