@@ -177,6 +177,10 @@ def build_hip(args, env):
         opt.zero_grad()
         logits = model.forward_logits(x)
         loss = cross_entropy(logits, y)
+        if ddp is None:
+            # PCMP_TAIL_STEP=1: SGD of every layer but the stem starts on the side stream while the
+            # stem's WGRAD (the step's last GEMM) runs (measured slower, off by default)
+            opt.prepare_step()
         loss.backward()
         if ddp is not None:
             ddp.finish_gradient_sync()

@@ -66,6 +66,11 @@ class TrainState:
         self.opt.zero_grad()
 
     def backward_step(self, loss):
+        if self.ddp is None and self.clip is None and self.timer is None:
+            # no gradient multiplier and no per-phase timing: the optimizer may start on the side
+            # stream before backward ends (SGD's tail step, pcmp.optim.SGD.prepare_step)
+            self.opt.set_grad_scale(None)
+            self.opt.prepare_step()
         with self.phase("backward"):
             loss.backward()
         if self.ddp is not None:
