@@ -22,6 +22,12 @@ def _port():
     return p
 
 
+def _why(r):
+    """The first error lines of a failed child (a c10d watchdog abort ends in a long frame dump)."""
+    lines = [ln for ln in r.stderr.splitlines() if ("rror" in ln or "WARN" in ln) and "frame #" not in ln]
+    return "\n".join(lines[:12]) + "\n...\n" + r.stderr[-1500:]
+
+
 def _env():
     return dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1",
                 LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
@@ -33,7 +39,7 @@ def test_forced_rccl_ddp_matches_local(gpu, grad_dtype):
             f"print('RESULT', json.dumps(rccl_force_check('resnet18', '{grad_dtype}')))")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=ROOT,
                        env=_env())
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
     res = json.loads(line[len("RESULT "):])
     assert res["backend"] == "nccl"
@@ -48,7 +54,7 @@ def test_bench_ddp_force_rccl(gpu):
            "--gpus", "1", "--steps", "3", "--warmup", "2", "--batch-size", "32", "--ddp-force",
            "--grad-dtype", "bf16", "--infer-images", "20"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=_env())
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     rec = json.loads(lines[0])
