@@ -217,14 +217,17 @@ def test_bn_fused_finalize_bitwise(gpu, T, C):
     mean, invstd = torch.randn(C, device=gpu, generator=g), torch.rand(C, device=gpu, generator=g) + 0.5
     count = T * 16
     outs = {}
-    for v in (0, 1, 1, 1):
-        ops.set_knob("bn_fused_fin", v)
-        rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
-        fwd = ops.bn_finalize(part, count, gam, bet, rm, rv, 0.1, 1e-5)
-        dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), 0.25, device=gpu)
-        coef = ops.bn_bwd_finalize(part, count, gam, mean, invstd, dg, db, True)
-        outs.setdefault(v, []).append([t.clone() for t in (*fwd, rm, rv, dg, db, coef)])
-    ops.set_knob("bn_fused_fin", 1)
+    prev = ops.set_knob("bn_fused_fin", 0)
+    try:
+        for v in (0, 1, 1, 1):
+            ops.set_knob("bn_fused_fin", v)
+            rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+            fwd = ops.bn_finalize(part, count, gam, bet, rm, rv, 0.1, 1e-5)
+            dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), 0.25, device=gpu)
+            coef = ops.bn_bwd_finalize(part, count, gam, mean, invstd, dg, db, True)
+            outs.setdefault(v, []).append([t.clone() for t in (*fwd, rm, rv, dg, db, coef)])
+    finally:
+        ops.set_knob("bn_fused_fin", prev)
     base = outs[0][0]
     for rep in outs[1]:
         for a, b in zip(base, rep):
