@@ -127,7 +127,8 @@ def graph_step(step, x, y):
             step(x, y)
     main.wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # thread-local capture: the RCCL watchdog thread's event queries must not break it
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         loss = step(x, y)
 
     def replay(x_, y_):

@@ -59,7 +59,7 @@ class GraphedStep:
             prev = dropout_rng.salt
             dropout_rng.salt = self.salt
             try:
-                with torch.cuda.graph(self.graph):
+                with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):   # see inference.py
                     self.loss = self._body()
                     self.salt.add_(1)
             finally:

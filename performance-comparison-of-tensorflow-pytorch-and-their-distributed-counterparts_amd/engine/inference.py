@@ -56,7 +56,9 @@ class Batch1Predictor:
                 if os.environ.get("PCMP_B1_HOST_OUT", "1") == "1":
                     self.host_out = torch.empty(1, dtype=torch.int64, pin_memory=True)
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph):
+                # thread-local capture: a process-group watchdog thread querying its events while this
+                # thread captures must not invalidate the capture (global mode aborts the process)
+                with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                     self.static_out = argmax_rows(_logits(model, self.static_in))
                     if self.host_out is not None:
                         self.host_out.copy_(self.static_out.view(-1)[:1], non_blocking=True)
