@@ -178,10 +178,6 @@ def build_hip(args, env):
         opt.zero_grad()
         logits = model.forward_logits(x)
         loss = cross_entropy(logits, y)
-        if ddp is None:
-            # PCMP_TAIL_STEP=1: SGD of every layer but the stem starts on the side stream while the
-            # stem's WGRAD (the step's last GEMM) runs (measured slower, off by default)
-            opt.prepare_step()
         loss.backward()
         if ddp is not None:
             ddp.finish_gradient_sync()
@@ -293,12 +289,12 @@ def main():
         if opt is not None:
             opt.set_lr(args.lr * (i + 1) / ramp)
         loss = step(x, y)
-        if i == 0 and env.world_size > 1:
-            # every shape is planned by now: all ranks take rank 0's autotuned kernels
-            from pcmp.parallel.ddp import sync_autotune
-            sync_autotune()
         if wd is not None:
             wd.kick(i, "warmup")
+    if env.world_size > 1:
+        # every shape is planned by now: all ranks take rank 0's autotuned kernels
+        from pcmp.parallel.ddp import sync_autotune
+        sync_autotune()
     if opt is not None:
         opt.set_lr(args.lr)
     if ddp is not None:

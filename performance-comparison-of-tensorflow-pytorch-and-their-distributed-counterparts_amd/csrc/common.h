@@ -109,19 +109,25 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 }
 
 // Counter-based hash RNG (stateless): used for dropout so backward regenerates the mask
-// from (seed, offset, index) instead of storing it.  32-bit mixing ("lowbias32" finaliser) of the
-// index folded with the 64-bit seed: two 32-bit multiplies per element where the splitmix64 form
-// needed three 64-bit ones (~40 VALU ops; 30 % of the attention kernels' time at p = 0.1,
-// profiles/r4_attn_micro.txt).  ops/ref.py hash_uniform is the bit-exact torch port.
-__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-  uint32_t x = (uint32_t)idx ^ ((uint32_t)(idx >> 32) * 0x85EBCA6Bu) ^ (uint32_t)seed ^
-               ((uint32_t)(seed >> 32) * 0x9E3779B9u);
+// from (seed, offset, index) instead of storing it.  32-bit "lowbias32" finaliser rounds: the high
+// index word (eager dropout's per-call counter, offset = counter << 32) is mixed with the folded
+// 64-bit seed by one round, and that per-call key is XORed into the low word before a second round.
+// (Round 4 folded both words into ONE round: every call's mask was then an XOR relabelling of the
+// same bijective sequence, and two calls whose keys differed by less than numel drew index
+// permutations of one mask; tests/test_transformer_gpu.py checks consecutive calls are uncorrelated.)
+// Two 32-bit multiplies per round where splitmix64 needed three 64-bit ones (~40 VALU ops).
+// ops/ref.py hash_uniform is the bit-exact torch port.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
   x *= 0x846CA68Bu;
   x ^= x >> 16;
   return x;
+}
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  const uint32_t key = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x9E3779B9u);
+  return lowbias32((uint32_t)idx ^ lowbias32((uint32_t)(idx >> 32) ^ key));
 }
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx) {
   return (hash_u32(seed, idx) >> 8) * (1.0f / 16777216.0f);
@@ -152,6 +158,16 @@ inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
   do {                                                                                        \
     const hipError_t e_ = (expr);                                                             \
     TORCH_CHECK(e_ == hipSuccess, #expr " failed: ", hipGetErrorString(e_));                  \
+  } while (0)
+// Launches whose dynamic LDS may exceed 64 KB need the per-kernel opt-in (once per call site).
+#define PCMP_ALLOW_BIG_LDS(kfn)                                                                             \
+  do {                                                                                                    \
+    static const bool pcmp_lds_ = [] {                                                                    \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&kfn),                             \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));        \
+      return true;                                                                                        \
+    }();                                                                                                  \
+    (void)pcmp_lds_;                                                                                      \
   } while (0)
 
 template <typename T>

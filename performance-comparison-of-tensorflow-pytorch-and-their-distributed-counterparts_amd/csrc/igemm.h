@@ -1475,6 +1475,451 @@ __global__ void __launch_bounds__(big_waves<BN>() * 64, 1) igemm_big_kernel(cons
 }
 
 // ------------------------------------------------------------------------------------------------
+// Round-5 critical-path FWD / DGRAD kernel: igemm_dma_kernel's operand staging (LDS-DMA, swizzled
+// 128-B rows, block-uniform tap walk) with the one-barrier-per-K-tile main loop of tools/gemm_lab v4
+// on v_mfma_f32_32x32x16_bf16 (the loop gemm32_kernel runs for plain GEMMs): two LDS stages, the
+// fragments of each 64-deep K-tile double-buffered over its two 32-deep halves,
+//   half 0: ds_read frags(t, 1)  || MFMA frags(t, 0)
+//           vmcnt(0) [stage t+1 landed] + lgkmcnt(0) + s_barrier [every wave done with stage t]
+//   half 1: DMA stage t+2 into stage t's buffer, ds_read frags(t+1, 0)  || MFMA frags(t, 1)
+// instead of igemm_dma_kernel's four per-quadrant barriers per K-tile on 16x16x32 (half the MFMA
+// instructions for the same wave tile and ds_read bytes; lab: 128x128 4-wave +5-12 %,
+// profiles/r4_gemm_lab_mfma32.txt).  4 waves, 2 blocks per CU (the WGRAD side stream keeps its CUs).
+//
+// Accumulator layout (MFMA runs B x A): lane l holds output pixel (l & 31) of each 32x32 tile and,
+// through the B-row channel permutation chan_perm32, the 16 CONSECUTIVE channels 16 * (l >> 5) + r in
+// register r -- two 16-B stores per (pixel, 32-channel block), no lane shuffles.  The epilogue
+// (igemm_epilogue32) has every igemm_epilogue_fd feature the conv paths use (bias, residual incl. the
+// sub-sampled one, ReLU, stride-2 sub-pixel output rows, BatchNorm partial statistics, the fused
+// BatchNorm-backward reduction with tensor / bit / recomputed ReLU masks, the dual-BN form); its
+// column sums are reduced in registers (a 4-step DPP transpose-reduction over the 16 lanes of a DPP
+// row + one ds_swizzle across the row pair, per 32-channel block) instead of an LDS transpose, and
+// the per-channel coefficient tables are staged in their own LDS region during the prologue.
+__device__ __forceinline__ int chan_perm32(int rho) {   // LDS B row -> channel offset within the tile
+  return (rho & ~31) | (((rho >> 2) & 1) << 4) | (((rho >> 3) & 3) << 2) | (rho & 3);
+}
+
+// v[0..15] of every lane -> the sum over the 16 lanes of the lane's DPP row of v[lane & 15]
+// (butterfly over row_mirror, row_half_mirror, quad xor-2, quad xor-1: each step a lane keeps half of
+// its values and adds the partner's copy of that half; 45 VALU for 16 values instead of 64)
+__device__ __forceinline__ float row16_transpose_sum(const float (&v)[16], int lane) {
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+  float w[8], x[4], y[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = (b3 ? v[k + 8] : v[k]) + dpp_mov<0x140>(b3 ? v[k] : v[k + 8]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = (b2 ? w[k + 4] : w[k]) + dpp_mov<0x141>(b2 ? w[k] : w[k + 4]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) y[k] = (b1 ? x[k + 2] : x[k]) + dpp_mov<0x4E>(b1 ? x[k] : x[k + 2]);
+  return (b0 ? y[1] : y[0]) + dpp_mov<0xB1>(b0 ? y[0] : y[1]);
+}
+
+// ctab: [6][BN] coefficient rows (BN-backward: istd, -mean*istd, mask scale, mask shift, istd2,
+// -mean2*istd2; otherwise row 0 = bias), filled in the prologue; red: [WM][NS][BN] scratch
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int EPD>
+__device__ __forceinline__ void igemm_epilogue32(const IgemmParams& p, f32x16 (&acc)[BN / WN / 32][BM / WM / 32],
+                                                 const float* ctab, float* red, int tid, int m0, int n0, int tile_m) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int NTH = 256;
+  constexpr int NI = TN * TM * 2;                 // 16-B store items per lane
+  constexpr int IPJ = TM * 2;                     // items per 32-channel block
+  constexpr bool stats = EPI == EPI_STATS;
+  constexpr bool bnr = MODE == MODE_DGRAD && (EPI == EPI_BNR || EPI == EPI_BNR2);
+  constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
+  constexpr int NS = bnr2 ? 3 : 2;
+  static_assert(EPI != EPI_GELU, "igemm_epilogue32: conv epilogues only");
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int h = lane >> 5, pr = lane & 31;
+  __bf16* out = reinterpret_cast<__bf16*>(p.out);
+  const bool has_res = p.resid != nullptr;
+  const bool has_mb = bnr && p.bn_mbits != nullptr;
+  const bool has_mk = bnr && !has_mb && p.bn_mask != nullptr;
+  const bool mfx = bnr && !has_mb && !has_mk && p.bn_msc != nullptr;
+  const bool has_bias = MODE == MODE_FWD && p.bias != nullptr;
+  size_t orows[TM];
+  int rrows[MODE == MODE_DGRAD ? TM : 1];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wr * WTM + i * 32 + pr;
+    size_t orow = m < p.gm ? m : 0;
+    if constexpr (MODE == MODE_DGRAD) {
+      rrows[i] = (int)orow;
+      if ((p.sub || p.resid_sub) && m < p.gm) {
+        const int n = fdiv(m, p.fd_HW);
+        const int rem = m - n * p.dH * p.dW;
+        const int hh = fdiv(rem, p.fd_W);
+        const int ww = rem - hh * p.dW;
+        if (p.sub) orow = ((size_t)n * p.H + 2 * hh + p.oph) * p.W + 2 * ww + p.opw;
+        else rrows[i] = ((hh | ww) & 1) ? -1 : (n * p.rs_H2 + (hh >> 1)) * p.rs_W2 + (ww >> 1);
+      }
+    }
+    orows[i] = orow;
+  }
+  // item t: 32-channel block j = t / IPJ (outer: its column sums are reduced when it completes),
+  // pixel row group i, 8-channel half c2
+  auto item_j = [](int t) { return t / IPJ; };
+  auto item_i = [](int t) { return (t / 2) % TM; };
+  auto item_c = [](int t) { return t & 1; };
+  auto chan = [&](int t) { return wc * WTN + 32 * item_j(t) + 16 * h + 8 * item_c(t); };   // within the tile
+  constexpr int D = EPD;
+  uint4 rvA[D], mkA[D], xvA[D], xv2A[D];
+  unsigned mbA[D];
+  auto issue = [&](int t, int b) {
+    const int i = item_i(t);
+    const int m = m0 + wr * WTM + i * 32 + pr;
+    const int n = n0 + chan(t);
+    const bool ok = m < p.gm && n < p.gn;
+    const size_t o = orows[i] * p.gn + (ok ? n : 0);
+    auto ldv = [&](const __bf16* src) { return ok ? *reinterpret_cast<const uint4*>(src + o) : uint4{0, 0, 0, 0}; };
+    if (has_res) {
+      if constexpr (MODE == MODE_DGRAD) {
+        if (p.resid_sub) {
+          const bool okr = ok && rrows[i] >= 0;
+          const size_t ro = (size_t)(okr ? rrows[i] : 0) * p.gn + (ok ? n : 0);
+          rvA[b] = okr ? *reinterpret_cast<const uint4*>(p.resid + ro) : uint4{0, 0, 0, 0};
+        } else {
+          rvA[b] = ldv(p.resid);
+        }
+      } else {
+        rvA[b] = ldv(p.resid);
+      }
+    }
+    if constexpr (bnr) {
+      if (has_mb) mbA[b] = ok ? p.bn_mbits[o >> 3] : 0u;
+      if (has_mk) mkA[b] = ldv(p.bn_mask);
+      xvA[b] = ldv(p.bn_x);
+      if constexpr (bnr2) xv2A[b] = ldv(p.bn_x2);
+    }
+  };
+  if (has_res || bnr) {
+#pragma unroll
+    for (int d = 0; d < D - 1; ++d)
+      if (d < NI) issue(d, d);
+  }
+  float sm[NS][16];
+#pragma unroll
+  for (int t = 0; t < NI; ++t) {
+    const int b = t % D;
+    if ((has_res || bnr) && t + D - 1 < NI) issue(t + D - 1, (t + D - 1) % D);
+    const int j = item_j(t), i = item_i(t), c2 = item_c(t);
+    if (t % IPJ == 0) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sm[k][e] = 0.f;
+    }
+    const int m = m0 + wr * WTM + i * 32 + pr;
+    const int ct = chan(t);
+    const int n = n0 + ct;
+    if (m < p.gm && n < p.gn) {
+      const size_t o = orows[i] * p.gn + n;
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = acc[j][i][8 * c2 + e];
+      if (has_bias) {
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(ctab + ct), b1 = *reinterpret_cast<const f32x4*>(ctab + ct + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { x[e] += b0[e]; x[e + 4] += b1[e]; }
+      }
+      if (has_res) {
+        const unsigned rw[4] = {rvA[b].x, rvA[b].y, rvA[b].z, rvA[b].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x[2 * q] += __uint_as_float(rw[q] << 16);
+          x[2 * q + 1] += __uint_as_float(rw[q] & 0xffff0000u);
+        }
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = fmaxf(x[e], 0.f);
+      }
+      unsigned ov[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ov[q] = f2bf2(x[2 * q], x[2 * q + 1]);
+      if constexpr (bnr) {
+        const unsigned xw[4] = {xvA[b].x, xvA[b].y, xvA[b].z, xvA[b].w};
+        if (has_mb) {
+          const unsigned bits = mbA[b];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            ov[q] &= (((bits >> (2 * q)) & 1u) ? 0x0000ffffu : 0u) | (((bits >> (2 * q + 1)) & 1u) ? 0xffff0000u : 0u);
+        } else if (has_mk) {
+          const unsigned yw[4] = {mkA[b].x, mkA[b].y, mkA[b].z, mkA[b].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const unsigned y = yw[q];
+            ov[q] &= (((y & 0x8000u) == 0 && (y & 0x7fffu) != 0) ? 0x0000ffffu : 0u) |
+                     (((y & 0x80000000u) == 0 && (y & 0x7fff0000u) != 0) ? 0xffff0000u : 0u);
+          }
+        } else if (mfx) {
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(ctab + 2 * BN + ct), s1 = *reinterpret_cast<const f32x4*>(ctab + 2 * BN + ct + 4);
+          const f32x4 h0 = *reinterpret_cast<const f32x4*>(ctab + 3 * BN + ct), h1 = *reinterpret_cast<const f32x4*>(ctab + 3 * BN + ct + 4);
+          const float msc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+          const float msh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float z0 = fmaf(__uint_as_float(xw[q] << 16), msc[2 * q], msh[2 * q]);
+            const float z1 = fmaf(__uint_as_float(xw[q] & 0xffff0000u), msc[2 * q + 1], msh[2 * q + 1]);
+            ov[q] &= (z0 > 0.f ? 0x0000ffffu : 0u) | (z1 > 0.f ? 0xffff0000u : 0u);
+          }
+        }
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(ctab + ct), a1 = *reinterpret_cast<const f32x4*>(ctab + ct + 4);
+        const f32x4 k0 = *reinterpret_cast<const f32x4*>(ctab + BN + ct), k1 = *reinterpret_cast<const f32x4*>(ctab + BN + ct + 4);
+        const float ka[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const float kb[8] = {k0[0], k0[1], k0[2], k0[3], k1[0], k1[1], k1[2], k1[3]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float g0 = __uint_as_float(ov[q] << 16), g1 = __uint_as_float(ov[q] & 0xffff0000u);
+          const int e = 8 * c2 + 2 * q;
+          sm[0][e] += g0; sm[0][e + 1] += g1;
+          sm[1][e] += g0 * fmaf(__uint_as_float(xw[q] << 16), ka[2 * q], kb[2 * q]);
+          sm[1][e + 1] += g1 * fmaf(__uint_as_float(xw[q] & 0xffff0000u), ka[2 * q + 1], kb[2 * q + 1]);
+        }
+        if constexpr (bnr2) {
+          const unsigned xw2[4] = {xv2A[b].x, xv2A[b].y, xv2A[b].z, xv2A[b].w};
+          const f32x4 c0 = *reinterpret_cast<const f32x4*>(ctab + 4 * BN + ct), c1 = *reinterpret_cast<const f32x4*>(ctab + 4 * BN + ct + 4);
+          const f32x4 d0 = *reinterpret_cast<const f32x4*>(ctab + 5 * BN + ct), d1 = *reinterpret_cast<const f32x4*>(ctab + 5 * BN + ct + 4);
+          const float ka2[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+          const float kb2[8] = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float g0 = __uint_as_float(ov[q] << 16), g1 = __uint_as_float(ov[q] & 0xffff0000u);
+            const int e = 8 * c2 + 2 * q;
+            sm[2][e] += g0 * fmaf(__uint_as_float(xw2[q] << 16), ka2[2 * q], kb2[2 * q]);
+            sm[2][e + 1] += g1 * fmaf(__uint_as_float(xw2[q] & 0xffff0000u), ka2[2 * q + 1], kb2[2 * q + 1]);
+          }
+        }
+      } else if constexpr (stats) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float r0 = __uint_as_float(ov[q] << 16), r1 = __uint_as_float(ov[q] & 0xffff0000u);
+          const int e = 8 * c2 + 2 * q;
+          sm[0][e] += r0; sm[0][e + 1] += r1;
+          sm[1][e] += r0 * r0; sm[1][e + 1] += r1 * r1;
+        }
+      }
+      *reinterpret_cast<uint4*>(out + o) = uint4{ov[0], ov[1], ov[2], ov[3]};
+    }
+    if constexpr (stats || bnr) {
+      if (t % IPJ == IPJ - 1) {   // block j complete: reduce its column sums over the wave's 32 pixels
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          float s = row16_transpose_sum(sm[k], lane);
+          s += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(s), 0x401F));   // lane ^ 16
+          if (!(lane & 16)) red[(wr * NS + k) * BN + wc * WTN + 32 * j + 16 * h + (lane & 15)] = s;
+        }
+      }
+    }
+  }
+  if constexpr (stats || bnr) {
+    __syncthreads();
+    float* st = p.stats + (size_t)tile_m * 2 * p.gn;
+    float* st2 = bnr2 ? p.stats2 + (size_t)tile_m * 2 * p.gn : nullptr;
+    for (int c = tid; c < BN; c += NTH) {
+      if (n0 + c < p.gn) {
+        float t[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          t[k] = 0.f;
+#pragma unroll
+          for (int w = 0; w < WM; ++w) t[k] += red[(w * NS + k) * BN + c];
+        }
+        st[n0 + c] = t[0];
+        st[p.gn + n0 + c] = t[1];
+        if constexpr (bnr2) {
+          st2[n0 + c] = t[0];
+          st2[p.gn + n0 + c] = t[2];
+        }
+      }
+    }
+  }
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int EPD = 2>
+__global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p) {
+  constexpr int NW = 4, NTHR = 256;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;   // LDS-DMA instructions (8 rows each) per wave
+  constexpr bool bnr = MODE == MODE_DGRAD && (EPI == EPI_BNR || EPI == EPI_BNR2);
+  constexpr bool bnr2 = MODE == MODE_DGRAD && EPI == EPI_BNR2;
+  constexpr int NS = bnr2 ? 3 : 2;
+  static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
+  static_assert(WM * WN == NW && TM >= 1 && TN >= 1 && NA >= 1 && NB >= 1 && NA * 8 * NW == BM && NB * 8 * NW == BN,
+                "igemm_dma32 tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* ctab = reinterpret_cast<float*>(smem + 2 * STAGE);   // [6][BN]
+  float* red = ctab + 6 * BN;                                 // [WM][NS][BN]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = lin % p.tiles_n;
+  const int tile_m = lin / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int nk = p.gk / BK;
+
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
+  const int gch = (lane & 7) ^ (lane >> 3);
+  int a_off[NA], a_y[NA], a_x[NA];
+  int b_off[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + (wid * NA + i) * 8 + (lane >> 3);
+    const bool v = m < p.gm;
+    const int mm = v ? m : 0;
+    if constexpr (MODE == MODE_FWD) {
+      const int n = fdiv(mm, p.fd_PQ);
+      const int rem = mm - n * p.P * p.Q;
+      const int pp = fdiv(rem, p.fd_Q);
+      const int qq = rem - pp * p.Q;
+      const int yv = pp * p.stride - p.pad;
+      a_y[i] = v ? yv : -(1 << 28);
+      a_x[i] = qq * p.stride - p.pad;
+      a_off[i] = ((n * p.H + yv) * p.W + a_x[i]) * p.C + gch * 8;
+    } else {
+      const int n = fdiv(mm, p.fd_HW);
+      const int rem = mm - n * p.dH * p.dW;
+      const int hh = fdiv(rem, p.fd_W);
+      const int ww = rem - hh * p.dW;
+      const int yv = hh + p.offy;
+      a_y[i] = v ? yv : -(1 << 28);
+      a_x[i] = ww + p.offx;
+      a_off[i] = ((n * p.P + yv) * p.Q + a_x[i]) * p.K + gch * 8;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int n = n0 + chan_perm32((wid * NB + i) * 8 + (lane >> 3));
+    b_off[i] = n < p.gn ? n * p.gk + gch * 8 : -1;
+  }
+  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
+  int kc = 0, k0 = 0, ks = 0, kr = 0;
+  // DMA of the K-tile at (k0, kr, ks, kc) into stage s, then advance; !live: zero-fill (tail)
+  auto issue = [&](int s, bool live) {
+    int tap;
+    if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
+    else tap = -(kr * p.Q + ks) * p.K + kc;
+    char* dst = smem + s * STAGE;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      bool ok;
+      if constexpr (MODE == MODE_FWD)
+        ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
+      else
+        ok = (unsigned)(a_y[i] - kr) < (unsigned)p.P && (unsigned)(a_x[i] - ks) < (unsigned)p.Q;
+      const int voff = (ok && live) ? (a_off[i] + tap) * 2 : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(dst + (wid * NA + i) * 1024),
+                                               16, voff, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int voff = (b_off[i] >= 0 && live) ? (b_off[i] + k0) * 2 : (int)kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsB, (__attribute__((address_space(3))) void*)(dst + A_BYTES + (wid * NB + i) * 1024), 16, voff, 0, 0, 0);
+    }
+    k0 += BK;
+    kc += BK;
+    if (kc >= CIN) {
+      kc = 0;
+      if (++ks == p.S) { ks = 0; ++kr; }
+    }
+  };
+
+  // per-channel epilogue coefficients: loaded ahead of the first DMAs, written to LDS once the first
+  // stage has landed (the prologue barrier publishes them)
+  float cv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool ld_ct = tid < BN && (bnr || (MODE == MODE_FWD && p.bias != nullptr));
+  if (ld_ct) {
+    const int c = min(n0 + tid, p.gn - 1);
+    if constexpr (bnr) {
+      const float is = p.bn_istd[c];
+      cv[0] = is;
+      cv[1] = -p.bn_mean[c] * is;
+      if (!p.bn_mbits && !p.bn_mask && p.bn_msc) { cv[2] = p.bn_msc[c]; cv[3] = p.bn_msh[c]; }
+      if constexpr (bnr2) {
+        const float is2 = p.bn_istd2[c];
+        cv[4] = is2;
+        cv[5] = -p.bn_mean2[c] * is2;
+      }
+    } else {
+      cv[0] = p.bias[c];
+    }
+  }
+
+  f32x16 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][i][r] = 0.f;
+  bf16x8 fa0[2][TM], fb0[2][TN], fa1[2][TM], fb1[2][TN];
+  auto rd = [&](bf16x8(&fa)[2][TM], bf16x8(&fb)[2][TN], int half, int s) {
+    const char* sA = smem + s * STAGE;
+    const char* sB = sA + A_BYTES;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int ch = half * 4 + q * 2 + (lane >> 5);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[q][i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[q][j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 32 + (lane & 31), ch));
+    }
+  };
+  auto mma = [&](bf16x8(&fa)[2][TM], bf16x8(&fb)[2][TN]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[q][j], fa[q][i], acc[j][i], 0, 0, 0);
+  };
+  constexpr int NMF = 2 * TM * TN, NDS = 2 * (TM + TN), NVM = NA + NB;
+  constexpr int DPM = NDS / NMF > 0 ? NDS / NMF : 1, MPD = NMF >= NDS ? NMF / NDS : 1;
+  issue(0, true);
+  issue(1, nk > 1);
+  wait_vm_b<NA + NB>();
+  if (ld_ct) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ctab[r * BN + tid] = cv[r];
+  }
+  lds_sync_b();
+  rd(fa0, fb0, 0, 0);
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    rd(fa1, fb1, 1, s);
+    mma(fa0, fb0);
+#pragma unroll
+    for (int g = 0; g < NDS; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vm_b<0>();
+    lds_sync_b();
+    __builtin_amdgcn_sched_barrier(0);
+    issue(s, t + 2 < nk);
+    rd(fa0, fb0, 0, s ^ 1);
+    mma(fa1, fb1);
+#pragma unroll
+    for (int g = 0; g < NDS; ++g) {
+      if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+      if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  wait_vm_b<0>();   // the tail zero-fill DMAs land before the workgroup can retire
+  (void)NS;
+  igemm_epilogue32<MODE, BM, BN, WM, WN, EPI, EPD>(p, acc, ctab, red, tid, m0, n0, tile_m);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Halo-tiled direct convolution for stride-1 convs with narrow channels: the ResNet layer-1 3x3
 // (64 -> 64 channels at 56x56: FWD and DGRAD) and the space-to-depth stem (16 -> 64 channels,
 // 4x4 taps at 112x112).  The implicit GEMM above re-reads every input pixel once per filter tap
@@ -2229,6 +2674,56 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
+// igemm_dma32_kernel in place of igemm_dma_kernel for the 4-wave 128x128 / 128x64 FWD and DGRAD
+// GEMMs (use_dma4 cases 1 and 2) with at least dma32_mink K-tiles; not for the GELU epilogues (the
+// planner's Linear GEMMs keep their own kernels).  Knob dma32 = 0 restores igemm_dma_kernel (A/B).
+inline Knob kn_dma32("dma32", 0);
+inline Knob kn_dma32_mink("dma32_mink", 3);
+static bool use_dma32(int mode, const IgemmParams& p) {
+  return kn_dma32.get() && mode != MODE_WGRAD && p.nsplit == 1 && p.relu < 2 && p.gn % 8 == 0 &&
+         p.gk / BK >= kn_dma32_mink.get();
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
+static void launch_dma32(IgemmParams& p, hipStream_t st) {
+  p.tiles_m = ceil_div(p.gm, BM);
+  p.tiles_n = ceil_div(p.gn, BN);
+  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_dma32: partial-stats buffer too small");
+  TORCH_CHECK(p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0 && p.ksplit >= p.gk && p.nsplit == 1,
+              "igemm_dma32: needs the block-uniform tap walk and no split-K");
+  TORCH_CHECK(p.relu < 2 && p.gn % 8 == 0, "igemm_dma32: conv epilogues with 8-channel groups only");
+  const int grid = p.tiles_m * p.tiles_n;
+  constexpr size_t smem = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
+  static_assert(2 * smem <= 160 * 1024, "igemm_dma32: two blocks per CU");
+  int epi = EPI_PLAIN;
+  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
+  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
+#define PCMP_DMA32_LAUNCH(E, D)                                                                        \
+  do {                                                                                                \
+    auto kfn = &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D>;                                         \
+    static bool attr_set = false;                                                                     \
+    if (!attr_set) {                                                                                  \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
+      attr_set = true;                                                                                \
+    }                                                                                                 \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), smem, st, p);                                      \
+  } while (0)
+  if constexpr (MODE == MODE_FWD) {
+    if (epi == EPI_STATS) PCMP_DMA32_LAUNCH(EPI_STATS, 2); else PCMP_DMA32_LAUNCH(EPI_PLAIN, 2);
+  } else {
+    if (epi == EPI_BNR) {
+      if (kn_epi_depth.get() >= 4) PCMP_DMA32_LAUNCH(EPI_BNR, 4); else PCMP_DMA32_LAUNCH(EPI_BNR, 2);
+    } else if (epi == EPI_BNR2) {
+      if (kn_epi_depth_bnr2.get() >= 4) PCMP_DMA32_LAUNCH(EPI_BNR2, 4); else PCMP_DMA32_LAUNCH(EPI_BNR2, 2);
+    } else {
+      PCMP_DMA32_LAUNCH(EPI_PLAIN, 2);
+    }
+  }
+#undef PCMP_DMA32_LAUNCH
+  PCMP_LAUNCH_CHECK();
+}
+
 // Round-4 "big" kernel (igemm_big_kernel: 256 x 256 tiles on 8 waves or 256 x 128 on 4, 1 block per CU).
 // Knob big (bitmask): 1 = 256x256 tiles for FWD/DGRAD grids of >= big_min256 such tiles and
 // N <= big_maxn, 2 = 256x128 tiles where 256x256 would leave too many CUs idle (>= big_min128 tiles).
@@ -2632,8 +3127,12 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
   if constexpr (MODE != MODE_WGRAD) {
     if (use_bm64_smallgrid(MODE, p)) { launch_cfg<MODE, 64, 128, 2, 2>(p, st); return; }
     switch (use_dma4(MODE, p)) {
-      case 1: launch_dma<MODE, 128, 128, 2, 2, NT, 2>(p, st); return;
-      case 2: launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st); return;
+      case 1:
+        if (use_dma32(MODE, p)) launch_dma32<MODE, 128, 128, 2, 2>(p, st); else launch_dma<MODE, 128, 128, 2, 2, NT, 2>(p, st);
+        return;
+      case 2:
+        if (use_dma32(MODE, p)) launch_dma32<MODE, 128, 64, 2, 2>(p, st); else launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st);
+        return;
       case 3: launch_dma<MODE, 256, 64, 4, 1, NT, 2>(p, st); return;
       default: break;
     }

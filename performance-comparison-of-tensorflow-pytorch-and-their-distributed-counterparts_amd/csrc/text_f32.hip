@@ -262,6 +262,7 @@ std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tens
   const int T = ceil_div(M, LN_RPB);
   auto part = at::empty({T, np, D}, mean.options());
   auto st = cur_stream();
+  PCMP_ALLOW_BIG_LDS(ln_bwd_f32_kernel);
   hipLaunchKernelGGL(ln_bwd_f32_kernel, dim3(T), dim3(256), (size_t)4 * np * D * sizeof(float), st, ptr<float>(dyc),
                      ptr<float>(xs), ptr<float>(mean), ptr<float>(rstd), ptr<float>(g), ptr<float>(dx),
                      ptr<float>(dxd), ptr<float>(part), M, D, np, (float)p, (uint64_t)seed, (uint64_t)offset,
@@ -458,6 +459,7 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional
   at::Tensor idc;
   if (ids.has_value() && ids->defined()) idc = ids->contiguous();
   if (B * H == 0) return {ctx, lse};
+  PCMP_ALLOW_BIG_LDS(attn_fwd_f32_kernel);
   hipLaunchKernelGGL(attn_fwd_f32_kernel, dim3(B * H), dim3(std::min<int64_t>(256, (S + 63) / 64 * 64)),
                      attn_f32_smem(S), cur_stream(), ptr<float>(qkv), idc.defined() ? idc.data_ptr<int64_t>() : nullptr,
                      ptr<float>(ctx), ptr<float>(lse), (int)B, (int)S, (int)H, (float)p_drop, (uint64_t)seed,
@@ -484,11 +486,13 @@ at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at
   auto dS = at::empty({B * H, S, S}, qkv.options());
   const dim3 blk(std::min<int64_t>(256, (S + 63) / 64 * 64));
   auto st = cur_stream();
+  PCMP_ALLOW_BIG_LDS(attn_bwd_q_f32_kernel);
   hipLaunchKernelGGL(attn_bwd_q_f32_kernel, dim3(B * H), blk, attn_f32_smem(S), st, ptr<float>(qkv),
                      idc.defined() ? idc.data_ptr<int64_t>() : nullptr, ptr<float>(dc), ptr<float>(ctx),
                      ptr<float>(lse), ptr<float>(Pd), ptr<float>(dS), ptr<float>(dqkv), (int)B, (int)S, (int)H,
                      (float)p_drop, (uint64_t)seed, (uint64_t)offset, p_drop > 0.0 ? salt_ptr(salt) : nullptr);
   PCMP_LAUNCH_CHECK();
+  PCMP_ALLOW_BIG_LDS(attn_bwd_kv_f32_kernel);
   hipLaunchKernelGGL(attn_bwd_kv_f32_kernel, dim3(B * H), blk, (size_t)2 * S * AD32 * sizeof(float), st,
                      ptr<float>(qkv), ptr<float>(dc), ptr<float>(Pd), ptr<float>(dS), ptr<float>(dqkv), (int)B, (int)S,
                      (int)H);
@@ -749,6 +753,7 @@ std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh
   hipLaunchKernelGGL(lstm_transpose_f32_kernel, dim3(tgrid(wt.numel())), dim3(256), 0, st, ptr<float>(whh),
                      ptr<float>(wt), 4 * H, H);
   PCMP_LAUNCH_CHECK();
+  PCMP_ALLOW_BIG_LDS(lstm_fwd_f32_kernel);
   hipLaunchKernelGGL(lstm_fwd_f32_kernel, dim3(2 * ceil_div(B, LR)), dim3(H), (size_t)LR * H * sizeof(float), st,
                      ptr<float>(gx), ptr<float>(wt), idc.data_ptr<int64_t>(), ptr<float>(hout), ptr<float>(gates),
                      ptr<float>(cst), B, S, H);
@@ -769,6 +774,7 @@ std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& 
   auto sync = at::zeros({4}, gates.options().dtype(at::kInt));
   if (B == 0 || S == 0) return {dgates, sync};
   TORCH_CHECK((size_t)LR * 4 * H * sizeof(float) <= 64 * 1024, "lstm_seq_bwd (fp32): LDS");
+  PCMP_ALLOW_BIG_LDS(lstm_bwd_f32_kernel);
   hipLaunchKernelGGL(lstm_bwd_f32_kernel, dim3(2 * ceil_div(B, LR)), dim3(H), (size_t)LR * 4 * H * sizeof(float),
                      cur_stream(), ptr<float>(dh), ptr<float>(gc), ptr<float>(cc), ptr<float>(whh),
                      idc.data_ptr<int64_t>(), ptr<float>(dgates), B, S, H);

@@ -66,11 +66,6 @@ class TrainState:
         self.opt.zero_grad()
 
     def backward_step(self, loss):
-        if self.ddp is None and self.clip is None and self.timer is None:
-            # no gradient multiplier and no per-phase timing: the optimizer may start on the side
-            # stream before backward ends (SGD's tail step, pcmp.optim.SGD.prepare_step)
-            self.opt.set_grad_scale(None)
-            self.opt.prepare_step()
         with self.phase("backward"):
             loss.backward()
         if self.ddp is not None:
@@ -90,11 +85,22 @@ class TrainState:
         if self.throttle is not None:
             self.throttle.tick()
         self.steps_done += 1
-        if self.steps_done == 1 and self.ddp is not None and self.ddp.world > 1:
-            # every shape has been planned in this first step: all ranks take rank 0's kernels
-            from ..parallel.ddp import sync_autotune
-            sync_autotune(self.ddp.pg)
+        if self.steps_done == 1:
+            # every shape of a full batch has been planned in this first step: all ranks take rank
+            # 0's kernels (shapes first seen later are synced at the epoch ends, end_epoch)
+            self.end_epoch()
         watchdog_kick("train_step")
+
+    def end_epoch(self):
+        """Re-sync the autotuned kernel tables over the ranks when any rank planned new shapes."""
+        if self.ddp is not None and self.ddp.world > 1:
+            from ..parallel.ddp import sync_autotune_if_grown
+            sync_autotune_if_grown(self.ddp.pg)
+
+    def before_eval(self):
+        """Every rank evaluates with the ranks' mean BatchNorm running statistics (DDP)."""
+        if self.ddp is not None and self.ddp.world > 1:
+            self.ddp.average_buffers()
 
     def phase_report(self, printer=None):
         """Summarise the per-phase device times into ``history['phases']`` (and print one line)."""
@@ -184,7 +190,9 @@ def train_image_classifier(state: TrainState, trainloader, testloader, epochs=1,
                 running += loss.detach().double()
             n_in_window += 1
         printer(R.TRAINLOADER_DONE)
+        state.end_epoch()
         if (epoch % print_every) == 0 or epoch == epochs - 1:
+            state.before_eval()
             test_loss, test_acc = evaluate_images(model, testloader, reference_compat)
             tot = all_reduce_sum([float(running), n_in_window])
             train_loss = tot[0] / print_every if reference_compat else tot[0] / max(1.0, tot[1])
@@ -262,6 +270,7 @@ def train_text_classifier(state: TrainState, train_loader, val_loader=None, epoc
             total += loss.detach().double()
             n += 1
             state.backward_step(loss)
+        state.end_epoch()
         avg = all_reduce_sum([float(total), n])
         avg_train_loss = avg[0] / max(1.0, avg[1])
         state.history["train_loss"].append(avg_train_loss)

@@ -637,7 +637,6 @@ class StemFn(torch.autograd.Function):
         g_, fx, fc = _fold_args(dc)
         if ctx.s2d is False:
             if tail:
-                _params.fire_tail_step((L.weight,), (x,))
                 grads[L.weight] = emit_grad(L.weight, lambda out, acc: K.conv_wgrad(
                     g_, x, out, L.R, L.S, L.stride, L.pad, acc, fx, fc))
             else:
@@ -653,9 +652,6 @@ class StemFn(torch.autograd.Function):
                     out[..., :4].copy_(g)
                     out[..., 4:].zero_()
             if tail:
-                # every other gradient is final: the armed optimizer updates the rest of the model
-                # on the side stream while this WGRAD runs (ops/params.py fire_tail_step)
-                _params.fire_tail_step((L.weight,), (x,))
                 grads[L.weight] = emit_grad(L.weight, fill)
             else:
                 _wgrad(L, dc, x, grads, fill)

@@ -227,38 +227,3 @@ def run_on_side(fn: Callable[[], None], keep_alive) -> None:
         torch._C._cuda_setStream(stream_id=cur[0], device_index=cur[1], device_type=cur[2])
     for t in keep_alive:
         t.record_stream(side)
-
-
-# ------------------------------------------------------------------------------------------------
-# Early optimizer step at the tail of backward.  The last GEMM of a ResNet training step is the stem's
-# WGRAD (~260 us on the compute stream, profiles/r4_tail.txt); every other gradient is final by the
-# time it is enqueued.  An optimizer that arms the tail step (``arm_tail_step``) gets a callback from
-# the stem's backward just before that WGRAD: it steps every parameter but the pending ones on the
-# side stream -- ordered after the compute stream's work so far and after the side stream's own
-# queued WGRADs -- so the update overlaps the WGRAD; ``step()`` then covers only the rest.  The
-# compute stream joins the side stream at the end of backward as usual, so the next forward sees
-# every update.
-_TAIL: dict = {}
-
-
-def arm_tail_step(fn: Callable[[tuple], bool]) -> None:
-    """``fn(pending_params)`` enqueues the early part of this step's optimizer update (on the current
-    stream, which is the side stream when it runs) and returns whether it did."""
-    _TAIL["fn"] = fn
-
-
-def disarm_tail_step() -> None:
-    _TAIL.pop("fn", None)
-
-
-def fire_tail_step(pending: tuple, keep_alive) -> bool:
-    """Called by the last backward node before its final gradient GEMM; one-shot per arming."""
-    fn = _TAIL.pop("fn", None)
-    if fn is None or not _ENV["side"] or not keep_alive[0].is_cuda:
-        return False
-    done = [False]
-
-    def run():
-        done[0] = bool(fn(pending))
-    run_on_side(run, keep_alive)
-    return done[0]

@@ -329,20 +329,24 @@ def _lsr(z, k):
     return (z >> k) & ((1 << (64 - k)) - 1)
 
 
-def hash_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
-    """Bit-exact torch port of ``uniform01`` in csrc/common.h (32-bit lowbias32 mixing of the index
-    folded with the 64-bit seed)."""
+def _lowbias32(x):
     m32 = 0xFFFFFFFF
-    seed &= _M64
-    key = (seed & m32) ^ (((seed >> 32) * 0x9E3779B9) & m32)
-    i = idx.long()
-    x = torch.bitwise_xor(i & m32, (_lsr(i, 32) * 0x85EBCA6B) & m32)
-    x = torch.bitwise_xor(x, key)
     x = torch.bitwise_xor(x, x >> 16)
     x = (x * 0x7FEB352D) & m32
     x = torch.bitwise_xor(x, x >> 15)
     x = (x * 0x846CA68B) & m32
-    x = torch.bitwise_xor(x, x >> 16)
+    return torch.bitwise_xor(x, x >> 16)
+
+
+def hash_uniform(seed: int, idx: torch.Tensor) -> torch.Tensor:
+    """Bit-exact torch port of ``uniform01`` in csrc/common.h: lowbias32(lo32(idx) ^
+    lowbias32(hi32(idx) ^ key)), key = the 64-bit seed folded to 32 bits."""
+    m32 = 0xFFFFFFFF
+    seed &= _M64
+    key = (seed & m32) ^ (((seed >> 32) * 0x9E3779B9) & m32)
+    i = idx.long()
+    inner = _lowbias32(torch.bitwise_xor(_lsr(i, 32) & m32, key))
+    x = _lowbias32(torch.bitwise_xor(i & m32, inner))
     return (x >> 8).float() * (1.0 / 16777216.0)
 
 

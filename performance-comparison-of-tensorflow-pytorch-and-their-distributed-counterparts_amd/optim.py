@@ -14,12 +14,11 @@ LR and step live in device scalars so a captured hipGraph replays correctly acro
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 from .ops.kernels import K
-from .ops.params import arm_tail_step, bump_weight_gen, disarm_tail_step
+from .ops.params import bump_weight_gen
 from .utils.flat import FlatParams
 
 
@@ -40,10 +39,6 @@ class _FlatOptimizer:
     def set_lr(self, lr: float):
         self._lr = float(lr)
         self.lr_t.fill_(self._lr)
-
-    def prepare_step(self) -> bool:
-        """Called before backward; optimizers that can start early (SGD) arm a tail step here."""
-        return False
 
     def zero_grad(self, set_to_none: bool = True):
         self.flat.zero_grad()
@@ -87,39 +82,8 @@ class SGD(_FlatOptimizer):
                    f.shadow[lo:hi] if f.shadow is not None else None, None, self.lr_t, self.grad_scale,
                    self.momentum, self.dampening, self.wd, self.nesterov, self.steps == 0)
 
-    def prepare_step(self) -> bool:
-        """Arm the early tail step for the coming backward (pcmp.ops.params.arm_tail_step): the flat
-        prefix in front of the last backward node's pending parameters is updated on the side stream
-        while their gradient GEMM runs.  Only without a gradient multiplier (clip coefficient, 1/world):
-        those need every gradient first.  Opt-in (PCMP_TAIL_STEP=1): on ResNet-50 B=256 the early
-        update slows the stem WGRAD it overlaps by more than it saves, 12,773 -> 12,700-12,764 img/s
-        with a full or a 256-block grid, 3/3 rounds (profiles/r4_tail_step_ab.txt)."""
-        self._early = 0
-        if (self.grad_scale is not None or not self.flat.master.is_cuda
-                or os.environ.get("PCMP_TAIL_STEP", "0") != "1"):
-            disarm_tail_step()
-            return False
-        arm_tail_step(self._tail_step)
-        return True
-
-    def _tail_step(self, pending) -> bool:
-        f = self.flat
-        idx = {id(p): i for i, p in enumerate(f.params)}
-        pos = sorted(idx.get(id(p), -1) for p in pending)
-        # the pending parameters must be exactly the flat buffer's suffix (reverse registration order
-        # puts the first layer last), everything in front of them final
-        if not pos or pos[0] < 0 or pos != list(range(len(f.params) - len(pos), len(f.params))):
-            return False
-        lo = f.offsets[pos[0]]
-        self._sgd(0, lo)
-        self._early = lo
-        return True
-
     def step(self):
-        lo = getattr(self, "_early", 0)
-        self._early = 0
-        disarm_tail_step()   # armed but never fired (no tail node): the whole buffer below
-        self._sgd(lo, self.flat.numel)
+        self._sgd(0, self.flat.numel)
         self.steps += 1
         bump_weight_gen()
 

@@ -18,7 +18,12 @@ synchronised data parallelism the north star asks for:
   4 MB): the last bucket's all-reduce cannot overlap anything (it waits for the stem's gradient,
   the end of backward), so only a few MB stay exposed instead of up to a whole 32 MB bucket;
 * the 1/world averaging is folded into the optimizer kernel's gradient scale (no extra pass);
-* initial parameters and buffers are broadcast from rank 0 (DDP constructor semantics).
+* initial parameters and buffers are broadcast from rank 0 (DDP constructor semantics);
+  ``broadcast_buffers="forward"`` (or ``True``) re-broadcasts the buffers (BatchNorm running
+  statistics) from rank 0 at every forward as torch DDP does, as ONE coalesced broadcast per dtype;
+  the default ``"init"`` broadcasts them at construction only (running statistics do not enter a
+  training-mode forward) and :meth:`average_buffers` all-reduces them before an evaluation, so a
+  per-rank eval aggregated by ``parallel/metrics.py`` uses one set of statistics.
 
 Stream ordering (MI355X: compute stream + WGRAD side stream + RCCL's internal stream):
 
@@ -48,7 +53,7 @@ from ..utils.flat import FlatParams
 
 
 class _Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched", "streams", "events")
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched", "streams", "events", "t_launch")
 
     def __init__(self, index, start, end, params):
         self.index, self.start, self.end, self.params = index, start, end, params
@@ -57,6 +62,7 @@ class _Bucket:
         self.launched = False
         self.streams = {}       # stream id -> stream that wrote a gradient of this bucket this step
         self.events = {}        # stream id -> reusable event (recorded when the bucket launches)
+        self.t_launch = None    # timing: comm-stream event (GPU) / host seconds (CPU) at launch
 
 
 def plan_buckets(sizes, first_bucket_elems, bucket_elems, last_bucket_elems=0):
@@ -92,7 +98,7 @@ def _plan_greedy(sizes, first_bucket_elems, bucket_elems):
 
 class DistributedDataParallel(torch.nn.Module):
     def __init__(self, module: torch.nn.Module, flat: FlatParams, process_group=None, bucket_cap_mb: float = 32.0,
-                 first_bucket_mb: float = 4.0, broadcast_buffers: bool = True, average: bool = True,
+                 first_bucket_mb: float = 4.0, broadcast_buffers: bool | str = "init", average: bool = True,
                  last_bucket_mb: float = 4.0, force: bool | None = None, grad_dtype: torch.dtype | str | None = None):
         super().__init__()
         self.module = module
@@ -137,8 +143,16 @@ class DistributedDataParallel(torch.nn.Module):
         self._next_launch = 0
         self._timing = False
         self._exposed = []      # per step: (compute-done event, comm-done event) or host seconds
+        self._timeline = []     # per step: [(bucket, launch, done)] events (GPU) / seconds vs finish (CPU)
+        self._tl_stream = None
+        self._ev_ref = None
+        if broadcast_buffers is True:
+            broadcast_buffers = "forward"
+        if broadcast_buffers not in (False, "init", "forward"):
+            raise ValueError(f"broadcast_buffers: True / 'forward', 'init' or False, not {broadcast_buffers!r}")
+        self.buffer_mode = broadcast_buffers
         if self.world > 1:
-            self._broadcast_state(broadcast_buffers)
+            self._broadcast_state(broadcast_buffers is not False)
 
     # ------------------------------------------------------------------------------------------
     def time_exposed(self, on: bool = True):
@@ -147,10 +161,17 @@ class DistributedDataParallel(torch.nn.Module):
         cast-back) finishing on the comm stream.  CUDA events (no host sync); host seconds on CPU."""
         self._timing = bool(on)
         self._exposed = []
+        self._timeline = []
+        if on and self._comm_stream is not None and self._tl_stream is None:
+            self._tl_stream = torch.cuda.Stream(self.flat.grad.device)
 
     def comm_report(self) -> dict:
-        """Bucket plan + exposed communication time (mean/max ms over the timed steps)."""
+        """Bucket plan + exposed communication time (mean/max ms over the timed steps) + a per-bucket
+        timeline: when each bucket's all-reduce was launched and when it completed, in ms relative
+        to the end of backward (the compute stream reaching ``finish_gradient_sync``; negative =
+        before it), averaged over the timed steps, with the bytes each bucket moves."""
         esz = self.flat.grad.element_size()
+        wsz = torch.tensor([], dtype=self.grad_dtype).element_size()
         rep = {"active": bool(self.active), "world": self.world, "buckets": len(self.buckets),
                "bucket_mb": [round((b.end - b.start) * esz / 2 ** 20, 2) for b in self.buckets],
                "grad_allreduce_dtype": str(self.grad_dtype).replace("torch.", "")}
@@ -165,6 +186,18 @@ class DistributedDataParallel(torch.nn.Module):
             rep["exposed_ms"] = round(sum(vals) / len(vals), 4)
             rep["exposed_ms_max"] = round(max(vals), 4)
             rep["timed_steps"] = len(vals)
+        acc = {}
+        for step in self._timeline:
+            for bi, lt, dt in step:
+                a = acc.setdefault(bi, [0.0, 0.0, 0])
+                a[0] += lt
+                a[1] += dt
+                a[2] += 1
+        if acc:
+            rep["bucket_timeline"] = [
+                {"bucket": bi, "bytes": (self.buckets[bi].end - self.buckets[bi].start) * wsz,
+                 "launch_ms": round(a[0] / a[2], 4), "done_ms": round(a[1] / a[2], 4)}
+                for bi, a in sorted(acc.items())]
         return rep
 
     # ------------------------------------------------------------------------------------------
@@ -175,16 +208,45 @@ class DistributedDataParallel(torch.nn.Module):
         if buffers:
             self.sync_buffers()
 
+    def _buffer_groups(self):
+        groups = {}
+        for b in self.module.buffers():
+            if b.is_floating_point() or b.dtype in (torch.int64, torch.int32):
+                groups.setdefault((b.dtype, b.device), []).append(b)
+        return groups
+
     def sync_buffers(self):
+        """Broadcast every buffer from rank 0: one coalesced broadcast per (dtype, device)."""
         if self.world <= 1:
             return
         src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
-        for b in self.module.buffers():
-            if b.is_floating_point() or b.dtype in (torch.int64, torch.int32):
-                dist.broadcast(b, src, group=self.pg)
+        for bufs in self._buffer_groups().values():
+            flat = torch._utils._flatten_dense_tensors(bufs)
+            dist.broadcast(flat, src, group=self.pg)
+            for b, v in zip(bufs, torch._utils._unflatten_dense_tensors(flat, bufs)):
+                b.copy_(v)
+
+    def average_buffers(self):
+        """All-reduce the floating buffers (BatchNorm running mean / variance) to their mean over the
+        ranks and broadcast the integer ones (batch counters) from rank 0: every rank then evaluates
+        with the same statistics.  Call before an evaluation; the trainers do."""
+        if self.world <= 1:
+            return
+        src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+        for (dt, _), bufs in self._buffer_groups().items():
+            flat = torch._utils._flatten_dense_tensors(bufs)
+            if flat.is_floating_point():
+                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg)
+                flat.div_(self.world)
+            else:
+                dist.broadcast(flat, src, group=self.pg)
+            for b, v in zip(bufs, torch._utils._unflatten_dense_tensors(flat, bufs)):
+                b.copy_(v)
 
     def forward(self, *a, **kw):
         self._reset()
+        if self.buffer_mode == "forward" and self.world > 1 and torch.is_grad_enabled():
+            self.sync_buffers()
         return self.module(*a, **kw)
 
     def _reset(self):
@@ -213,6 +275,9 @@ class DistributedDataParallel(torch.nn.Module):
         if self._comm_stream is not None:
             s = torch.cuda.current_stream(p.device)
             b.streams[s.cuda_stream] = s
+            if self._timing and self._ev_ref is None:    # the step's first gradient: time origin
+                self._ev_ref = torch.cuda.Event(enable_timing=True)
+                self._ev_ref.record(s)
         b.pending -= 1
         if b.pending == 0:
             self._launch_ready()
@@ -229,6 +294,8 @@ class DistributedDataParallel(torch.nn.Module):
         view = self.flat.grad[b.start:b.end]
         cs = self._comm_stream
         if cs is None:                                   # CPU tensors (gloo)
+            if self._timing:
+                b.t_launch = time.perf_counter()
             if self._lowp is not None:
                 low = self._lowp[b.start:b.end]
                 low.copy_(view)
@@ -244,6 +311,9 @@ class DistributedDataParallel(torch.nn.Module):
                 ev = b.events[key] = torch.cuda.Event()
             ev.record(s)
             cs.wait_event(ev)
+        if self._timing:
+            b.t_launch = torch.cuda.Event(enable_timing=True)
+            b.t_launch.record(cs)                        # every gradient of the bucket written
         with torch.cuda.stream(cs):
             if self._lowp is not None:
                 low = self._lowp[b.start:b.end]
@@ -267,25 +337,55 @@ class DistributedDataParallel(torch.nn.Module):
             b.pending = 0
         self._launch_ready()
         ctx = torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()
+        line = []
         with ctx:
             for b in self.buckets:
                 if b.work is not None:
+                    if timing and cs is not None and b.t_launch is not None:
+                        # completion on a stream of its own: the comm stream is still queued behind
+                        # later buckets' input waits, the timeline stream only behind this collective
+                        with torch.cuda.stream(self._tl_stream):
+                            b.work.wait()
+                            ev_d = torch.cuda.Event(enable_timing=True)
+                            ev_d.record(self._tl_stream)
+                        line.append((b.index, b.t_launch, ev_d))
                     b.work.wait()
+                    if timing and cs is None and b.t_launch is not None:
+                        line.append((b.index, b.t_launch - t0, time.perf_counter() - t0))
                     if self._lowp is not None:
                         self.flat.grad[b.start:b.end].copy_(self._lowp[b.start:b.end])
                     b.work = None
+                b.t_launch = None
             if timing and cs is not None:
                 ev_b = torch.cuda.Event(enable_timing=True)
                 ev_b.record(cs)
                 self._exposed.append((ev_a, ev_b))
         if timing and cs is None:
             self._exposed.append(time.perf_counter() - t0)
+            self._timeline.append([(bi, lt * 1e3, dt * 1e3) for bi, lt, dt in line])
+        elif timing and line and self._ev_ref is not None:
+            self._timeline.append(_EventLine(self._ev_ref, ev_a, line))
+        self._ev_ref = None
         if cs is not None:
             torch.cuda.current_stream(cs.device).wait_stream(cs)
         self._reset()
 
     def grad_scale(self) -> float:
         return 1.0 / self.world if (self.average and self.world > 1) else 1.0
+
+
+class _EventLine:
+    """One step's GPU bucket timeline, resolved to ms relative to end of backward when iterated."""
+
+    def __init__(self, ev_ref, ev_end, line):
+        self.ev_ref, self.ev_end, self.line = ev_ref, ev_end, line
+
+    def __iter__(self):
+        self.ev_end.synchronize()
+        end = self.ev_ref.elapsed_time(self.ev_end)
+        for bi, ev_l, ev_d in self.line:
+            ev_d.synchronize()
+            yield bi, self.ev_ref.elapsed_time(ev_l) - end, self.ev_ref.elapsed_time(ev_d) - end
 
 
 def _parse_dtype(d) -> torch.dtype:
@@ -331,6 +431,29 @@ def sync_autotune(process_group=None) -> int:
     if not have or not table[0]:
         return 0
     return int(torch.ops.pcmp.autotune_load(table[0]))
+
+
+_SYNCED_MAX = [-1]   # the largest plan-table size any rank had at the last sync
+
+
+def sync_autotune_if_grown(process_group=None) -> int:
+    """Run :func:`sync_autotune` again when some rank planned shapes after the last sync (a last
+    partial batch, other text batch shapes, the first eval batches): one all-reduce of the table
+    sizes decides, so every rank takes the same branch.  Called at epoch ends by the training
+    loops; returns the entries applied (0 when nothing grew)."""
+    if not dist.is_initialized() or dist.get_world_size(process_group) <= 1:
+        return 0
+    from ..ops import _lib
+    n = len(torch.ops.pcmp.autotune_table()) if _lib.load() else 0
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(process_group) == "nccl" \
+        else torch.device("cpu")
+    t = torch.tensor([n], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=process_group)
+    m = int(t.item())
+    if m <= _SYNCED_MAX[0]:
+        return 0
+    _SYNCED_MAX[0] = m
+    return sync_autotune(process_group)
 
 
 def step_time_spread(seconds: float, process_group=None) -> dict:

@@ -147,42 +147,6 @@ def test_training_is_bitwise_deterministic(gpu):
         assert torch.equal(u, v)
 
 
-def test_sgd_tail_step_matches(gpu, monkeypatch):
-    """SGD's tail step (every parameter but the stem conv's updated on the side stream while the
-    stem WGRAD runs, SGD.prepare_step) fires on ResNet-50 and leaves losses, gradients, weights and
-    momenta bitwise those of the single update after backward."""
-    from pcmp.models.resnet import resnet50
-    from pcmp.ops import cross_entropy
-    from pcmp.optim import SGD
-    from pcmp.utils.flat import FlatParams
-
-    g = torch.Generator(device=gpu).manual_seed(7)
-    x = torch.rand(8, 3, 64, 64, device=gpu, generator=g)
-    y = torch.randint(0, 10, (8,), device=gpu, generator=g)
-
-    def run(tail):
-        monkeypatch.setenv("PCMP_TAIL_STEP", "1" if tail else "0")
-        torch.manual_seed(11)
-        m = resnet50(num_classes=10).to(gpu).train()
-        flat = FlatParams(m.parameters())
-        opt = SGD(flat, lr=0.01, momentum=0.9, weight_decay=5e-5)
-        losses, early = [], []
-        for _ in range(3):
-            opt.zero_grad()
-            loss = cross_entropy(m.forward_logits(x), y)
-            assert opt.prepare_step() == tail
-            loss.backward()
-            early.append(opt._early)
-            opt.step()
-            losses.append(loss.detach().clone())
-        torch.cuda.synchronize()
-        return early, torch.stack(losses), flat.grad.clone(), flat.master.clone(), flat.shadow.clone(), opt.mom.clone()
-
-    a, b = run(True), run(False)
-    assert all(e > 0 for e in a[0]) and all(e == 0 for e in b[0]), (a[0], b[0])
-    for u, v in zip(a[1:], b[1:]):
-        assert torch.equal(u, v)
-
 
 def test_stem_tail_mode_matches(gpu, monkeypatch):
     """Stem backward tail mode (BN-backward apply folded into the stem WGRAD, run on the compute

@@ -144,3 +144,21 @@ def test_stem_space_to_depth_equivalence(hw):
     torch.testing.assert_close(s2d_weight_grad(w4.grad), w7.grad[..., :4], rtol=1e-4, atol=1e-3)
     gx = s2d_input_grad(xs_.grad.permute(0, 2, 3, 1), hw, hw, 3, 8)
     torch.testing.assert_close(gx[..., :3], x7.grad[..., :3], rtol=1e-4, atol=1e-3)
+
+
+def test_hash_rng_consecutive_calls_uncorrelated():
+    """Eager dropout draws call k's mask at offset k << 32 (ops/functions.py).  The round-4 hash folded
+    both index words into one lowbias32 round, so call k+1's values were an index permutation of call
+    k's (advisor finding); the two-round hash must give independent streams: equal sorted values would
+    expose a permutation, and the values of the same index must be uncorrelated."""
+    n = 1 << 18
+    idx = torch.arange(n, dtype=torch.int64)
+    for k in (1, 77, 12345):
+        u1 = ref.hash_uniform(1234, idx + (k << 32))
+        u2 = ref.hash_uniform(1234, idx + ((k + 1) << 32))
+        assert not torch.equal(torch.sort(u1).values, torch.sort(u2).values)
+        c = torch.corrcoef(torch.stack([u1.double(), u2.double()]))[0, 1].item()
+        assert abs(c) < 0.01, c
+        m1, m2 = u1 >= 0.1, u2 >= 0.1
+        both = (m1 & m2).double().mean().item()
+        assert abs(both - 0.81) < 0.005, both

@@ -98,24 +98,3 @@ def test_optimizer_state_dict_roundtrip():
     o2.load_state_dict(sd)
     assert o2.lr == 1e-3 and torch.equal(o2.m1, o.m1) and o2.steps == 1
 
-
-def test_sgd_tail_step_split_equals_one_update():
-    """SGD's early tail step (pcmp.optim.SGD._tail_step: the flat prefix in front of the pending
-    parameters, then step() for the rest) gives the same update as one step over the whole buffer;
-    a pending set that is not the flat suffix is refused; prepare_step never arms on the CPU."""
-    def make():
-        torch.manual_seed(3)
-        m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Linear(5, 3))
-        flat = FlatParams(m.parameters(), shadow_dtype=None)
-        flat.grad.copy_(torch.randn_like(flat.grad))
-        return m, flat, popt.SGD(flat, lr=0.05, momentum=0.9, weight_decay=1e-3)
-
-    m1, f1, o1 = make()
-    o1.step()
-    m2, f2, o2 = make()
-    assert o2.prepare_step() is False                     # CPU: no side stream, never armed
-    first = list(m2.parameters())[0]                      # first registered = last in the flat buffer
-    assert o2._tail_step((list(m2.parameters())[-1],)) is False   # not the suffix
-    assert o2._tail_step((first,)) is True and o2._early > 0
-    o2.step()
-    assert torch.equal(f1.master, f2.master) and torch.equal(o1.mom, o2.mom)

@@ -56,10 +56,12 @@ def test_embed_layernorm_f32(gpu):
         assert _rel(a, e) < 1e-5
 
 
+@pytest.mark.parametrize("S", [128, 256, 137])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention_f32(gpu, p):
+def test_attention_f32(gpu, p, S):
+    """fp32 attention incl. S > 128 (up to 132 KB of dynamic LDS: the kernels opt in to > 64 KB)."""
     torch.manual_seed(2)
-    B, S, H = 3, 128, 4
+    B, H = 3, 4
     D = 64 * H
     qkv = torch.randn(B * S, 3 * D, device=gpu)
     ids = torch.randint(1, 100, (B, S), device=gpu)
