@@ -154,96 +154,44 @@ __device__ __forceinline__ void bn_bwd_finalize_channel(int c, double sg, double
   a.coef[2 * a.C + c] = k3;
 }
 
-// ---- fused stage-1 reduction + finalize (one launch instead of two) --------------------------
-typedef __attribute__((address_space(1))) unsigned long long gu64;   // global (not flat) shared words
-typedef __attribute__((address_space(1))) int gi32;
-// grid (ceil(C/32), G), 256 threads = 64 columns (sum 0 and sum 1 of 32 channels) x 4 row lanes.
-// Stage 1 is partials_reduce_kernel's arithmetic column for column (same rows, same order); each
-// block publishes its fp64 row of `red` with write-through (sc1) 8-byte agent-scope atomic stores,
-// drains them, and takes a ticket on its channel group's counter with an agent-scope release
-// fetch_add (the last arriver acquires before reading; an agent release per block, i.e. a
-// buffer_wbl2, cost 3.6% of the ResNet-50 step, which is why the knob stays off).  The last of
-// the G blocks reads the rows with sc1 (agent-scope atomic) loads, which bypass its L1, and runs
-// the finalize over the G rows in bn_finalize_kernel's order (lane g sums rows g, g+4, ...; lanes
-// added 0..3), so the result is bitwise that of the two-launch path, whichever block arrives last.
-// It resets the counter to zero for the next use of the slot.
-template <bool BWD, typename FA>
-__global__ __launch_bounds__(256) void partials_reduce_finalize_kernel(const float* __restrict__ part, int T, int C,
-                                                                      int rpb, double* __restrict__ red,
-                                                                      int* __restrict__ cnt, FA fa) {
-  __shared__ double sh[4][64];
-  __shared__ double shf[2][4][32];
-  __shared__ int flag;
+// ---- one-launch finalize for up to a few hundred partial rows -------------------------------
+// The GEMM epilogues emit one partial row per BM-row tile: 98-392 rows for ResNet-50's layer-3/4
+// BatchNorms at B=256.  1024 threads = 64 channels x 16 row lanes (8 loads in flight per thread),
+// the lanes summed in fixed order: ONE launch where the two-stage path (partials_reduce_kernel into
+// <= 64 fp64 rows + the finalize) takes two -- ~100 launches per ResNet-50 step, each a ~5 us
+// dependent kernel boundary on the compute stream.  (Round 4's single-launch alternative, a last-
+// arriver ticket over stage-1 blocks, paid an agent-scope release per block: -3.2 %, removed.)
+template <typename PT, bool BWD, typename FA>
+__global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(const PT* __restrict__ part, int T, int C, FA fa) {
+  __shared__ double sh[2][16][64];
   const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int cb = blockIdx.x * 32;
-  const int cj = cb + (j & 31);
-  const int L = 2 * C;
-  const int col = (j < 32) ? cj : C + cj;
-  const bool ok = cj < C;
-  const int r0 = blockIdx.y * rpb, r1 = min(T, r0 + rpb);
-  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (ok) {
-    int r = r0 + g;
-    for (; r + 28 < r1; r += 32) {
-      float v[8];
+  const int c = blockIdx.x * 64 + j;
+  double s1 = 0, s2 = 0;
+  if (c < C) {
+    int t = g;
+    for (; t + 48 < T; t += 64) {
+      PT a[4], b[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + 4 * u) * L + col];
+      for (int u = 0; u < 4; ++u) {
+        a[u] = part[(size_t)(t + 16 * u) * 2 * C + c];
+        b[u] = part[(size_t)(t + 16 * u) * 2 * C + C + c];
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s8[u] += v[u];
+      for (int u = 0; u < 4; ++u) { s1 += a[u]; s2 += b[u]; }
     }
-    for (; r < r1; r += 4) s8[0] += part[(size_t)r * L + col];
-  }
-  const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-  sh[g][j] = s;
-  __syncthreads();
-  gu64* redg = (gu64*)red;
-  if (g == 0 && ok)
-    __hip_atomic_store(redg + (size_t)blockIdx.y * L + col,
-                       (unsigned long long)__double_as_longlong(s + sh[1][j] + sh[2][j] + sh[3][j]),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-  __syncthreads();
-  gi32* my = (gi32*)cnt + blockIdx.x;
-  if (threadIdx.x == 0) {
-    // release/acquire pair in the HIP memory model: the ticket is an agent-scope
-    // release, the last arriver issues an agent-scope acquire before reading the rows.  This path
-    // is off by default (knob bn_fused_fin=0), so the extra L2 write-back costs the default nothing.
-    const int t = __hip_atomic_fetch_add(my, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    flag = (t == (int)gridDim.y - 1) ? 1 : 0;
-  }
-  __syncthreads();
-  if (!flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int G = gridDim.y;
-  const int q = threadIdx.x & 31, lane = (threadIdx.x >> 5) & 3;
-  const int c = cb + q;
-  if (threadIdx.x < 128) {
-    // all (<= 16 + 16) loads in flight first, then the ordered sums (G <= 64 by construction)
-    double va[16], vb[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int t = lane + 4 * k;
-      const bool in = c < C && t < G;
-      va[k] = in ? __longlong_as_double((long long)__hip_atomic_load(redg + (size_t)t * L + c, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
-      vb[k] = in ? __longlong_as_double((long long)__hip_atomic_load(redg + (size_t)t * L + C + c, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
+    for (; t < T; t += 16) {
+      s1 += part[(size_t)t * 2 * C + c];
+      s2 += part[(size_t)t * 2 * C + C + c];
     }
-    double a = 0, b = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (lane + 4 * k < G) { a += va[k]; b += vb[k]; }
-    shf[0][lane][q] = a;
-    shf[1][lane][q] = b;
   }
+  sh[0][g][j] = s1;
+  sh[1][g][j] = s2;
   __syncthreads();
-  if (threadIdx.x < 32 && c < C) {
-    double a = shf[0][0][q], b = shf[1][0][q];
-    for (int k = 1; k < 4; ++k) { a += shf[0][k][q]; b += shf[1][k][q]; }
-    if constexpr (BWD) bn_bwd_finalize_channel(c, a, b, fa);
-    else bn_finalize_channel(c, a, b, fa);
+  if (g == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) { s1 += sh[0][k][j]; s2 += sh[1][k][j]; }
+    if constexpr (BWD) bn_bwd_finalize_channel(c, s1, s2, fa);
+    else bn_finalize_channel(c, s1, s2, fa);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(my, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- finalize: partials [T][2][C] -> mean, invstd, scale, shift; running stats update --------
@@ -735,24 +683,15 @@ static at::Tensor reduce_partials(const at::Tensor& part, int& T_out) {
   return red;
 }
 
-int* counter_slots(int n, int device);   // igemm.hip: zeroed ticket counters, reset by their last user
-static Knob kn_bn_fused_fin("bn_fused_fin", 0);   // 1: one-launch partials reduction + finalize (neutral: off)
-
-// The fused path for T > 64 partial rows: returns false (caller takes the two-launch path) when
-// disabled or when no counters can be had (first use inside a graph capture).
+// Partial-row count up to which the finalize is one wide launch (knob bn_wide_rows; <= 64 rows the
+// 256-thread finalize reads them directly, above bn_wide_rows the two-stage path runs).
+static Knob kn_bn_wide_rows("bn_wide_rows", 512);
 template <bool BWD, typename FA>
-static bool fused_finalize(const at::Tensor& part, const FA& fa) {
+static bool wide_finalize(const at::Tensor& part, const FA& fa) {
   const int T = part.size(0), C = part.size(2);
-  if (T <= 64 || !kn_bn_fused_fin.get()) return false;
-  const int rpb = std::max(16, ceil_div(T, 64));
-  const int G = ceil_div(T, rpb);   // <= 64: the reducer holds 16 rows per lane in registers
-  TORCH_CHECK(G <= 64, "fused_finalize: too many row groups");
-  const int nb = ceil_div(C, 32);
-  int* cnt = counter_slots(nb, part.get_device());
-  if (!cnt) return false;
-  auto red = at::empty({G, 2 * (int64_t)C}, part.options().dtype(at::kDouble));
-  hipLaunchKernelGGL((partials_reduce_finalize_kernel<BWD, FA>), dim3(nb, G), dim3(256), 0, cur_stream(),
-                     ptr<float>(part), T, C, rpb, ptr<double>(red), cnt, fa);
+  if (T <= 64 || T > kn_bn_wide_rows.get()) return false;
+  hipLaunchKernelGGL((bn_finalize_wide_kernel<float, BWD, FA>), dim3(ceil_div(C, 64)), dim3(1024), 0, cur_stream(),
+                     ptr<float>(part), T, C, fa);
   PCMP_LAUNCH_CHECK();
   return true;
 }
@@ -776,7 +715,7 @@ std::vector<at::Tensor> bn_finalize(const at::Tensor& part, int64_t count, const
   }
   PCMP_CHECK_F32(part);
   TORCH_CHECK(part.is_contiguous(), "bn_finalize: contiguous partials");
-  if (fused_finalize<false>(part, FinFwd{(double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
+  if (wide_finalize<false>(part, FinFwd{(double)count, optr<float>(gamma), optr<float>(beta), optr<float>(running_mean),
                                          optr<float>(running_var), (float)momentum, (float)eps, ptr<float>(out) + 0 * C,
                                          ptr<float>(out) + 1 * C, ptr<float>(out) + 2 * C, ptr<float>(out) + 3 * C}))
     return {out[0], out[1], out[2], out[3]};
@@ -886,7 +825,7 @@ at::Tensor bn_bwd_finalize(const at::Tensor& part, int64_t count, const c10::opt
   }
   PCMP_CHECK_F32(part);
   TORCH_CHECK(part.is_contiguous(), "bn_bwd_finalize: contiguous partials");
-  if (fused_finalize<true>(part, FinBwd{(double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
+  if (wide_finalize<true>(part, FinBwd{(double)count, optr<float>(gamma), ptr<float>(mean), ptr<float>(invstd),
                                         optr<float>(dgamma), optr<float>(dbeta), (int)accumulate, ptr<float>(coef), C}))
     return coef;
   int T2;

@@ -1737,7 +1737,12 @@ __device__ __forceinline__ void igemm_epilogue32(const IgemmParams& p, f32x16 (&
   }
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, int EPI, int EPD = 2>
+// XP: the accumulators are transposed through LDS into igemm_dma_kernel's 16x16 D^T / PAIR
+// fragment layout and the tile runs igemm_epilogue_fd: a store / load instruction then covers 16
+// pixels x 64 B (4 lanes per pixel) instead of 32 pixels x 2 x 16 B, which is what the memory-bound
+// short-K DGRAD + BN-backward epilogues (residual, x and mask loads per output) need (per-shape A/B
+// profiles/r5_knob_dma32.txt: -14 to -25 % on the 1x1 DGRADs into 1024 / 2048 channels without it).
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int EPD = 2, bool XP = false>
 __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p) {
   constexpr int NW = 4, NTHR = 256;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -1833,7 +1838,7 @@ __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p
   // per-channel epilogue coefficients: loaded ahead of the first DMAs, written to LDS once the first
   // stage has landed (the prologue barrier publishes them)
   float cv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bool ld_ct = tid < BN && (bnr || (MODE == MODE_FWD && p.bias != nullptr));
+  const bool ld_ct = !XP && tid < BN && (bnr || (MODE == MODE_FWD && p.bias != nullptr));
   if (ld_ct) {
     const int c = min(n0 + tid, p.gn - 1);
     if constexpr (bnr) {
@@ -1881,16 +1886,13 @@ __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p
   };
   constexpr int NMF = 2 * TM * TN, NDS = 2 * (TM + TN), NVM = NA + NB;
   constexpr int DPM = NDS / NMF > 0 ? NDS / NMF : 1, MPD = NMF >= NDS ? NMF / NDS : 1;
-  issue(0, true);
-  issue(1, nk > 1);
-  wait_vm_b<NA + NB>();
-  if (ld_ct) {
-#pragma unroll
-    for (int r = 0; r < 6; ++r) ctab[r * BN + tid] = cv[r];
-  }
-  lds_sync_b();
-  rd(fa0, fb0, 0, 0);
-  for (int t = 0; t < nk; ++t) {
+  // K-tile t in three forms (compile-time, so each half stays one scheduling region): FULL issues
+  // the DMA of tile t+2; NODMA (t = nk-2) only waits for tile t+1; LAST (t = nk-1) has no barrier.
+  // No zero-fill DMA of a dead stage is issued or waited for: at 3-4 K-tiles per output tile (the
+  // short-K 1x1 DGRADs) two dead-DMA round trips per tile cost more than the loop saves.
+  enum { FULL = 0, NODMA = 1, LAST = 2 };
+  auto ktile = [&](int t, auto form) {
+    constexpr int F = decltype(form)::value;
     const int s = t & 1;
     rd(fa1, fb1, 1, s);
     mma(fa0, fb0);
@@ -1900,23 +1902,71 @@ __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p
       if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    wait_vm_b<0>();
-    lds_sync_b();
-    __builtin_amdgcn_sched_barrier(0);
-    issue(s, t + 2 < nk);
-    rd(fa0, fb0, 0, s ^ 1);
+    if constexpr (F != LAST) {
+      wait_vm_b<0>();
+      lds_sync_b();   // every wave's reads of stage s retired; stage t+1 landed for every wave
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (F == FULL) issue(s, true);
+      rd(fa0, fb0, 0, s ^ 1);
+    }
     mma(fa1, fb1);
+    if constexpr (F == FULL) {
 #pragma unroll
-    for (int g = 0; g < NDS; ++g) {
-      if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-      if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
+      for (int g = 0; g < NDS; ++g) {
+        if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
+      }
+    } else if constexpr (F == NODMA) {
+#pragma unroll
+      for (int g = 0; g < NDS; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
+  };
+  issue(0, true);
+  issue(1, true);   // nk >= 2 (the dispatcher sends >= 3 K-tiles)
+  wait_vm_b<NA + NB>();
+  if (ld_ct) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ctab[r * BN + tid] = cv[r];
   }
-  wait_vm_b<0>();   // the tail zero-fill DMAs land before the workgroup can retire
+  lds_sync_b();
+  rd(fa0, fb0, 0, 0);
+  for (int t = 0; t < nk - 2; ++t) ktile(t, std::integral_constant<int, FULL>{});
+  ktile(nk - 2, std::integral_constant<int, NODMA>{});
+  ktile(nk - 1, std::integral_constant<int, LAST>{});
   (void)NS;
-  igemm_epilogue32<MODE, BM, BN, WM, WN, EPI, EPD>(p, acc, ctab, red, tid, m0, n0, tile_m);
+  if constexpr (XP) {
+    // per-wave [WTM pixels][WTN + 4] fp32 image over the dead stage buffers
+    constexpr int RSX = WTN + 4;
+    __syncthreads();   // every wave's last fragment reads and tail DMAs are done
+    float* xb = reinterpret_cast<float*>(smem) + wid * WTM * RSX;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float* row = xb + (i * 32 + (lane & 31)) * RSX + j * 32 + 16 * (lane >> 5);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(row + 4 * q) =
+              f32x4{acc[j][i][4 * q], acc[j][i][4 * q + 1], acc[j][i][4 * q + 2], acc[j][i][4 * q + 3]};
+      }
+    constexpr int TM16 = WTM / 16, TN16 = WTN / 16;
+    f32x4 a16[TN16][TM16];
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < TN16; ++j)
+#pragma unroll
+      for (int i = 0; i < TM16; ++i)
+        a16[j][i] = *reinterpret_cast<const f32x4*>(xb + (i * 16 + fr) * RSX + (j >> 1) * 32 + fq * 8 + (j & 1) * 4);
+    __syncthreads();   // the images are read before the epilogue reuses the LDS
+    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, a16, smem, tid, m0, n0, tile_m, 0);
+  } else {
+    igemm_epilogue32<MODE, BM, BN, WM, WN, EPI, EPD>(p, acc, ctab, red, tid, m0, n0, tile_m);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2676,12 +2726,26 @@ static void launch_dma(IgemmParams& p, hipStream_t st) {
 
 // igemm_dma32_kernel in place of igemm_dma_kernel for the 4-wave 128x128 / 128x64 FWD and DGRAD
 // GEMMs (use_dma4 cases 1 and 2) with at least dma32_mink K-tiles; not for the GELU epilogues (the
-// planner's Linear GEMMs keep their own kernels).  Knob dma32 = 0 restores igemm_dma_kernel (A/B).
-inline Knob kn_dma32("dma32", 0);
+// planner's Linear GEMMs keep their own kernels).  Per-shape A/B on the ResNet-50 B=256 conv shapes
+// with their training epilogues (profiles/r5_knob_dma32.txt): every FWD + BN-statistics GEMM gains or
+// ties (l2 3x3 85.5 -> 72.4 us, l3 1x1 256->1024 60.4 -> 47.3, l4 3x3 73.3 -> 65.3, l4 1x1 2048->512
+// 37.4 -> 32.8), so do the 3x3 DGRAD + BN-reduce GEMMs (l1 157.7 -> 151.0, l2 107.2 -> 102.8, l4 85.5
+// -> 81.0); the short-K 1x1 DGRADs into wide outputs lose 4-30 % (l3 1x1 1024->256 125.6 -> 139.8, its
+// dual-BN form 153 -> 200) and stay on igemm_dma_kernel: DGRAD takes the new kernel for filters wider
+// than 1x1 or >= dma32_dgrad_mink K-tiles.  Knob dma32 = 0 restores igemm_dma_kernel (A/B).
+inline Knob kn_dma32("dma32", 1);
+inline Knob kn_dma32_modes("dma32_modes", 1);   // bit 0: FWD, bit 1: DGRAD (whole-step A/B: FWD only, profiles/r5_bench_ab_dma32_modes.txt)
 inline Knob kn_dma32_mink("dma32_mink", 3);
+inline Knob kn_dma32_dgrad_mink("dma32_dgrad_mink", 16);
+// dma32_xpose: 0 = register epilogue everywhere, 1 = LDS-transposed igemm_epilogue_fd for the
+// BN-backward DGRAD epilogues, 2 = for every epilogue
+inline Knob kn_dma32_xpose("dma32_xpose", 0);
 static bool use_dma32(int mode, const IgemmParams& p) {
-  return kn_dma32.get() && mode != MODE_WGRAD && p.nsplit == 1 && p.relu < 2 && p.gn % 8 == 0 &&
-         p.gk / BK >= kn_dma32_mink.get();
+  if (!kn_dma32.get() || mode == MODE_WGRAD || p.nsplit != 1 || p.relu >= 2 || p.gn % 8 != 0 ||
+      p.gk / BK < kn_dma32_mink.get())
+    return false;
+  if (!(kn_dma32_modes.get() & (mode == MODE_FWD ? 1 : 2))) return false;
+  return mode == MODE_FWD || p.R * p.S > 1 || p.gk / BK >= kn_dma32_dgrad_mink.get();
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>
@@ -2692,19 +2756,28 @@ static void launch_dma32(IgemmParams& p, hipStream_t st) {
   TORCH_CHECK(p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0 && p.ksplit >= p.gk && p.nsplit == 1,
               "igemm_dma32: needs the block-uniform tap walk and no split-K");
   TORCH_CHECK(p.relu < 2 && p.gn % 8 == 0, "igemm_dma32: conv epilogues with 8-channel groups only");
+  TORCH_CHECK(p.gk / BK >= 2, "igemm_dma32: at least two K-tiles");
   const int grid = p.tiles_m * p.tiles_n;
-  constexpr size_t smem = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
+  constexpr size_t smem_reg = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
+  constexpr size_t smem_xp = (size_t)4 * (BM / WM) * (BN / WN + 4) * sizeof(float);
+  constexpr size_t smem_fd = (size_t)(4 * 16 * (3 * (BN / WN) + 4) + WM * 3 * BN) * sizeof(float);
+  constexpr size_t smem = std::max(smem_reg, std::max(smem_xp, smem_fd));
   static_assert(2 * smem <= 160 * 1024, "igemm_dma32: two blocks per CU");
+  const int xk = kn_dma32_xpose.get();
   int epi = EPI_PLAIN;
   if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
 #define PCMP_DMA32_LAUNCH(E, D)                                                                        \
   do {                                                                                                \
-    auto kfn = &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D>;                                         \
+    const bool xp_ = xk >= 2 || (xk == 1 && (E == EPI_BNR || E == EPI_BNR2));                          \
+    auto kfn = xp_ ? &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, true>                              \
+                   : &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, false>;                           \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
-      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
+      for (auto f : {&igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, true>,                             \
+                     &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, false>})                           \
+        PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f),                          \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
       attr_set = true;                                                                                \
     }                                                                                                 \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), smem, st, p);                                      \
@@ -3233,37 +3306,57 @@ __global__ void __launch_bounds__(WM * WN * 64, MINB) gemm32_kernel(const IgemmP
   };
   constexpr int NMF = 2 * TM * TN, NDS = 2 * (TM + TN), NVM = NA + NB;
   constexpr int DPM = NDS / NMF > 0 ? NDS / NMF : 1, MPD = NMF >= NDS ? NMF / NDS : 1;
-  if (nk > 0) {
-    issue(0, 0, true);
-    issue(1, BK, nk > 1);
-    wait_vm_b<NA + NB>();
-    lds_sync_b();
-    rd(fa0, fb0, 0, 0);
-    for (int t = 0; t < nk; ++t) {
-      const int s = t & 1;
-      rd(fa1, fb1, 1, s);
-      mma(fa0, fb0);
+  // last two K-tiles peeled (no zero-fill DMA of a dead stage is issued or waited for), as in
+  // igemm_dma32_kernel
+  enum { FULL = 0, NODMA = 1, LAST = 2 };
+  auto ktile = [&](int t, auto form) {
+    constexpr int F = decltype(form)::value;
+    const int s = t & 1;
+    rd(fa1, fb1, 1, s);
+    mma(fa0, fb0);
 #pragma unroll
-      for (int g = 0; g < NDS; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    for (int g = 0; g < NDS; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (F != LAST) {
       wait_vm_b<0>();
       lds_sync_b();
       __builtin_amdgcn_sched_barrier(0);
-      issue(s, (t + 2) * BK, t + 2 < nk);
+      if constexpr (F == FULL) issue(s, (t + 2) * BK, true);
       rd(fa0, fb0, 0, s ^ 1);
-      mma(fa1, fb1);
+    }
+    mma(fa1, fb1);
+    if constexpr (F == FULL) {
 #pragma unroll
       for (int g = 0; g < NDS; ++g) {
         if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
         if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (F == NODMA) {
+#pragma unroll
+      for (int g = 0; g < NDS; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        if (g % DPM == 0) __builtin_amdgcn_sched_group_barrier(0x8, MPD, 1);
+      }
     }
-    wait_vm_b<0>();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if (nk > 0) {
+    issue(0, 0, true);
+    if (nk > 1) {
+      issue(1, BK, true);
+      wait_vm_b<NA + NB>();
+    } else {
+      wait_vm_b<0>();
+    }
+    lds_sync_b();
+    rd(fa0, fb0, 0, 0);
+    for (int t = 0; t < nk - 2; ++t) ktile(t, std::integral_constant<int, FULL>{});
+    if (nk >= 2) ktile(nk - 2, std::integral_constant<int, NODMA>{});
+    ktile(nk - 1, std::integral_constant<int, LAST>{});
   }
   // ---- epilogue: lane = output row m, 4 groups of 4 consecutive channels per 32x32 tile ----------
   if (p.nsplit > 1) {
@@ -3378,7 +3471,6 @@ static const char* plan_kind_name(int k) {
   }
 }
 
-int* counter_slots(int n, int device);
 template <int MODE>
 static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::TensorOptions& fopts, hipStream_t st) {
   const int kq = pl.kind == 6 ? 32 : BK;   // K granularity of the kernel
@@ -3528,10 +3620,6 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
 }
 
 
-// ------------------------------------------------------------------------------------------------
-// Zero-initialised int32 ticket counters for in-launch hand-offs (bn.hip's one-launch finalize,
-// knob bn_fused_fin): a per-device ring over one persistent buffer; the last user of a slot resets
-// it, so a slot is zero again once the kernel that used it has finished.
 
 static unsigned tensor_bytes(const at::Tensor& t) {
   const int64_t b = t.numel() * t.element_size();

@@ -32,30 +32,6 @@ std::vector<std::string> gemm_plans() {
   return r;
 }
 
-constexpr int kCounterSlots = 1 << 20;
-
-int* counter_slots(int n, int device) {
-  static std::mutex mu;
-  static std::unordered_map<int, std::pair<int*, int>> bufs;   // device -> (buffer, cursor)
-  std::lock_guard<std::mutex> g(mu);
-  auto it = bufs.find(device);
-  if (it == bufs.end()) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* buf = nullptr;
-    PCMP_HIP_CHECK(hipMalloc(&buf, sizeof(int) * kCounterSlots));
-    PCMP_HIP_CHECK(hipMemset(buf, 0, sizeof(int) * kCounterSlots));
-    PCMP_HIP_CHECK(hipDeviceSynchronize());
-    it = bufs.emplace(device, std::make_pair(buf, 0)).first;
-  }
-  auto& e = it->second;
-  if (n > kCounterSlots) return nullptr;
-  if (e.second + n > kCounterSlots) e.second = 0;
-  int* r = e.first + e.second;
-  e.second += n;
-  return r;
-}
-
 // src/dst: flat bf16 buffers; desc: int64 [n][12] on device (see wt_transpose_multi_kernel)
 void wt_transpose_multi(const at::Tensor& src, at::Tensor dst, const at::Tensor& desc, int64_t blocks) {
   PCMP_CHECK_CUDA(src); PCMP_CHECK_BF16(src); PCMP_CHECK_BF16(dst); PCMP_CHECK_CONTIG(src); PCMP_CHECK_CONTIG(dst);

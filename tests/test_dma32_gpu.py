@@ -35,15 +35,20 @@ def close_sum(a, b, rtol=2e-2, atol=1.0):
 
 
 def both(fn):
-    """fn() with the new kernel (dma32=1) and with the round-4 kernel (dma32=0)."""
+    """fn() with the new kernel (dma32=1; dma32_modes=3 and dma32_dgrad_mink=1 also route the DGRADs
+    the default policy keeps on the old kernel) and with the round-4 kernel (dma32=0)."""
     ops = _ops()
     old = ops.set_knob("dma32", 1)
+    oldk = ops.set_knob("dma32_dgrad_mink", 1)
+    oldm = ops.set_knob("dma32_modes", 3)
     try:
         a = fn()
         ops.set_knob("dma32", 0)
         b = fn()
     finally:
         ops.set_knob("dma32", old)
+        ops.set_knob("dma32_dgrad_mink", oldk)
+        ops.set_knob("dma32_modes", oldm)
     return a, b
 
 
@@ -60,7 +65,7 @@ SHAPES = [
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_dma32_fwd(gpu, shape):
+def test_dma32_fwd(gpu, shape, xpose):
     torch.manual_seed(1)
     N, H, W, C, K, R, s, p = shape
     ops = _ops()
@@ -84,8 +89,15 @@ def test_dma32_fwd(gpu, shape):
     assert torch.equal(y2, y3)
 
 
+@pytest.fixture(params=[0, 2], ids=["reg_epilogue", "lds_transposed_epilogue"])
+def xpose(request):
+    old = _ops().set_knob("dma32_xpose", request.param)
+    yield request.param
+    _ops().set_knob("dma32_xpose", old)
+
+
 @pytest.mark.parametrize("shape", SHAPES)
-def test_dma32_dgrad(gpu, shape):
+def test_dma32_dgrad(gpu, shape, xpose):
     torch.manual_seed(2)
     N, H, W, C, K, R, s, p = shape
     ops = _ops()
@@ -97,6 +109,8 @@ def test_dma32_dgrad(gpu, shape):
     dxr = ref.conv_dgrad(dy, w, H, W, s, p, res)
     close_el(dx, dxr)
     close_el(dx, dxo)
+    if R == 1 and s == 2:
+        return   # a 1x1 stride-2 DGRAD leaves pixel classes uncovered: no fused BN-backward form
     xb = rnd(N, H, W, C, dev=gpu)
     mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
     ymask = rnd(N, H, W, C, dev=gpu).relu()

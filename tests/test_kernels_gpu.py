@@ -203,11 +203,12 @@ def test_bn_forward_backward(gpu, C):
     close(gg, ggr)
 
 
-@pytest.mark.parametrize("T,C", [(65, 64), (6272, 64), (300, 72), (1568, 2048)])
-def test_bn_fused_finalize_bitwise(gpu, T, C):
-    """One-launch partials reduction + finalize (last-arriver ticket) == the two-launch path, bitwise,
-    for the forward (mean/invstd/scale/shift/running stats) and backward (dgamma/dbeta/coef)
-    finalize; both against an fp64 torch reduction.  Repeated calls reuse the ticket counters."""
+@pytest.mark.parametrize("T,C", [(65, 64), (392, 256), (512, 2048), (300, 72), (1568, 2048), (6272, 64)])
+def test_bn_wide_finalize(gpu, T, C):
+    """One-launch wide finalize (64 < T <= bn_wide_rows partial rows) == the two-stage path
+    (bn_wide_rows = 64) to fp64 rounding, for the forward (mean/invstd/scale/shift/running stats) and
+    backward (dgamma/dbeta/coef) finalize; both against an fp64 torch reduction; repeated calls are
+    bitwise equal."""
     ops = _ops()
     g = torch.Generator(device=gpu).manual_seed(T + C)
     part = torch.randn(T, 2, C, device=gpu, generator=g)
@@ -217,21 +218,22 @@ def test_bn_fused_finalize_bitwise(gpu, T, C):
     mean, invstd = torch.randn(C, device=gpu, generator=g), torch.rand(C, device=gpu, generator=g) + 0.5
     count = T * 16
     outs = {}
-    prev = ops.set_knob("bn_fused_fin", 0)
+    prev = ops.set_knob("bn_wide_rows", 512)
     try:
-        for v in (0, 1, 1, 1):
-            ops.set_knob("bn_fused_fin", v)
+        for v in (64, 512, 512):
+            ops.set_knob("bn_wide_rows", v)
             rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
             fwd = ops.bn_finalize(part, count, gam, bet, rm, rv, 0.1, 1e-5)
             dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), 0.25, device=gpu)
             coef = ops.bn_bwd_finalize(part, count, gam, mean, invstd, dg, db, True)
             outs.setdefault(v, []).append([t.clone() for t in (*fwd, rm, rv, dg, db, coef)])
     finally:
-        ops.set_knob("bn_fused_fin", prev)
-    base = outs[0][0]
-    for rep in outs[1]:
-        for a, b in zip(base, rep):
-            assert torch.equal(a, b)
+        ops.set_knob("bn_wide_rows", prev)
+    base = outs[512][0]
+    for a, b in zip(base, outs[512][1]):
+        assert torch.equal(a, b)
+    for a, b in zip(base, outs[64][0]):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
     s = part.double().sum(0)
     m = s[0] / count
     var = (s[1] / count - m * m).clamp_min(0)
