@@ -156,18 +156,34 @@ __device__ __forceinline__ int rr_off(int row, int chunk) {  // byte offset
 }
 
 // Transposed-read LDS image for WGRAD operands: [BK rows (reduction)][COLS] bf16.
-template <int COLS>
+// 16x16x32 reads (M32 = false): a 32-lane LDS cycle of ds_read_b64_tr_b16 covers 8 rows x 32 B, so 8
+// distinct even XOR masks spread the rows' 32-B pairs over the 64 banks.  32x32x16 reads (M32): a
+// 32-lane cycle covers 4 rows x 64 B (rows rowb..rowb+3, 32 columns), so the row's 64-B group is XOR-
+// shifted by a multiple of 4 chunks: (row & 3) for >= 256-B rows, ((row >> 1) & 1) for 128-B rows,
+// whose odd rows already sit on the other 32 banks.  (Round 4 used the 16x16x32 masks for the 32x32
+// reads: rows 0/1 and 2/3 collided, 33 % of the WGRAD kernel's LDS cycles were bank conflicts --
+// SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r5_wgrad_pmc.txt.)  The 16-B row writes (8 lanes
+// per row and cycle) stay conflict-free under either mapping.
+template <int COLS, bool M32 = false>
 __device__ __forceinline__ int tr_off(int row, int col) {  // byte offset of element (row,col), col%4==0 ok
   constexpr int RB = COLS * 2;  // row bytes
-  int f;
-  if constexpr (RB >= 256) {
-    f = (row & 3) | (((row >> 3) & 1) << 2);            // 8 distinct 32-B slots per half-wave
-  } else if constexpr (RB == 128) {
-    f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  int x;
+  if constexpr (M32) {
+    if constexpr (RB >= 256) x = 4 * (row & 3);
+    else if constexpr (RB == 128) x = 4 * ((row >> 1) & 1);
+    else x = 0;
   } else {
-    f = 0;
+    int f;
+    if constexpr (RB >= 256) {
+      f = (row & 3) | (((row >> 3) & 1) << 2);            // 8 distinct 32-B slots per half-wave
+    } else if constexpr (RB == 128) {
+      f = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    } else {
+      f = 0;
+    }
+    x = 2 * f;
   }
-  const int chunk = (col >> 3) ^ (2 * f);  // 16-B chunk, XOR keeps 32-B pairs intact
+  const int chunk = (col >> 3) ^ x;  // 16-B chunk, XOR keeps 32-B pairs intact
   return row * RB + (chunk << 4) + ((col & 7) << 1);
 }
 
@@ -827,7 +843,8 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
         }
         wa_off[i] += BK * p.K;
       }
-      // B': rows = m, cols = j=(r,s,c): im2col gather of x
+      // B': rows = m, cols = j=(r,s,c): im2col gather of x (a specialised linear walk for 1x1
+      // stride-1 convs measured neutral in the step, profiles/r5_wgrad_experiments.txt)
 #pragma unroll
       for (int i = 0; i < NVB; ++i) {
         const int row = (tid + NTHR * i) / CPR_B;
@@ -900,12 +917,12 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
 #pragma unroll
       for (int i = 0; i < NVA; ++i) {
         const int v = tid + NTHR * i;
-        *reinterpret_cast<uint4*>(sA + tr_off<BM>(v / CPR_A, wa_col)) = ra[i];
+        *reinterpret_cast<uint4*>(sA + tr_off<BM, M32>(v / CPR_A, wa_col)) = ra[i];
       }
 #pragma unroll
       for (int i = 0; i < NVB; ++i) {
         const int v = tid + NTHR * i;
-        *reinterpret_cast<uint4*>(sB + tr_off<BN>(v / CPR_B, wb_col)) = rb[i];
+        *reinterpret_cast<uint4*>(sB + tr_off<BN, M32>(v / CPR_B, wb_col)) = rb[i];
       }
     }
   };
@@ -928,15 +945,15 @@ __global__ void __launch_bounds__(NTHR, NTHR == NT ? 2 : 1) igemm_kernel(const I
 #pragma unroll
         for (int i = 0; i < TM32; ++i) {
           const int col = wr * WTM + i * 32 + 16 * (g & 1) + pc;
-          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb, col)));
-          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM>(rowb + 4, col)));
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM, true>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sA + tr_off<BM, true>(rowb + 4, col)));
           fa[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
 #pragma unroll
         for (int j = 0; j < TN32; ++j) {
           const int col = wc * WTN + j * 32 + 16 * (g & 1) + pc;
-          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb, col)));
-          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN>(rowb + 4, col)));
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN, true>(rowb, col)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(sB + tr_off<BN, true>(rowb + 4, col)));
           fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
 #pragma unroll
@@ -1283,25 +1300,11 @@ __global__ void __launch_bounds__(NTHR, MINB) igemm_dma_kernel(const IgemmParams
 }
 
 // ------------------------------------------------------------------------------------------------
-// "Big" LDS-DMA kernel for the compute-bound FWD/DGRAD GEMMs (round 4 main loop).  BM = 256 rows,
-// BN = 256 (8 waves, 2x4, 128x64 wave tiles) or 128 (4 waves, 2x2, 128x64), one block per CU, two LDS
-// stages.  The fragments are double-buffered over the two 32-deep halves of each 64-deep K-tile, so
-// there is ONE workgroup barrier per K-tile:
-//   half 0: ds_read frags(t, 1)  || MFMA frags(t, 0)
-//           vmcnt(0) [stage t+1 landed] + lgkmcnt(0) + barrier [every wave done reading stage t]
-//   half 1: DMA stage t+2 into stage t's buffer, ds_read frags(t+1, 0)  || MFMA frags(t, 1)
-// The DMA of stage t+2 has a whole K-tile of MFMAs to land.  The loop body is branch-free (the DMA of
-// the last two iterations reads out of range and zero-fills a dead stage; their fragment reads hit a
-// dead stage), so each half is one scheduling region: sched_group_barrier spreads the DMA issues and
-// ds_reads between the MFMAs (an LDS-DMA issue costs ~60 cycles of the issuing wave), and SG = 2 adds
-// sched_barrier fences so hipcc keeps each half's MFMAs on its side of the workgroup barrier.  Waits
-// use the s_waitcnt builtin (not inline asm), so hipcc's waitcnt pass sees them and adds no
-// conservative lgkmcnt waits in front of the half-1 MFMAs.
-// Measured in tools/gemm_lab (profiles/r4_gemm_lab.txt, same box, uniform random operands):
-// 8 waves + fences 1,283 TF at 4096^3 and 953 TF at 50176x256x2304 (the layer-3 3x3 GEMM) against
-// 1,249 / 898 for the same loop without interleave and fences; 4-wave 256x256 variants (256 fp32
-// accumulators per lane) lose 10-25 % to hipcc's AGPR copies.  Operand staging, swizzle, channel
-// permutation and epilogue are those of igemm_dma_kernel.
+// Waits visible to the compiler (the one-barrier-per-K-tile loops of igemm_dma32_kernel / gemm32_kernel):
+// the s_waitcnt builtin rather than inline asm, so hipcc's waitcnt pass sees them and adds no
+// conservative lgkmcnt waits in front of the MFMAs.  (Round 4's 8-wave one-barrier "big" FWD/DGRAD
+// kernel, igemm_big_kernel, was removed in round 5: neutral for the FWD GEMMs alone and -0.3 % to
+// -4.5 % with the DGRADs or the 256x128 tiles in the whole step, profiles/r5_big_fwd_ab.txt.)
 template <int N>
 __device__ __forceinline__ void wait_vm_b() {   // vmcnt(N) through the builtin (gfx9 simm16 encoding)
   static_assert(N >= 0 && N < 64, "vmcnt");
@@ -1311,169 +1314,6 @@ __device__ __forceinline__ void lds_sync_b() {   // lgkmcnt(0) + s_barrier, both
   __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));
   __builtin_amdgcn_s_barrier();
 }
-constexpr int BIG_BM = 256;
-template <int BN>
-constexpr int big_waves() { return BN == 256 ? 8 : 4; }
-
-template <int MODE, int BN, int EPI, int EPD = 2>
-__global__ void __launch_bounds__(big_waves<BN>() * 64, 1) igemm_big_kernel(const IgemmParams p) {
-  constexpr int BM = BIG_BM, NW = big_waves<BN>(), NTHR = NW * 64, WM = 2, WN = NW / 2;
-  constexpr int SG = NW == 8 ? 2 : 1;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
-  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;   // LDS-DMA instructions (8 rows each) per wave
-  static_assert(MODE != MODE_WGRAD, "FWD/DGRAD only");
-  static_assert(WTN % 32 == 0 && TN % 2 == 0, "PAIR channel permutation");
-  static_assert(NA >= 1 && NB >= 1, "loader");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid / WN, wc = wid % WN;
-
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int tiles_mn = p.tiles_m * p.tiles_n;
-  const int split = lin / tiles_mn;
-  const int tl = lin - split * tiles_mn;
-  const int tile_n = tl % p.tiles_n;
-  const int tile_m = tl / p.tiles_n;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int kbeg = split * p.ksplit;
-  const int nk = (min(p.gk, kbeg + p.ksplit) - kbeg) / BK;
-
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
-  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(p.b, p.b_bytes);
-  // loader slots: DMA instruction i of wave w fills LDS rows (w*NA + i)*8 .. +7; lane -> row
-  // + lane/8, position lane%8, loading global chunk (lane%8) ^ (row & 7)
-  const int gch = (lane & 7) ^ (lane >> 3);
-  int a_off[NA], a_y[NA], a_x[NA];
-  int b_off[NB];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int row0 = (wid * NA + i) * 8;
-    const int m = m0 + row0 + (lane >> 3);
-    const bool v = m < p.gm;
-    const int mm = v ? m : 0;
-    if constexpr (MODE == MODE_FWD) {
-      const int n = fdiv(mm, p.fd_PQ);
-      const int rem = mm - n * p.P * p.Q;
-      const int pp = fdiv(rem, p.fd_Q);
-      const int qq = rem - pp * p.Q;
-      const int yv = pp * p.stride - p.pad;
-      a_y[i] = v ? yv : -(1 << 28);
-      a_x[i] = qq * p.stride - p.pad;
-      a_off[i] = ((n * p.H + yv) * p.W + a_x[i]) * p.C + gch * 8;
-    } else {
-      const int n = fdiv(mm, p.fd_HW);
-      const int rem = mm - n * p.dH * p.dW;
-      const int hh = fdiv(rem, p.fd_W);
-      const int ww = rem - hh * p.dW;
-      const int yv = hh + p.offy;
-      a_y[i] = v ? yv : -(1 << 28);
-      a_x[i] = ww + p.offx;
-      a_off[i] = ((n * p.P + yv) * p.Q + a_x[i]) * p.K + gch * 8;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int rho = (wid * NB + i) * 8 + (lane >> 3);
-    const int n = n0 + chan_perm<true>(rho);
-    b_off[i] = n < p.gn ? n * p.gk + gch * 8 : -1;
-  }
-  // block-uniform tap / channel walk (C or K a multiple of BK)
-  const int CIN = (MODE == MODE_FWD) ? p.C : p.K;
-  int kc = kbeg % CIN, k0 = kbeg;
-  int ks = (kbeg / CIN) % p.S, kr = (kbeg / CIN) / p.S;
-  // DMA of the K-tile at (k0, kr, ks, kc) into stage s, then advance; !live: zero-fill (tail)
-  auto issue = [&](int s, bool live) {
-    int tap;
-    if constexpr (MODE == MODE_FWD) tap = (kr * p.W + ks) * p.C + kc;
-    else tap = -(kr * p.Q + ks) * p.K + kc;
-    char* dst = smem + s * STAGE;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      bool ok;
-      if constexpr (MODE == MODE_FWD)
-        ok = (unsigned)(a_y[i] + kr) < (unsigned)p.H && (unsigned)(a_x[i] + ks) < (unsigned)p.W;
-      else
-        ok = (unsigned)(a_y[i] - kr) < (unsigned)p.P && (unsigned)(a_x[i] - ks) < (unsigned)p.Q;
-      const int voff = (ok && live) ? (a_off[i] + tap) * 2 : (int)kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(dst + (wid * NA + i) * 1024),
-                                               16, voff, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int voff = (b_off[i] >= 0 && live) ? (b_off[i] + k0) * 2 : (int)kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsB, (__attribute__((address_space(3))) void*)(dst + A_BYTES + (wid * NB + i) * 1024), 16, voff, 0, 0, 0);
-    }
-    k0 += BK;
-    kc += BK;
-    if (kc >= CIN) {
-      kc = 0;
-      if (++ks == p.S) { ks = 0; ++kr; }
-    }
-  };
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-  auto rd = [&](bf16x8(&fa)[TM], bf16x8(&fb)[TN], int kk, int s) {
-    const char* sA = smem + s * STAGE;
-    const char* sB = sA + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-      fa[i] = *reinterpret_cast<const bf16x8*>(sA + rr_off(wr * WTM + i * 16 + (lane & 15), kk * 4 + (lane >> 4)));
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      fb[j] = *reinterpret_cast<const bf16x8*>(sB + rr_off(wc * WTN + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
-  };
-  auto mma = [&](bf16x8(&fa)[TM], bf16x8(&fb)[TN]) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
-  };
-  constexpr int NMF = TM * TN, NDS = TM + TN, NVM = NA + NB;
-
-  if (nk > 0) {
-    issue(0, true);
-    issue(1, nk > 1);
-    wait_vm_b<NA + NB>();
-    lds_sync_b();
-    rd(fa0, fb0, 0, 0);
-    for (int t = 0; t < nk; ++t) {
-      const int s = t & 1;
-      rd(fa1, fb1, 1, s);
-      mma(fa0, fb0);
-#pragma unroll
-      for (int g = 0; g < NDS; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);            // 1 DS_READ
-        __builtin_amdgcn_sched_group_barrier(0x8, NMF / NDS, 0);      // MFMAs
-      }
-      if constexpr (SG >= 2) __builtin_amdgcn_sched_barrier(0);
-      wait_vm_b<0>();
-      lds_sync_b();   // every wave's reads of stage s retired; stage t+1 landed for every wave
-      if constexpr (SG >= 2) __builtin_amdgcn_sched_barrier(0);
-      issue(s, t + 2 < nk);
-      rd(fa0, fb0, 0, s ^ 1);
-      mma(fa1, fb1);
-#pragma unroll
-      for (int g = 0; g < NDS; ++g) {
-        if (g < NVM) __builtin_amdgcn_sched_group_barrier(0x10, 1, 1);  // 1 VMEM (LDS-DMA)
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x8, NMF / NDS, 1);
-      }
-      if constexpr (SG >= 2) __builtin_amdgcn_sched_barrier(0);
-    }
-    wait_vm_b<0>();   // the tail zero-fill DMAs land before the epilogue reuses the LDS
-  }
-  igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, acc, smem, tid, m0, n0, tile_m, split);
-}
-
 // ------------------------------------------------------------------------------------------------
 // Round-5 critical-path FWD / DGRAD kernel: igemm_dma_kernel's operand staging (LDS-DMA, swizzled
 // 128-B rows, block-uniform tap walk) with the one-barrier-per-K-tile main loop of tools/gemm_lab v4
@@ -2797,83 +2637,6 @@ static void launch_dma32(IgemmParams& p, hipStream_t st) {
   PCMP_LAUNCH_CHECK();
 }
 
-// Round-4 "big" kernel (igemm_big_kernel: 256 x 256 tiles on 8 waves or 256 x 128 on 4, 1 block per CU).
-// Knob big (bitmask): 1 = 256x256 tiles for FWD/DGRAD grids of >= big_min256 such tiles and
-// N <= big_maxn, 2 = 256x128 tiles where 256x256 would leave too many CUs idle (>= big_min128 tiles).
-// Both need the block-uniform tap walk (source channels % 64) and >= big_mink K-tiles.
-// Default (profiles/r4_knob_ab_big.txt, in-process per-shape A/B on ResNet-50 B=256): the 8-wave
-// 256x256 path wins 2-5 % only on the N=256, >=196-tile layer-3 GEMMs (3x3 FWD/DGRAD, 1x1 to/from
-// 256 channels) and loses on N>=512 / fewer tiles; the 4-wave 256x128 path loses everywhere.  In the
-// whole training step (profiles/r4_bench_ab_big.txt) big=1 is still 0.3 % slower than big=0: its
-// 128 KB-LDS, 1-block-per-CU grid leaves no room for the side-stream WGRAD blocks, so it ships off.
-inline Knob kn_big("big", 0);
-inline Knob kn_big_maxn("big_maxn", 256);
-inline Knob kn_big_min256("big_min256", 192);
-inline Knob kn_big_min128("big_min128", 160);
-inline Knob kn_big_mink("big_mink", 4);
-
-template <int MODE, int BN>
-static void launch_big(IgemmParams& p, hipStream_t st) {
-  p.tiles_m = ceil_div(p.gm, BIG_BM);
-  p.tiles_n = ceil_div(p.gn, BN);
-  TORCH_CHECK(!p.stats || p.tiles_m <= p.stats_cap, "igemm_big: partial-stats buffer too small");
-  TORCH_CHECK(p.gk % BK == 0 && (MODE == MODE_FWD ? p.C : p.K) % BK == 0 && p.ksplit % BK == 0,
-              "igemm_big: needs the block-uniform tap walk");
-  TORCH_CHECK(p.nsplit == 1 || (!p.stats && !p.bn_x), "igemm_big: split-K only with the plain epilogue");
-  const int grid = p.tiles_m * p.tiles_n * p.nsplit;
-  size_t smem = (size_t)2 * (BIG_BM + BN) * BK * 2;
-  const bool epi_red = (MODE == MODE_FWD && p.stats) || (MODE == MODE_DGRAD && p.bn_x);
-  if (epi_red) {
-    const int NS = MODE == MODE_DGRAD && p.bn_x2 ? 3 : 2;
-    constexpr int NW = big_waves<BN>();
-    smem = std::max(smem, (size_t)(NW * 16 * (NS * (BN / (NW / 2)) + 4) + 2 * NS * BN) * sizeof(float));
-  }
-  TORCH_CHECK(smem <= 160 * 1024, "igemm_big: LDS budget");
-  int epi = EPI_PLAIN;
-  if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
-  if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
-#define PCMP_BIG_LAUNCH(E, D)                                                                         \
-  do {                                                                                                \
-    auto kfn = &igemm_big_kernel<MODE, BN, E, D>;                                                     \
-    static bool attr_set = false;                                                                     \
-    if (!attr_set) {                                                                                  \
-      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
-      attr_set = true;                                                                                \
-    }                                                                                                 \
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(big_waves<BN>() * 64), smem, st, p);                     \
-  } while (0)
-  if constexpr (MODE == MODE_FWD) {
-    if (epi == EPI_STATS) PCMP_BIG_LAUNCH(EPI_STATS, 2);
-    else if (p.relu >= 2) PCMP_BIG_LAUNCH(EPI_GELU, 2);
-    else PCMP_BIG_LAUNCH(EPI_PLAIN, 2);
-  } else {
-    if (epi == EPI_BNR) PCMP_BIG_LAUNCH(EPI_BNR, 2);
-    else if (epi == EPI_BNR2) {
-      if constexpr (BN == 128) PCMP_BIG_LAUNCH(EPI_BNR2, 2);   // 8 waves: the dual-BN epilogue spills
-      else TORCH_CHECK(false, "igemm_big: dual BN-reduce epilogue is instantiated for 256x128 tiles only");
-    }
-    else if (p.relu >= 2) PCMP_BIG_LAUNCH(EPI_GELU, 2);
-    else PCMP_BIG_LAUNCH(EPI_PLAIN, 2);
-  }
-#undef PCMP_BIG_LAUNCH
-  PCMP_LAUNCH_CHECK();
-}
-
-// 0: not used; 256 / 128: the tile width of the big kernel for this GEMM
-static int use_big(int mode, const IgemmParams& p) {
-  const int kb = kn_big.get();
-  if (!kb || mode == MODE_WGRAD || p.nsplit != 1 || p.fold_x || p.act_sc) return 0;
-  const int cin = mode == MODE_FWD ? p.C : p.K;
-  if (cin % BK != 0 || p.gk % BK != 0 || p.gk / BK < kn_big_mink.get()) return 0;
-  const int tm = ceil_div(p.gm, BIG_BM);
-  if ((kb & 1) && p.gn >= 256 && p.gn <= kn_big_maxn.get() && !(mode == MODE_DGRAD && p.bn_x2) &&
-      tm * ceil_div(p.gn, 256) >= kn_big_min256.get())
-    return 256;
-  if ((kb & 2) && p.gn >= 128 && tm * ceil_div(p.gn, 128) >= kn_big_min128.get()) return 128;
-  return 0;
-}
-
 // 4-wave LDS-DMA kernel (2 blocks per CU) in place of the register-staged 4-wave kernel for the
 // FWD/DGRAD GEMMs with the block-uniform tap walk and >= 3 K-tiles (measured
 // profiles/r1_dma4_ab.txt: 3x3 layers 10-16 % faster, e.g. layer4 3x3 DGRAD 97 -> 84 us; GEMMs
@@ -3077,7 +2840,6 @@ static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
 static int igemm_bm(int mode, const IgemmParams& p) {
   if (p.fold_x || p.act_sc) return 128;
   if (use_halo(mode, p)) return HALO_BM;
-  if (use_big(mode, p)) return BIG_BM;
   if (use_igemm8(mode, p)) return BM8;
   if (use_bm64_smallgrid(mode, p)) return 64;
   if (use_dma4(mode, p) == 3) return 256;
@@ -3185,11 +2947,6 @@ static void dispatch(IgemmParams& p, hipStream_t st) {
   if (p.fold_x || p.act_sc) { launch_fold<MODE>(p, st); return; }
   if constexpr (MODE != MODE_WGRAD) {
     if (use_halo(MODE, p)) { launch_halo<MODE>(p, st); return; }
-    switch (use_big(MODE, p)) {
-      case 256: launch_big<MODE, 256>(p, st); return;
-      case 128: launch_big<MODE, 128>(p, st); return;
-      default: break;
-    }
     if (use_igemm8(MODE, p) == 256) { launch_dma<MODE, 256, 256, 2, 4, NT8, 1>(p, st); return; }
   }
   if constexpr (MODE == MODE_WGRAD) {
@@ -3452,7 +3209,7 @@ inline Knob kn_plan_nsplit("plan_nsplit", 0); // tests: >= 1 (with plan_force) a
 struct GemmPlan {
   int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves),
                 // 3 = register-staged 64x64, 4 = register-staged 32x64, 5 = DMA 128x64 (small-M inference convs),
-                // 6 = skinny FWD, 7 / 8 = big 256x256 / 256x128 (4 waves, 1 block per CU)
+                // 6 = skinny FWD, 9 / 10 = 32x32x16 gemm32 128x128 / 256x256 (7 / 8: round 4 big kernel, removed)
   int nsplit;
 };
 static const char* plan_kind_name(int k) {
@@ -3463,8 +3220,6 @@ static const char* plan_kind_name(int k) {
     case 4: return "reg32x64";
     case 5: return "dma128x64";
     case 6: return "skinny64x64";
-    case 7: return "big256x256";
-    case 8: return "big256x128";
     case 9: return "m32_128x128";
     case 10: return "m32_256x256";
     default: return "default";
@@ -3493,8 +3248,6 @@ static void run_plan(IgemmParams p, const GemmPlan& pl, __bf16* out, const at::T
   else if (pl.kind == 3) launch_cfg<MODE, 64, 64, 2, 2>(p, st);
   else if (pl.kind == 4) launch_cfg<MODE, 32, 64, 1, 4>(p, st);
   else if (pl.kind == 5) launch_dma<MODE, 128, 64, 2, 2, NT, 2>(p, st);
-  else if (pl.kind == 7) launch_big<MODE, 256>(p, st);
-  else if (pl.kind == 8) launch_big<MODE, 128>(p, st);
   else if (pl.kind == 9) launch_gemm32<128, 128, 2, 2, 2>(p, st);
   else if (pl.kind == 10) launch_gemm32<256, 256, 2, 2, 1>(p, st);
   else if (pl.kind == 6) {
@@ -3578,8 +3331,6 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
         if (p.gn >= 256) cands.push_back({10, ns});
       }
       if (p.gn >= 256) cands.push_back({2, ns});
-      if (kn_big.get() & 1 && p.gn >= 256) cands.push_back({7, ns});
-      if (kn_big.get() & 2 && p.gn >= 128) cands.push_back({8, ns});
     }
   }
   if (force >= 0) {

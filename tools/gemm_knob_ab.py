@@ -4,7 +4,7 @@ BN-backward reduction (mask bits, residual gradient), WGRAD into an fp32 gradien
 rounds, min microseconds, achieved TB/s / TF/s, and the max abs difference against the first
 variant's output.
 
-Usage: python tools/gemm_knob_ab.py --variants 'base:;big:big=3' [--only l1_] [--rounds 3]
+Usage: python tools/gemm_knob_ab.py --variants 'base:;new:dma32=0' [--only l1_] [--rounds 3]
 """
 import argparse
 import os

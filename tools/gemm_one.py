@@ -1,6 +1,6 @@
 """Run one plain GEMM (or one conv case) a few times on the HIP kernels, for rocprofv3 --pmc passes.
 
-Usage: python tools/gemm_one.py --shape 8192,8192,8192 [--knobs big=3] [--plan 2] [--iters 5]
+Usage: python tools/gemm_one.py --shape 8192,8192,8192 [--knobs dma32=0] [--plan 2] [--iters 5]
        python tools/gemm_one.py --conv l3_3x3_256:fwd
 """
 import argparse

@@ -135,6 +135,22 @@ task_pmc_dgrad() {
     -d $R/gpurun_out/pmc/p2 -o run -- python $R/tools/dgrad_pmc.py > $R/gpurun_out/pmc/p2.log 2>&1 || die pmc-p2 $R/gpurun_out/pmc/p2.log
   cd $R
 }
+task_pmc_wgrad() {   # SHAPE=l3_3x3 ...: three passes (LDS, waits / MFMA, memory) over tools/wgrad_pmc.py
+  mkdir -p $R/gpurun_out/pmcw; cd /tmp
+  local sh=${SHAPE:-l3_3x3}
+  timeout -k 10 120 python -u $R/tools/wgrad_pmc.py > $R/gpurun_out/pmcw/${sh}_time.txt 2>&1 || die pmcw-time
+  cat $R/gpurun_out/pmcw/${sh}_time.txt
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
+    SQ_INSTS_LDS SQ_INSTS_VALU --kernel-trace --output-format csv -d $R/gpurun_out/pmcw/${sh}_p1 -o run -- \
+    python $R/tools/wgrad_pmc.py > $R/gpurun_out/pmcw/p1.log 2>&1 || die pmcw-p1 $R/gpurun_out/pmcw/p1.log
+  timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD \
+    GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $R/gpurun_out/pmcw/${sh}_p2 -o run -- \
+    python $R/tools/wgrad_pmc.py > $R/gpurun_out/pmcw/p2.log 2>&1 || die pmcw-p2 $R/gpurun_out/pmcw/p2.log
+  timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum --kernel-trace --output-format csv \
+    -d $R/gpurun_out/pmcw/${sh}_p3 -o run -- python $R/tools/wgrad_pmc.py > $R/gpurun_out/pmcw/p3.log 2>&1 || die pmcw-p3 $R/gpurun_out/pmcw/p3.log
+  cd $R
+  python tools/pmc_summary.py gpurun_out/pmcw/${sh}_p1 gpurun_out/pmcw/${sh}_p2 gpurun_out/pmcw/${sh}_p3 2>&1 | tail -40
+}
 
 [ $# -ge 1 ] || { sed -n '2,27p' "$0"; exit 2; }
 for t in "$@"; do
