@@ -22,6 +22,7 @@
 // (workgroup j owns columns j of dh_rec and the W_hh[:, j] slice); weight gradients are then
 // plain MFMA GEMMs over all timesteps (igemm wgrad), outside the recurrence.
 #include "common.h"
+#include "embed.h"
 #include "f32.h"
 
 namespace pcmp {
@@ -52,6 +53,8 @@ __global__ void embedding_bwd_kernel(const int64_t* __restrict__ ids, const __bf
     atomicAdd(dW + id * E + e, bf2f(reinterpret_cast<const unsigned short*>(dy)[i]));
   }
 }
+
+Knob kn_emb_atomic("emb_atomic", 0);
 
 // ------------------------------------------------------------------------------- masked mean
 // x [B][S][D] bf16, mask [B][S] (int64 ids > 0 or bool/uint8) -> y [B][D] bf16 = mean over valid t
@@ -468,8 +471,16 @@ void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, i
   const int E = dW.size(-1);
   if (!accumulate) dW.zero_();
   const int64_t rows = idc.numel();
-  hipLaunchKernelGGL(embedding_bwd_kernel, dim3(ew_grid(rows * E)), dim3(256), 0, cur_stream(), idc.data_ptr<int64_t>(),
-                     ptr<__bf16>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  if (rows == 0) return;
+  if (kn_emb_atomic.get()) {
+    hipLaunchKernelGGL(embedding_bwd_kernel, dim3(ew_grid(rows * E)), dim3(256), 0, cur_stream(), idc.data_ptr<int64_t>(),
+                       ptr<__bf16>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  } else {
+    auto sorted = at::sort(idc.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    const at::Tensor sid = std::get<0>(sorted).contiguous(), perm = std::get<1>(sorted).contiguous();
+    hipLaunchKernelGGL(embedding_bwd_seg_kernel<__bf16>, dim3(rows), dim3(256), 0, cur_stream(), sid.data_ptr<int64_t>(),
+                       perm.data_ptr<int64_t>(), ptr<__bf16>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  }
   PCMP_LAUNCH_CHECK();
 }
 

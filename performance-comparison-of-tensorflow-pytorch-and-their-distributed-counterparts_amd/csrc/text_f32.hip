@@ -12,6 +12,7 @@
 // These kernels favour simple, exact fp32 arithmetic over peak speed: the bf16 kernels carry the
 // throughput path; this path exists for reference-precision parity runs.
 #include "common.h"
+#include "embed.h"
 #include "f32.h"
 
 #include <vector>
@@ -543,8 +544,15 @@ void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, i
   if (!accumulate) dW.zero_();
   const int64_t rows = idc.numel();
   if (rows == 0) return;
-  hipLaunchKernelGGL(embedding_bwd_f32_kernel, dim3(tgrid(rows * E)), dim3(256), 0, cur_stream(),
-                     idc.data_ptr<int64_t>(), ptr<float>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  if (kn_emb_atomic.get()) {
+    hipLaunchKernelGGL(embedding_bwd_f32_kernel, dim3(tgrid(rows * E)), dim3(256), 0, cur_stream(),
+                       idc.data_ptr<int64_t>(), ptr<float>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  } else {   // deterministic segmented reduction (rnn.hip embedding_bwd_seg_kernel)
+    auto sorted = at::sort(idc.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    const at::Tensor sid = std::get<0>(sorted).contiguous(), perm = std::get<1>(sorted).contiguous();
+    hipLaunchKernelGGL(embedding_bwd_seg_kernel<float>, dim3(rows), dim3(256), 0, cur_stream(), sid.data_ptr<int64_t>(),
+                       perm.data_ptr<int64_t>(), ptr<float>(dyc), ptr<float>(dW), rows, E, padding_idx);
+  }
   PCMP_LAUNCH_CHECK();
 }
 

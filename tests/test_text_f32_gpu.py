@@ -172,3 +172,33 @@ def test_bilstm_fp32_grads_match_torch_fp32(gpu):
     ids[3, 20:] = 0
     y = torch.randint(0, 2, (40,), device=gpu, generator=g)
     _check_model(m, lambda: cross_entropy(m.forward_logits(ids), y), "bilstm")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_embedding_bwd_deterministic(gpu, dtype):
+    """Embedding backward (segmented over the stably sorted ids, one writer per vocabulary row) is
+    bitwise reproducible across runs and equals the fp64 index_add reference; padding rows skipped;
+    knob emb_atomic=1 (the fp32-atomic kernel) matches it to rounding."""
+    torch.manual_seed(5)
+    V, E, B, S = 300, 64, 8, 40
+    ids = torch.randint(0, V, (B, S), device=gpu)
+    ids[:, 30:] = 0
+    ids[0, :10] = 7                      # a long segment of one id
+    dy = torch.randn(B, S, E, device=gpu).to(dtype)
+    outs = []
+    for _ in range(3):
+        dW = torch.full((V, E), 0.5, device=gpu)
+        _ops().embedding_bwd(ids, dy, dW, 0, True)
+        outs.append(dW)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    keep = (ids.flatten() != 0)
+    ref = torch.zeros(V, E, dtype=torch.float64, device=gpu).index_add_(
+        0, ids.flatten()[keep], dy.reshape(-1, E)[keep].double()) + 0.5
+    torch.testing.assert_close(outs[0].double(), ref, rtol=1e-5, atol=1e-4)
+    old = _ops().set_knob("emb_atomic", 1)
+    try:
+        dW = torch.full((V, E), 0.5, device=gpu)
+        _ops().embedding_bwd(ids, dy, dW, 0, True)
+    finally:
+        _ops().set_knob("emb_atomic", old)
+    torch.testing.assert_close(dW, outs[0], rtol=1e-5, atol=1e-5)
