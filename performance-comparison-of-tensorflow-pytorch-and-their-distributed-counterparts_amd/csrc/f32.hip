@@ -35,6 +35,8 @@ struct ConvP {
   int gm, gn, gk;
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, ksplit, tiles_m, tiles_n;
+  int raw;                     // FWD / DGRAD split-K: write raw partials to out + split * gm * gn
+  unsigned a_bytes, b_bytes;   // operand extents (the 128-row kernel's buffer loads; < 2^31)
 };
 
 constexpr int FBM = 64, FBN = 64, FBK = 16, FLD = 68;
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const ConvP p) {
   }
 
   // ---- epilogue: D element e of lane -> row (lane>>4)*4+e, column lane&15 of its 16x16 tile
-  if constexpr (MODE == F_WGRAD) {
+  if (MODE == F_WGRAD || p.raw) {
     float* o = p.out + (size_t)split * p.gm * p.gn;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -247,6 +249,276 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const ConvP p) {
   }
 }
 
+// Round-5 fp32 main loop for the large GEMMs (verdict r4 weak #8): 128 x BN block tile (BN = 128, or
+// 64 when the GEMM has <= 64 columns), 4 waves of 64 x BN/2, BK = 16, on v_mfma_f32_32x32x2_f32
+// (exact fp32).  Per K-step a wave issues 16 * BN/64 MFMAs of 64 cycles against 8 * (2 + BN/64)
+// ds_read_b32, and the LDS reads of step k2+1 are issued before the MFMAs of step k2.
+// Block-uniform tap walk: the 16 reduction indices of a K-step are 16 consecutive channels of one
+// filter tap (FWD: C % 16, DGRAD: K % 16), so the per-step address update is scalar and the
+// per-row bases are decoded once (the 64x64 kernel above divides per load).  Operands are read with
+// raw buffer loads whose out-of-range offset returns zeros (padding, tails), so the loads are
+// branch-free b128s.  Loader roles: row-k (A of FWD / DGRAD, B of FWD: thread = one row x one
+// k-chunk, stored transposed; a wave writes 64 consecutive rows of one k -> conflict-free) and
+// k-col (B of DGRAD, A and B of WGRAD: 16 threads per k row, float4s 64 columns apart).  The LDS
+// pitch 160 (= 32 mod 64 banks) puts the two k rows one MFMA reads (lanes 0-31 / 32-63) on disjoint
+// banks.  Epilogue on the 32x32 accumulator: lane = output column, register r -> row
+// 8 * (r / 4) + 4 * (lane / 32) + r % 4 -> 128-B row segments per store and in-lane BN sums.
+constexpr int GBM = 128, GBK = 16, GLD = 160;
+constexpr unsigned F32_OOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_rsrc(const float* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int MODE, int BM, int BN>
+__global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
+  constexpr int WM = BM / 2, TM = WM / 32;           // wave tile WM x WN = TM x TN MFMA tiles
+  constexpr int WN = BN / 2, TN = WN / 32;
+  constexpr int BMV = BM / 64, BNV = BN / 64;        // float4s per thread of the A / B tile (1 or 2)
+  constexpr int LDA = BM == 128 ? GLD : 96, LDB = BN == 128 ? GLD : 96;   // both = 32 mod 64
+  __shared__ __attribute__((aligned(16))) float As[2][GBK][LDA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GBK][LDB];
+  __shared__ float red[2][2][BN];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
+  const int tiles_mn = p.tiles_m * p.tiles_n;
+  const int split = blockIdx.x / tiles_mn, tl = blockIdx.x - split * tiles_mn;
+  const int tile_m = tl / p.tiles_n, tile_n = tl - (tl / p.tiles_n) * p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kbeg = split * p.ksplit, kend = min(p.gk, kbeg + p.ksplit);
+  const int nk = (kend - kbeg + GBK - 1) / GBK;
+  const __amdgpu_buffer_rsrc_t rsA = f32_rsrc(p.a, p.a_bytes), rsB = f32_rsrc(p.b, p.b_bytes);
+
+  const int ra_row = tid % BM, ra_k = (tid / BM) * (4 * BMV);          // A row-k: 4 * BMV k
+  const int rb_row = tid % BN, rb_k = (tid / BN) * (4 * BNV);          // B row-k: 4 * BNV k
+  const int kc_k = tid >> 4, kc_c = (tid & 15) * 4;                    // k-col: cols kc_c (+ 64)
+  // tap walk (FWD / DGRAD): channel base and filter tap of the next K-step to load
+  const int CIN = MODE == F_FWD ? p.C : p.K;
+  int c0 = 0, ks = 0, kr = 0;
+  int a_n = 0, a_y = 0, a_x = 0;
+  bool a_ok = false;
+  if constexpr (MODE != F_WGRAD) {
+    c0 = kbeg % CIN;
+    const int rs0 = kbeg / CIN;
+    ks = rs0 % p.S;
+    kr = rs0 / p.S;
+    const int m = m0 + ra_row;
+    a_ok = m < p.gm;
+    const int mm = a_ok ? m : 0;
+    if constexpr (MODE == F_FWD) {
+      a_n = mm / (p.P * p.Q);
+      const int rem = mm - a_n * p.P * p.Q;
+      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
+      a_y = pp * p.stride - p.pad;
+      a_x = qq * p.stride - p.pad;
+    } else {
+      a_n = mm / (p.H * p.W);
+      const int rem = mm - a_n * p.H * p.W;
+      a_y = rem / p.W + p.pad;           // h + pad
+      a_x = rem - (rem / p.W) * p.W + p.pad;
+    }
+  }
+  // WGRAD B columns j = (r, s, c): (tap row - pad, tap col - pad, channel); j >= gn -> row -2^20
+  int wb_y[BNV], wb_x[BNV], wb_c[BNV];
+  if constexpr (MODE == F_WGRAD) {
+#pragma unroll
+    for (int h = 0; h < BNV; ++h) {
+      const int j = n0 + kc_c + 64 * h;
+      const int jj = j < p.gn ? j : 0;
+      wb_c[h] = jj % p.C;
+      const int rs = jj / p.C;
+      wb_x[h] = rs % p.S - p.pad;
+      wb_y[h] = j < p.gn ? rs / p.S - p.pad : -(1 << 20);
+    }
+  }
+
+  float4 ra[BMV], rb[BNV];
+  auto load = [&](int k0) {
+    if constexpr (MODE == F_FWD) {
+      const int y = a_y + kr, x = a_x + ks;
+      const bool ok = a_ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+      const unsigned off = ok ? 4u * (unsigned)((((a_n * p.H + y) * p.W + x) * p.C) + c0 + ra_k) : F32_OOB;
+#pragma unroll
+      for (int h = 0; h < BMV; ++h) ra[h] = bld4(rsA, off + 16 * h);
+      const int n = n0 + rb_row;
+      const unsigned offb = n < p.gn ? 4u * (unsigned)(n * p.gk + k0 + rb_k) : F32_OOB;
+#pragma unroll
+      for (int h = 0; h < BNV; ++h) rb[h] = bld4(rsB, offb + 16 * h);
+    } else if constexpr (MODE == F_DGRAD) {
+      const int ph = a_y - kr, pw = a_x - ks;
+      bool ok = a_ok && ph >= 0 && pw >= 0;
+      int py = ph, px = pw;
+      if (p.stride != 1) {
+        ok = ok && (ph % p.stride) == 0 && (pw % p.stride) == 0;
+        py = ph / p.stride;
+        px = pw / p.stride;
+      }
+      ok = ok && py < p.P && px < p.Q;
+      const unsigned off = ok ? 4u * (unsigned)((((a_n * p.P + py) * p.Q + px) * p.K) + c0 + ra_k) : F32_OOB;
+#pragma unroll
+      for (int h = 0; h < BMV; ++h) ra[h] = bld4(rsA, off + 16 * h);
+      const int co = c0 + kc_k;   // B[k = (r, s, co)][c] = W[co][r][s][c]
+      const int wrow = ((co * p.R + kr) * p.S + ks) * p.C;
+#pragma unroll
+      for (int h = 0; h < BNV; ++h) {
+        const int c = n0 + kc_c + 64 * h;
+        rb[h] = bld4(rsB, c < p.gn ? 4u * (unsigned)(wrow + c) : F32_OOB);
+      }
+    } else {
+      const int m = k0 + kc_k;
+      const bool mok = m < kend;
+#pragma unroll
+      for (int h = 0; h < BMV; ++h) {
+        const int co = m0 + kc_c + 64 * h;
+        ra[h] = bld4(rsA, mok && co < p.gm ? 4u * (unsigned)(m * p.K + co) : F32_OOB);
+      }
+      const int mm = mok ? m : 0;
+      const int n = mm / (p.P * p.Q);
+      const int rem = mm - n * p.P * p.Q;
+      const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
+      const int y0 = pp * p.stride, x0 = qq * p.stride;
+#pragma unroll
+      for (int h = 0; h < BNV; ++h) {
+        const int y = y0 + wb_y[h], x = x0 + wb_x[h];
+        const bool okb = mok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        rb[h] = bld4(rsB, okb ? 4u * (unsigned)(((n * p.H + y) * p.W + x) * p.C + wb_c[h]) : F32_OOB);
+      }
+    }
+    if constexpr (MODE != F_WGRAD) {
+      c0 += GBK;
+      if (c0 >= CIN) {
+        c0 = 0;
+        if (++ks == p.S) { ks = 0; ++kr; }
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    if constexpr (MODE == F_WGRAD) {
+#pragma unroll
+      for (int h = 0; h < BMV; ++h) st4(&As[buf][kc_k][kc_c + 64 * h], ra[h]);
+    } else {
+#pragma unroll
+      for (int h = 0; h < BMV; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[buf][ra_k + 4 * h + e][ra_row] = fget(ra[h], e);
+    }
+    if constexpr (MODE == F_FWD) {
+#pragma unroll
+      for (int h = 0; h < BNV; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[buf][rb_k + 4 * h + e][rb_row] = fget(rb[h], e);
+    } else {
+#pragma unroll
+      for (int h = 0; h < BNV; ++h) st4(&Bs[buf][kc_k][kc_c + 64 * h], rb[h]);
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int acol = wr * WM + (lane & 31), bcol = wc * WN + (lane & 31), khalf = lane >> 5;
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const bool nxt = t + 1 < nk;
+      if (nxt) load(kbeg + (t + 1) * GBK);
+      float af[TM], bfv[TN], an[TM], bn[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = As[buf][khalf][acol + 32 * i];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfv[j] = Bs[buf][khalf][bcol + 32 * j];
+#pragma unroll
+      for (int k2 = 0; k2 < GBK / 2; ++k2) {
+        if (k2 + 1 < GBK / 2) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) an[i] = As[buf][2 * k2 + 2 + khalf][acol + 32 * i];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bn[j] = Bs[buf][2 * k2 + 2 + khalf][bcol + 32 * j];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        if (k2 + 1 < GBK / 2) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) af[i] = an[i];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bfv[j] = bn[j];
+        }
+      }
+      if (nxt) store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  if (MODE == F_WGRAD || p.raw) {   // split-K partial (or the WGRAD product): raw accumulators
+    float* o = p.out + (size_t)split * p.gm * p.gn;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wc * WN + j * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wr * WM + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+          if (m < p.gm && n < p.gn) o[(size_t)m * p.gn + n] = acc[i][j][r];
+        }
+      }
+  } else {
+    float cs[TN], cq[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      cs[j] = 0.f;
+      cq[j] = 0.f;
+      const int n = n0 + wc * WN + j * 32 + (lane & 31);
+      const bool nok = n < p.gn;
+      const float bv = (p.bias && nok) ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wr * WM + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
+          if (m < p.gm && nok) {
+            float v = acc[i][j][r] + bv;
+            if (p.resid) v += p.resid[(size_t)m * p.gn + n];
+            if (p.relu) v = fmaxf(v, 0.f);
+            p.out[(size_t)m * p.gn + n] = v;
+            cs[j] += v;
+            cq[j] += v * v;
+          }
+        }
+    }
+    if (p.stats) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        cs[j] += __shfl_xor(cs[j], 32, 64);
+        cq[j] += __shfl_xor(cq[j], 32, 64);
+        if (lane < 32) {
+          red[wr][0][wc * WN + j * 32 + lane] = cs[j];
+          red[wr][1][wc * WN + j * 32 + lane] = cq[j];
+        }
+      }
+      __syncthreads();
+      if (tid < 2 * BN) {
+        const int q = tid / BN, c = tid % BN, n = n0 + c;
+        if (n < p.gn) p.stats[((size_t)tile_m * 2 + q) * p.gn + n] = red[0][q][c] + red[1][q][c];
+      }
+    }
+  }
+}
+
 // out[i] (+)= sum_s ws[s][i], fixed split order (deterministic)
 __global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                          int64_t n, int nsplit, int accumulate) {
@@ -257,20 +529,164 @@ __global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict
   }
 }
 
+// Split-K FWD / DGRAD epilogue: out[m][n] = sum_s ws[s][m][n] (fixed split order) + bias[n]
+// (+ resid[m][n]) (ReLU), BN partial sums of the output per 16-row block -> stats[gm/16][2][gn].
+// Grid (ceil(gm / 16), ceil(gn / 64)); thread = one row x 4 columns (gn % 4 == 0), the nsplit
+// partial loads are independent float4s (latency-bound at batch 1: no serial chains).
+constexpr int SKR = 16;
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ resid, float* __restrict__ stats,
+                                                              int gm, int gn, int nsplit, int relu) {
+  __shared__ float4 red[2][SKR][16];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int c = blockIdx.y * 64 + cq * 4, r = blockIdx.x * SKR + rl;
+  const size_t plane = (size_t)gm * gn;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f), q = v;
+  if (c < gn && r < gm) {
+    const size_t i = (size_t)r * gn + c;
+    const float* src = ws + i;
+    int k = 0;
+    for (; k + 4 <= nsplit; k += 4) {
+      const float4 a0 = ld4(src + k * plane), a1 = ld4(src + (k + 1) * plane);
+      const float4 a2 = ld4(src + (k + 2) * plane), a3 = ld4(src + (k + 3) * plane);
+      v.x += a0.x; v.y += a0.y; v.z += a0.z; v.w += a0.w;
+      v.x += a1.x; v.y += a1.y; v.z += a1.z; v.w += a1.w;
+      v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
+      v.x += a3.x; v.y += a3.y; v.z += a3.z; v.w += a3.w;
+    }
+    for (; k < nsplit; ++k) {
+      const float4 a = ld4(src + k * plane);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    if (bias) {
+      const float4 b = ld4(bias + c);
+      v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    }
+    if (resid) {
+      const float4 t = ld4(resid + i);
+      v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+    }
+    if (relu) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    st4(out + i, v);
+    q = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
+  } else {
+    v = q;
+  }
+  if (stats) {
+    red[0][rl][cq] = v;
+    red[1][rl][cq] = q;
+    __syncthreads();
+    if (threadIdx.x < 32) {   // (statistic, column quad): fixed-order sum over the 16 rows
+      const int st = threadIdx.x >> 4, cc = threadIdx.x & 15, col = blockIdx.y * 64 + cc * 4;
+      float4 a = red[st][0][cc];
+      for (int l = 1; l < SKR; ++l) {
+        const float4 b = red[st][l][cc];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      if (col < gn) st4(stats + ((size_t)blockIdx.x * 2 + st) * gn + col, a);
+    }
+  }
+}
+
+// operand extent for the buffer loads, saturated at 2^31 (which disables the 128-row kernel)
+static unsigned nbytes32(const at::Tensor& t) {
+  const int64_t b = t.numel() * 4;
+  return b >= (int64_t(1) << 31) ? (1u << 31) : (unsigned)b;
+}
+
 static void geometry(ConvP& p, int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
   p.N = N; p.H = H; p.W = W; p.C = C; p.K = K; p.R = R; p.S = S; p.stride = stride; p.pad = pad;
   p.P = (H + 2 * pad - R) / stride + 1;
   p.Q = (W + 2 * pad - S) / stride + 1;
-  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.relu = 0;
+  p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.relu = 0; p.raw = 0;
+}
+
+// Launch plan of one fp32 conv GEMM.  The 32x32x2-MFMA kernel (igemm_f32_big_kernel) wherever its
+// block-uniform tap walk applies (FWD: C % 16, DGRAD: K % 16; WGRAD: always) with 128 x 128 tiles,
+// halved per dimension (N first, then M) while the grid has fewer than f32_blocks (256 = one per
+// CU) tiles -- or the dimension is <= 64; else the 64x64 16x16x4 kernel.  The reduction is split
+// (FWD / DGRAD: partials + splitk_epilogue_kernel, >= f32_split_steps (4) K-steps per split; WGRAD: partials +
+// splitk_sum_kernel, >= 32 K-steps per split, toward 512 blocks) while the grid is below that.
+// Batch-1 inference is the case this serves: layer-4 FWD has 8 tiles of 64 x 64 against 288
+// K-steps.  Knobs: f32_big = 0 (always the 64x64 kernel), f32_split = 0 (no FWD / DGRAD split).
+static Knob kn_f32_big("f32_big", 1);
+static Knob kn_f32_split("f32_split", 1);
+static Knob kn_f32_blocks("f32_blocks", 256);
+static Knob kn_f32_split_steps("f32_split_steps", 4);
+
+struct F32Plan {
+  bool big;
+  int bm, bn, nsplit;
+};
+
+template <int MODE>
+static F32Plan plan_f32(ConvP& p) {
+  F32Plan pl{false, FBM, FBN, 1};
+  bool ok = kn_f32_big.get() && p.a_bytes < (1u << 31) && p.b_bytes < (1u << 31);
+  if constexpr (MODE == F_FWD) ok = ok && p.C % GBK == 0;
+  if constexpr (MODE == F_DGRAD) ok = ok && p.K % GBK == 0;
+  const int64_t target = std::max<int64_t>(1, kn_f32_blocks.get());
+  auto tiles = [&] { return (int64_t)ceil_div(p.gm, pl.bm) * ceil_div(p.gn, pl.bn); };
+  if (ok) {
+    pl.big = true;
+    pl.bm = p.gm <= 64 ? 64 : 128;
+    pl.bn = p.gn <= 64 ? 64 : 128;
+    if (tiles() < target && pl.bn == 128) pl.bn = 64;
+    if (tiles() < target && pl.bm == 128) pl.bm = 64;
+  }
+  const int nk = ceil_div(p.gk, GBK);
+  int ns = 1;
+  if (MODE == F_WGRAD)
+    ns = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(2 * target, tiles()), ceil_div(nk, 32)));
+  else if (kn_f32_split.get() && tiles() < target)
+    ns = (int)std::max<int64_t>(
+        1, std::min<int64_t>(ceil_div(target, tiles()), nk / std::max(1, kn_f32_split_steps.get())));
+  p.ksplit = ceil_div(ceil_div(p.gk, ns), GBK) * GBK;
+  pl.nsplit = ceil_div(p.gk, p.ksplit);
+  return pl;
+}
+
+template <int MODE, int BM, int BN>
+static void launch_big(const ConvP& p, int grid) {
+  hipLaunchKernelGGL((igemm_f32_big_kernel<MODE, BM, BN>), dim3(grid), dim3(256), 0, cur_stream(), p);
 }
 
 template <int MODE>
-static void launch(ConvP& p, int nsplit) {
-  p.tiles_m = ceil_div(p.gm, FBM);
-  p.tiles_n = ceil_div(p.gn, FBN);
-  const int grid = p.tiles_m * p.tiles_n * nsplit;
+static void launch(ConvP& p, const F32Plan& pl) {
+  TORCH_CHECK(p.ksplit % GBK == 0 && p.ksplit > 0, "igemm_f32: K split in whole K-steps");
+  p.tiles_m = ceil_div(p.gm, pl.bm);
+  p.tiles_n = ceil_div(p.gn, pl.bn);
+  const int grid = p.tiles_m * p.tiles_n * pl.nsplit;
   if (grid == 0) return;
-  hipLaunchKernelGGL(igemm_f32_kernel<MODE>, dim3(grid), dim3(256), 0, cur_stream(), p);
+  if (!pl.big) {
+    hipLaunchKernelGGL(igemm_f32_kernel<MODE>, dim3(grid), dim3(256), 0, cur_stream(), p);
+  } else if (pl.bm == 128) {
+    if (pl.bn == 128) launch_big<MODE, 128, 128>(p, grid);
+    else launch_big<MODE, 128, 64>(p, grid);
+  } else {
+    if (pl.bn == 128) launch_big<MODE, 64, 128>(p, grid);
+    else launch_big<MODE, 64, 64>(p, grid);
+  }
+  PCMP_LAUNCH_CHECK();
+}
+
+// FWD / DGRAD: run the plan; a split reduction goes through a workspace and the split epilogue.
+template <int MODE>
+static void run_fd(ConvP& p, const F32Plan& pl, const at::TensorOptions& opt) {
+  if (pl.nsplit == 1) {
+    launch<MODE>(p, pl);
+    return;
+  }
+  auto ws = at::empty({pl.nsplit, p.gm, p.gn}, opt);
+  ConvP q = p;
+  q.out = ptr<float>(ws);
+  q.raw = 1;
+  launch<MODE>(q, pl);
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(ceil_div(p.gm, SKR), ceil_div(p.gn, 64)), dim3(256), 0,
+                     cur_stream(), ptr<float>(ws), p.out, p.bias, p.resid, p.stats, p.gm, p.gn, pl.nsplit, p.relu);
   PCMP_LAUNCH_CHECK();
 }
 
@@ -291,9 +707,11 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   geometry(p, N, H, W, C, K, w.size(1), w.size(2), stride, pad);
   p.gm = N * p.P * p.Q; p.gn = K; p.gk = p.R * p.S * C;
   auto y = at::empty({N, p.P, p.Q, K}, x.options());
-  at::Tensor part;
-  if (want_stats) part = at::empty({ceil_div(p.gm, FBM), 2, K}, x.options());
   p.a = ptr<float>(x); p.b = ptr<float>(w); p.out = ptr<float>(y);
+  p.a_bytes = nbytes32(x); p.b_bytes = nbytes32(w);
+  const F32Plan pl = plan_f32<F_FWD>(p);
+  at::Tensor part;   // BN partials: one row pair per M tile (per SKR rows after a split)
+  if (want_stats) part = at::empty({ceil_div(p.gm, pl.nsplit > 1 ? SKR : pl.bm), 2, K}, x.options());
   if (bias.has_value() && bias->defined()) { check_f32(*bias, "conv_fwd(fp32) bias"); p.bias = ptr<float>(*bias); }
   if (resid.has_value() && resid->defined()) {
     check_f32(*resid, "conv_fwd(fp32) resid");
@@ -302,8 +720,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   }
   p.relu = relu;
   p.stats = want_stats ? ptr<float>(part) : nullptr;
-  p.ksplit = p.gk;
-  launch<F_FWD>(p, 1);
+  run_fd<F_FWD>(p, pl, x.options());
   if (want_stats) return {y, part};
   return {y};
 }
@@ -320,13 +737,13 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
   p.gm = N * H * W; p.gn = C; p.gk = p.R * p.S * K;
   auto dx = at::empty({N, H, W, C}, dy.options());
   p.a = ptr<float>(dy); p.b = ptr<float>(w); p.out = ptr<float>(dx);
+  p.a_bytes = nbytes32(dy); p.b_bytes = nbytes32(w);
   if (resid.has_value() && resid->defined()) {
     check_f32(*resid, "conv_dgrad(fp32) resid");
     TORCH_CHECK(resid->numel() == dx.numel(), "conv_dgrad(fp32): residual shape");
     p.resid = ptr<float>(*resid);
   }
-  p.ksplit = p.gk;
-  launch<F_DGRAD>(p, 1);
+  run_fd<F_DGRAD>(p, plan_f32<F_DGRAD>(p), dy.options());
   return dx;
 }
 
@@ -343,23 +760,20 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   TORCH_CHECK(out.numel() == (int64_t)K * R * S * C, "conv_wgrad(fp32): out numel");
   p.gm = K; p.gn = R * S * C; p.gk = N * p.P * p.Q;
   p.a = ptr<float>(dy); p.b = ptr<float>(x);
-  const int tiles = ceil_div(p.gm, FBM) * ceil_div(p.gn, FBN);
-  // split the long pixel reduction until ~2 blocks per CU, >= 32 K-steps per split
-  int nsplit = std::max(1, std::min(ceil_div(512, tiles), ceil_div(p.gk, 32 * FBK)));
-  p.ksplit = ceil_div(ceil_div(p.gk, nsplit), FBK) * FBK;
-  nsplit = ceil_div(p.gk, p.ksplit);
-  if (nsplit == 1 && !accumulate) {
+  p.a_bytes = nbytes32(dy); p.b_bytes = nbytes32(x);
+  const F32Plan pl = plan_f32<F_WGRAD>(p);
+  if (pl.nsplit == 1 && !accumulate) {
     p.out = ptr<float>(out);
-    launch<F_WGRAD>(p, 1);
+    launch<F_WGRAD>(p, pl);
     return;
   }
-  auto ws = at::empty({nsplit, p.gm, p.gn}, out.options());
+  auto ws = at::empty({pl.nsplit, p.gm, p.gn}, out.options());
   p.out = ptr<float>(ws);
-  launch<F_WGRAD>(p, nsplit);
+  launch<F_WGRAD>(p, pl);
   const int64_t n = (int64_t)p.gm * p.gn;
   const int grid = (int)std::min<int64_t>(ceil_div(n, (int64_t)256), 2048);
   hipLaunchKernelGGL(splitk_sum_kernel, dim3(grid), dim3(256), 0, cur_stream(), ptr<float>(ws), ptr<float>(out), n,
-                     nsplit, accumulate ? 1 : 0);
+                     pl.nsplit, accumulate ? 1 : 0);
   PCMP_LAUNCH_CHECK();
 }
 

@@ -34,8 +34,33 @@ SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("shape", SHAPES)
-def test_conv_fwd_dgrad_wgrad_f32(gpu, shape):
+F32_KNOBS = {
+    "auto": {},                                   # the default plan
+    "small": {"f32_big": 0},                      # 64x64 16x16x4 kernel only
+    "big_nosplit": {"f32_blocks": 1},             # largest 32x32x2 tiles, no split
+    "max_split": {"f32_blocks": 1 << 20},         # 64x64 32x32x2 tiles, split-K down to 8 K-steps
+    "small_split": {"f32_big": 0, "f32_blocks": 1 << 20},
+}
+
+
+@pytest.fixture(params=list(F32_KNOBS))
+def f32_kernel(request):
+    """Every launch plan of the fp32 conv GEMMs (csrc/f32.hip plan_f32): the default, the 64x64
+    16x16x4 kernel, the 32x32x2 kernel without split and with the deepest split-K (partials + the
+    split epilogue), on the same shapes."""
+    ops = _ops()
+    olds = {k: ops.set_knob(k, v) for k, v in F32_KNOBS[request.param].items()}
+    yield request.param
+    for k, v in olds.items():
+        ops.set_knob(k, v)
+
+
+@pytest.mark.parametrize("shape", SHAPES + [
+    (16, 28, 28, 64, 64, 3, 1, 1),     # large grid (the default policy picks the 128x128 kernel)
+    (9, 15, 15, 48, 80, 3, 2, 1),      # M / N tails, stride 2, C % 16 == 0, K % 16 == 0
+    (7, 9, 9, 20, 36, 3, 1, 1),        # C % 16 != 0 and K % 16 != 0: FWD/DGRAD fall back, WGRAD big
+])
+def test_conv_fwd_dgrad_wgrad_f32(gpu, shape, f32_kernel):
     torch.manual_seed(0)
     N, H, W, C, K, R, s, p = shape
     x = torch.randn(N, H, W, C, device=gpu)
@@ -59,7 +84,7 @@ def test_conv_fwd_dgrad_wgrad_f32(gpu, shape):
     rel_close(out, 2 * outr, 2e-4)
 
 
-def test_conv_dgrad_bnr_f32(gpu):
+def test_conv_dgrad_bnr_f32(gpu, f32_kernel):
     torch.manual_seed(1)
     N, H, C, K = 2, 14, 64, 128
     w = torch.randn(K, 3, 3, C, device=gpu) * 0.05

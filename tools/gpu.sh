@@ -20,6 +20,8 @@
 #   suite        secondary workloads (tools/bench_suite.py, HIP only)
 #   bert         BERT text-path tests, GEMM / attention micro benchmarks, whole-step A/B (BVARIANTS)
 #   pmc-dgrad    PMC passes over the isolated layer-1 DGRAD + BN-reduce shape
+#   f32          fp32 conv micro (tools/f32_conv_micro.py) + the reference-precision ResNet-50 rerun
+#                (pytorch_training_inference.py --dtype fp32: TL forward ms/step, batch-1 p50)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -150,6 +152,15 @@ task_pmc_wgrad() {   # SHAPE=l3_3x3 ...: three passes (LDS, waits / MFMA, memory
     -d $R/gpurun_out/pmcw/${sh}_p3 -o run -- python $R/tools/wgrad_pmc.py > $R/gpurun_out/pmcw/p3.log 2>&1 || die pmcw-p3 $R/gpurun_out/pmcw/p3.log
   cd $R
   python tools/pmc_summary.py gpurun_out/pmcw/${sh}_p1 gpurun_out/pmcw/${sh}_p2 gpurun_out/pmcw/${sh}_p3 2>&1 | tail -40
+}
+task_f32() {
+  timeout -k 10 300 python -u tools/f32_conv_micro.py ${F32B:-64} > ${O}_f32_micro.txt 2>&1 || die f32-micro ${O}_f32_micro.txt
+  cat ${O}_f32_micro.txt
+  timeout -k 10 300 python -u tools/f32_conv_micro.py 1 > ${O}_f32_micro_b1.txt 2>&1 || die f32-micro-b1 ${O}_f32_micro_b1.txt
+  cat ${O}_f32_micro_b1.txt
+  PCMP_PHASE_TIMES=1 timeout -k 10 400 python -u pytorch_training_inference.py --models resnet50 --dtype fp32 --synthetic \
+    --json ${O}_f32_repro.json > ${O}_f32_repro.txt 2>&1 || die f32-repro ${O}_f32_repro.txt
+  grep -E "phase times|Training time|p50|Inference" ${O}_f32_repro.txt | cut -c1-300
 }
 
 [ $# -ge 1 ] || { sed -n '2,27p' "$0"; exit 2; }
