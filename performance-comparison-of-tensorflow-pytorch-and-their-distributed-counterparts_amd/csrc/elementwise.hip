@@ -10,6 +10,7 @@
 //   * Dropout(0.2/0.4/0.5/0.1) — counter-based hash RNG, mask regenerated in backward
 //   * ToTensor/normalise of the image pipeline — fused NCHW f32/u8 -> NHWC bf16
 //     with zero channel padding to a multiple of 8 (the stem conv's MFMA K granularity)
+#include <type_traits>
 #include "common.h"
 #include "f32.h"
 
@@ -783,10 +784,10 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const unsigned char* __re
 // the image and for c >= Cin) with the 7x7 filter embedded in an 8x8 one (ops/conv_blocks.py
 // s2d_weight): the GEMM reduction shrinks from 7*7*8 (Cin padded to 8 for 16-B chunks) to
 // 4*4*16 = 256, four full K-tiles, and every 16-B chunk still holds one tap's channels.
-// One thread per S pixel (16 channels = two 16-B stores).  NHWC: X is [N,H,W,Cs] bf16 (the
-// 8-channel padded stem input) instead of [N,Cin,H,W] f32/u8.
-template <typename T, bool NHWC>
-__global__ void image_to_s2d_kernel(const T* __restrict__ x, __bf16* __restrict__ y, int N, int Cin, int H, int W,
+// One thread per S pixel (16 channels = two 16-B stores).  NHWC: X is [N,H,W,Cs] (the 8-channel
+// padded stem input; bf16, or fp32 for the fp32 path, TO = float) instead of [N,Cin,H,W] f32/u8.
+template <typename T, bool NHWC, typename TO = __bf16>
+__global__ void image_to_s2d_kernel(const T* __restrict__ x, TO* __restrict__ y, int N, int Cin, int H, int W,
                                     int Cs, int Hs, int Ws, int pad, float scale, const float* __restrict__ mean,
                                     const float* __restrict__ stdv) {
   const int64_t total = (int64_t)N * Hs * Ws;
@@ -820,8 +821,14 @@ __global__ void image_to_s2d_kernel(const T* __restrict__ x, __bf16* __restrict_
         v[d * 4 + c] = a;
       }
     }
-    st8(y + t * 16, v);
-    st8(y + t * 16 + 8, v + 8);
+    if constexpr (std::is_same<TO, float>::value) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(y + t * 16 + 4 * q) = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+      st8(y + t * 16, v);
+      st8(y + t * 16 + 8, v + 8);
+    }
   }
 }
 
@@ -1152,9 +1159,14 @@ at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c1
   const int Cs = nhwc ? x.size(3) : 0;
   TORCH_CHECK(Cin <= 4 && pad >= 0, "image_to_s2d: at most 4 input channels");
   const int Hs = (H + 2 * pad + 1) / 2, Ws = (W + 2 * pad + 1) / 2;
-  auto y = at::empty({N, Hs, Ws, 16}, x.options().dtype(at::kBFloat16));
+  const bool f32 = nhwc && x.scalar_type() == at::kFloat;   // fp32 path: fp32 in, fp32 out
+  auto y = at::empty({N, Hs, Ws, 16}, x.options().dtype(f32 ? at::kFloat : at::kBFloat16));
   const int64_t total = (int64_t)N * Hs * Ws;
-  if (nhwc) {
+  if (f32) {
+    hipLaunchKernelGGL((image_to_s2d_kernel<float, true, float>), dim3(grid_for(total, 256, INT_MAX)), dim3(256), 0,
+                       cur_stream(), ptr<float>(x), ptr<float>(y), N, Cin, H, W, Cs, Hs, Ws, (int)pad, 1.f, nullptr,
+                       nullptr);
+  } else if (nhwc) {
     PCMP_CHECK_BF16(x);
     hipLaunchKernelGGL((image_to_s2d_kernel<__bf16, true>), dim3(grid_for(total, 256, INT_MAX)), dim3(256), 0, cur_stream(),
                        ptr<__bf16>(x), ptr<__bf16>(y), N, Cin, H, W, Cs, Hs, Ws, (int)pad, 1.f, nullptr, nullptr);

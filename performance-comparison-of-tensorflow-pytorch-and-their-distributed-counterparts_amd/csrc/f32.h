@@ -9,9 +9,12 @@
 namespace pcmp {
 namespace f32 {
 
+// in_scale / in_shift (optional, per input channel): the conv reads relu(x * in_scale + in_shift)
+// (a BatchNorm + ReLU left unmaterialised by the producer; zero padding stays zero).
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
-                                 bool relu, bool want_stats);
+                                 bool relu, bool want_stats, const at::Tensor* in_scale = nullptr,
+                                 const at::Tensor* in_shift = nullptr);
 at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W, int64_t stride, int64_t pad,
                       const c10::optional<at::Tensor>& resid);
 std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W,
@@ -23,7 +26,8 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
                                        const c10::optional<at::Tensor>& mshift,
                                        const c10::optional<at::Tensor>& ymask_bits);
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-                int64_t pad, bool accumulate);
+                int64_t pad, bool accumulate, const at::Tensor* in_scale = nullptr,
+                const at::Tensor* in_shift = nullptr);
 
 at::Tensor bn_partials(const at::Tensor& x);
 at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,

@@ -36,6 +36,8 @@ struct ConvP {
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, ksplit, tiles_m, tiles_n;
   int raw;                     // FWD / DGRAD split-K: write raw partials to out + split * gm * gn
+  const float* isc;            // FWD A / WGRAD B operand read as relu(x * isc + ish) (per channel C)
+  const float* ish;
   unsigned a_bytes, b_bytes;   // operand extents (the 128-row kernel's buffer loads; < 2^31)
 };
 
@@ -263,7 +265,10 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const ConvP p) {
 // pitch 160 (= 32 mod 64 banks) puts the two k rows one MFMA reads (lanes 0-31 / 32-63) on disjoint
 // banks.  Epilogue on the 32x32 accumulator: lane = output column, register r -> row
 // 8 * (r / 4) + 4 * (lane / 32) + r % 4 -> 128-B row segments per store and in-lane BN sums.
-constexpr int GBM = 128, GBK = 16, GLD = 160;
+#ifndef F32_BK
+#define F32_BK 32
+#endif
+constexpr int GBK = F32_BK;
 constexpr unsigned F32_OOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_rsrc(const float* base, unsigned bytes) {
@@ -278,11 +283,13 @@ template <int MODE, int BM, int BN>
 __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
   constexpr int WM = BM / 2, TM = WM / 32;           // wave tile WM x WN = TM x TN MFMA tiles
   constexpr int WN = BN / 2, TN = WN / 32;
-  constexpr int BMV = BM / 64, BNV = BN / 64;        // float4s per thread of the A / B tile (1 or 2)
-  constexpr int LDA = BM == 128 ? GLD : 96, LDB = BN == 128 ? GLD : 96;   // both = 32 mod 64
-  __shared__ __attribute__((aligned(16))) float As[2][GBK][LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][GBK][LDB];
-  __shared__ float red[2][2][BN];
+  constexpr int BMV = BM * GBK / 1024, BNV = BN * GBK / 1024;   // float4s per thread of the A / B tile
+  constexpr int KCT = 256 / GBK, KCS = 4 * KCT;      // k-col role: threads per k row, column stride
+  // unpadded rows; odd k rows stored with column ^ 32 (sw()), so the two k rows one MFMA reads
+  // (lanes 0-31 / 32-63) sit on disjoint bank halves
+  __shared__ __attribute__((aligned(16))) float As[2][GBK][BM];
+  __shared__ __attribute__((aligned(16))) float Bs[2][GBK][BN];
+  auto sw = [](int k, int col) { return col ^ ((k & 1) << 5); };
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
   const int tiles_mn = p.tiles_m * p.tiles_n;
   const int split = blockIdx.x / tiles_mn, tl = blockIdx.x - split * tiles_mn;
@@ -294,17 +301,34 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
 
   const int ra_row = tid % BM, ra_k = (tid / BM) * (4 * BMV);          // A row-k: 4 * BMV k
   const int rb_row = tid % BN, rb_k = (tid / BN) * (4 * BNV);          // B row-k: 4 * BNV k
-  const int kc_k = tid >> 4, kc_c = (tid & 15) * 4;                    // k-col: cols kc_c (+ 64)
-  // tap walk (FWD / DGRAD): channel base and filter tap of the next K-step to load
+  const int kc_k = tid / KCT, kc_c = (tid % KCT) * 4;                 // k-col: cols kc_c + KCS * h
+  // tap walks (FWD / DGRAD): (channel, filter col, filter row) of the reduction index a thread loads
+  // next -- the A row-k chunk at k0 + ra_k, and (DGRAD) the B k-col row at k0 + kc_k.  A chunk of
+  // 4 * BMV <= 16 consecutive k stays inside one tap (FWD C % 16, DGRAD K % 16); a K-step may span
+  // several taps (C = 16 with BK = 32: the space-to-depth stem).
   const int CIN = MODE == F_FWD ? p.C : p.K;
-  int c0 = 0, ks = 0, kr = 0;
+  struct Walk { int c, s, r; };
+  auto walk_at = [&](int k) {
+    Walk w;
+    w.c = k % CIN;
+    const int rs = k / CIN;
+    w.s = rs % p.S;
+    w.r = rs / p.S;
+    return w;
+  };
+  auto walk_next = [&](Walk& w) {
+    w.c += GBK;
+    while (w.c >= CIN) {
+      w.c -= CIN;
+      if (++w.s == p.S) { w.s = 0; ++w.r; }
+    }
+  };
+  Walk wa{0, 0, 0}, wbk{0, 0, 0};
   int a_n = 0, a_y = 0, a_x = 0;
   bool a_ok = false;
   if constexpr (MODE != F_WGRAD) {
-    c0 = kbeg % CIN;
-    const int rs0 = kbeg / CIN;
-    ks = rs0 % p.S;
-    kr = rs0 / p.S;
+    wa = walk_at(kbeg + ra_k);
+    if constexpr (MODE == F_DGRAD) wbk = walk_at(kbeg + kc_k);
     const int m = m0 + ra_row;
     a_ok = m < p.gm;
     const int mm = a_ok ? m : 0;
@@ -326,7 +350,7 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
   if constexpr (MODE == F_WGRAD) {
 #pragma unroll
     for (int h = 0; h < BNV; ++h) {
-      const int j = n0 + kc_c + 64 * h;
+      const int j = n0 + kc_c + KCS * h;
       const int jj = j < p.gn ? j : 0;
       wb_c[h] = jj % p.C;
       const int rs = jj / p.C;
@@ -336,20 +360,40 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
   }
 
   float4 ra[BMV], rb[BNV];
+  // input fold (p.isc): channel base of the loaded x chunk(s) and which loads were in bounds; the
+  // BN + ReLU is applied at LDS-store time, when the data has arrived
+  int fold_ok = 0;
+  float4 fsc[MODE == F_FWD ? BMV : BNV], fsh[MODE == F_FWD ? BMV : BNV];   // fold coefficients
+  if (MODE == F_WGRAD && p.isc) {   // WGRAD: the B columns' channels are fixed per thread
+#pragma unroll
+    for (int h = 0; h < BNV; ++h) {
+      fsc[h] = ld4(p.isc + wb_c[h]);
+      fsh[h] = ld4(p.ish + wb_c[h]);
+    }
+  }
   auto load = [&](int k0) {
     if constexpr (MODE == F_FWD) {
-      const int y = a_y + kr, x = a_x + ks;
-      const bool ok = a_ok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-      const unsigned off = ok ? 4u * (unsigned)((((a_n * p.H + y) * p.W + x) * p.C) + c0 + ra_k) : F32_OOB;
+      const int y = a_y + wa.r, x = a_x + wa.s;
+      const bool kok = k0 + ra_k < kend;
+      const bool ok = a_ok && kok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+      const unsigned off = ok ? 4u * (unsigned)((((a_n * p.H + y) * p.W + x) * p.C) + wa.c) : F32_OOB;
 #pragma unroll
       for (int h = 0; h < BMV; ++h) ra[h] = bld4(rsA, off + 16 * h);
+      if (p.isc) {   // loaded with the data (in flight together), applied at LDS-store time
+        fold_ok = ok;
+#pragma unroll
+        for (int h = 0; h < BMV; ++h) {
+          fsc[h] = ld4(p.isc + wa.c + 4 * h);
+          fsh[h] = ld4(p.ish + wa.c + 4 * h);
+        }
+      }
       const int n = n0 + rb_row;
-      const unsigned offb = n < p.gn ? 4u * (unsigned)(n * p.gk + k0 + rb_k) : F32_OOB;
+      const unsigned offb = n < p.gn && k0 + rb_k < kend ? 4u * (unsigned)(n * p.gk + k0 + rb_k) : F32_OOB;
 #pragma unroll
       for (int h = 0; h < BNV; ++h) rb[h] = bld4(rsB, offb + 16 * h);
     } else if constexpr (MODE == F_DGRAD) {
-      const int ph = a_y - kr, pw = a_x - ks;
-      bool ok = a_ok && ph >= 0 && pw >= 0;
+      const int ph = a_y - wa.r, pw = a_x - wa.s;
+      bool ok = a_ok && k0 + ra_k < kend && ph >= 0 && pw >= 0;
       int py = ph, px = pw;
       if (p.stride != 1) {
         ok = ok && (ph % p.stride) == 0 && (pw % p.stride) == 0;
@@ -357,22 +401,23 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
         px = pw / p.stride;
       }
       ok = ok && py < p.P && px < p.Q;
-      const unsigned off = ok ? 4u * (unsigned)((((a_n * p.P + py) * p.Q + px) * p.K) + c0 + ra_k) : F32_OOB;
+      const unsigned off = ok ? 4u * (unsigned)((((a_n * p.P + py) * p.Q + px) * p.K) + wa.c) : F32_OOB;
 #pragma unroll
       for (int h = 0; h < BMV; ++h) ra[h] = bld4(rsA, off + 16 * h);
-      const int co = c0 + kc_k;   // B[k = (r, s, co)][c] = W[co][r][s][c]
-      const int wrow = ((co * p.R + kr) * p.S + ks) * p.C;
+      // B[k = (r, s, co)][c] = W[co][r][s][c]
+      const bool kokb = k0 + kc_k < kend;
+      const int wrow = ((wbk.c * p.R + wbk.r) * p.S + wbk.s) * p.C;
 #pragma unroll
       for (int h = 0; h < BNV; ++h) {
-        const int c = n0 + kc_c + 64 * h;
-        rb[h] = bld4(rsB, c < p.gn ? 4u * (unsigned)(wrow + c) : F32_OOB);
+        const int c = n0 + kc_c + KCS * h;
+        rb[h] = bld4(rsB, kokb && c < p.gn ? 4u * (unsigned)(wrow + c) : F32_OOB);
       }
     } else {
       const int m = k0 + kc_k;
       const bool mok = m < kend;
 #pragma unroll
       for (int h = 0; h < BMV; ++h) {
-        const int co = m0 + kc_c + 64 * h;
+        const int co = m0 + kc_c + KCS * h;
         ra[h] = bld4(rsA, mok && co < p.gm ? 4u * (unsigned)(m * p.K + co) : F32_OOB);
       }
       const int mm = mok ? m : 0;
@@ -380,39 +425,54 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
       const int rem = mm - n * p.P * p.Q;
       const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
       const int y0 = pp * p.stride, x0 = qq * p.stride;
+      fold_ok = 0;
 #pragma unroll
       for (int h = 0; h < BNV; ++h) {
         const int y = y0 + wb_y[h], x = x0 + wb_x[h];
         const bool okb = mok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
         rb[h] = bld4(rsB, okb ? 4u * (unsigned)(((n * p.H + y) * p.W + x) * p.C + wb_c[h]) : F32_OOB);
+        fold_ok |= okb << h;
       }
     }
-    if constexpr (MODE != F_WGRAD) {
-      c0 += GBK;
-      if (c0 >= CIN) {
-        c0 = 0;
-        if (++ks == p.S) { ks = 0; ++kr; }
-      }
-    }
+    if constexpr (MODE != F_WGRAD) walk_next(wa);
+    if constexpr (MODE == F_DGRAD) walk_next(wbk);
+  };
+  auto bnrelu = [](float4& v, const float4& a, const float4& b) {
+    v.x = fmaxf(fmaf(v.x, a.x, b.x), 0.f);
+    v.y = fmaxf(fmaf(v.y, a.y, b.y), 0.f);
+    v.z = fmaxf(fmaf(v.z, a.z, b.z), 0.f);
+    v.w = fmaxf(fmaf(v.w, a.w, b.w), 0.f);
   };
   auto store = [&](int buf) {
+    if (p.isc) {
+      if constexpr (MODE == F_FWD) {
+        if (fold_ok) {
+#pragma unroll
+          for (int h = 0; h < BMV; ++h) bnrelu(ra[h], fsc[h], fsh[h]);
+        }
+      } else if constexpr (MODE == F_WGRAD) {
+#pragma unroll
+        for (int h = 0; h < BNV; ++h)
+          if (fold_ok >> h & 1) bnrelu(rb[h], fsc[h], fsh[h]);
+      }
+    }
     if constexpr (MODE == F_WGRAD) {
 #pragma unroll
-      for (int h = 0; h < BMV; ++h) st4(&As[buf][kc_k][kc_c + 64 * h], ra[h]);
+      for (int h = 0; h < BMV; ++h) st4(&As[buf][kc_k][sw(kc_k, kc_c + KCS * h)], ra[h]);
     } else {
 #pragma unroll
       for (int h = 0; h < BMV; ++h)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) As[buf][ra_k + 4 * h + e][ra_row] = fget(ra[h], e);
+        for (int e = 0; e < 4; ++e) As[buf][ra_k + 4 * h + e][sw(e, ra_row)] = fget(ra[h], e);
     }
     if constexpr (MODE == F_FWD) {
 #pragma unroll
       for (int h = 0; h < BNV; ++h)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Bs[buf][rb_k + 4 * h + e][rb_row] = fget(rb[h], e);
+        for (int e = 0; e < 4; ++e) Bs[buf][rb_k + 4 * h + e][sw(e, rb_row)] = fget(rb[h], e);
     } else {
 #pragma unroll
-      for (int h = 0; h < BNV; ++h) st4(&Bs[buf][kc_k][kc_c + 64 * h], rb[h]);
+      for (int h = 0; h < BNV; ++h) st4(&Bs[buf][kc_k][sw(kc_k, kc_c + KCS * h)], rb[h]);
     }
   };
 
@@ -433,30 +493,28 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
       const int buf = t & 1;
       const bool nxt = t + 1 < nk;
       if (nxt) load(kbeg + (t + 1) * GBK);
-      float af[TM], bfv[TN], an[TM], bn[TN];
+      // LDS fragments in two register sets (ping-pong): the reads of step k2 + 1 are issued before
+      // the MFMAs of step k2
+      float fa[2][TM], fb[2][TN];
+      auto frag = [&](int set, int k2) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = As[buf][khalf][acol + 32 * i];
+        for (int i = 0; i < TM; ++i) fa[set][i] = As[buf][2 * k2 + khalf][(acol + 32 * i) ^ (khalf << 5)];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfv[j] = Bs[buf][khalf][bcol + 32 * j];
+        for (int j = 0; j < TN; ++j) fb[set][j] = Bs[buf][2 * k2 + khalf][(bcol + 32 * j) ^ (khalf << 5)];
+      };
+      frag(0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
       for (int k2 = 0; k2 < GBK / 2; ++k2) {
-        if (k2 + 1 < GBK / 2) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) an[i] = As[buf][2 * k2 + 2 + khalf][acol + 32 * i];
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bn[j] = Bs[buf][2 * k2 + 2 + khalf][bcol + 32 * j];
-        }
+        const int cur = k2 & 1;
+        if (k2 + 1 < GBK / 2) frag(cur ^ 1, k2 + 1);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
-        if (k2 + 1 < GBK / 2) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i) af[i] = an[i];
-#pragma unroll
-          for (int j = 0; j < TN; ++j) bfv[j] = bn[j];
-        }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
+        if (k2 + 1 < GBK / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
       }
       if (nxt) store(buf ^ 1);
       __syncthreads();
@@ -501,6 +559,7 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
         }
     }
     if (p.stats) {
+      float(*red)[2][BN] = reinterpret_cast<float(*)[2][BN]>(&As[0][0][0]);   // main loop is done
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         cs[j] += __shfl_xor(cs[j], 32, 64);
@@ -602,6 +661,7 @@ static void geometry(ConvP& p, int N, int H, int W, int C, int K, int R, int S, 
   p.P = (H + 2 * pad - R) / stride + 1;
   p.Q = (W + 2 * pad - S) / stride + 1;
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.relu = 0; p.raw = 0;
+  p.isc = nullptr; p.ish = nullptr;
 }
 
 // Launch plan of one fp32 conv GEMM.  The 32x32x2-MFMA kernel (igemm_f32_big_kernel) wherever its
@@ -626,8 +686,8 @@ template <int MODE>
 static F32Plan plan_f32(ConvP& p) {
   F32Plan pl{false, FBM, FBN, 1};
   bool ok = kn_f32_big.get() && p.a_bytes < (1u << 31) && p.b_bytes < (1u << 31);
-  if constexpr (MODE == F_FWD) ok = ok && p.C % GBK == 0;
-  if constexpr (MODE == F_DGRAD) ok = ok && p.K % GBK == 0;
+  if constexpr (MODE == F_FWD) ok = ok && p.C % 16 == 0;
+  if constexpr (MODE == F_DGRAD) ok = ok && p.K % 16 == 0;
   const int64_t target = std::max<int64_t>(1, kn_f32_blocks.get());
   auto tiles = [&] { return (int64_t)ceil_div(p.gm, pl.bm) * ceil_div(p.gn, pl.bn); };
   if (ok) {
@@ -695,9 +755,26 @@ static void check_f32(const at::Tensor& t, const char* what) {
               ": contiguous fp32 GPU tensor expected");
 }
 
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
+                    const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
+                    const c10::optional<at::Tensor>& shift2, bool relu, const c10::optional<at::Tensor>& mbits);
+
+// input fold: the 32x32x2 kernel applies it while staging; the 64x64 kernel gets the materialised
+// relu(x * in_scale + in_shift) instead
+static bool set_fold(ConvP& p, const at::Tensor* isc, const at::Tensor* ish) {
+  if (!isc) return false;
+  TORCH_CHECK(ish, "fp32 conv: in_shift required with in_scale");
+  check_f32(*isc, "fp32 conv in_scale");
+  check_f32(*ish, "fp32 conv in_shift");
+  TORCH_CHECK(isc->numel() == p.C && ish->numel() == p.C, "fp32 conv: in_scale / in_shift size");
+  p.isc = ptr<float>(*isc);
+  p.ish = ptr<float>(*ish);
+  return true;
+}
+
 std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
                                  const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
-                                 bool relu, bool want_stats) {
+                                 bool relu, bool want_stats, const at::Tensor* in_scale, const at::Tensor* in_shift) {
   check_f32(x, "conv_fwd(fp32) x");
   check_f32(w, "conv_fwd(fp32) w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(3) == x.size(3), "conv_fwd(fp32): NHWC x, KRSC w");
@@ -710,6 +787,10 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   p.a = ptr<float>(x); p.b = ptr<float>(w); p.out = ptr<float>(y);
   p.a_bytes = nbytes32(x); p.b_bytes = nbytes32(w);
   const F32Plan pl = plan_f32<F_FWD>(p);
+  if (set_fold(p, in_scale, in_shift) && !pl.big) {
+    at::Tensor xa = bn_apply(x, *in_scale, *in_shift, c10::nullopt, c10::nullopt, c10::nullopt, true, c10::nullopt);
+    return conv_fwd(xa, w, stride, pad, bias, resid, relu, want_stats);
+  }
   at::Tensor part;   // BN partials: one row pair per M tile (per SKR rows after a split)
   if (want_stats) part = at::empty({ceil_div(p.gm, pl.nsplit > 1 ? SKR : pl.bm), 2, K}, x.options());
   if (bias.has_value() && bias->defined()) { check_f32(*bias, "conv_fwd(fp32) bias"); p.bias = ptr<float>(*bias); }
@@ -748,7 +829,7 @@ at::Tensor conv_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int6
 }
 
 void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64_t R, int64_t S, int64_t stride,
-                int64_t pad, bool accumulate) {
+                int64_t pad, bool accumulate, const at::Tensor* in_scale, const at::Tensor* in_shift) {
   check_f32(dy, "conv_wgrad(fp32) dy");
   check_f32(x, "conv_wgrad(fp32) x");
   check_f32(out, "conv_wgrad(fp32) out");
@@ -762,6 +843,10 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   p.a = ptr<float>(dy); p.b = ptr<float>(x);
   p.a_bytes = nbytes32(dy); p.b_bytes = nbytes32(x);
   const F32Plan pl = plan_f32<F_WGRAD>(p);
+  if (set_fold(p, in_scale, in_shift) && !pl.big) {
+    at::Tensor xa = bn_apply(x, *in_scale, *in_shift, c10::nullopt, c10::nullopt, c10::nullopt, true, c10::nullopt);
+    return conv_wgrad(dy, xa, out, R, S, stride, pad, accumulate);
+  }
   if (pl.nsplit == 1 && !accumulate) {
     p.out = ptr<float>(out);
     launch<F_WGRAD>(p, pl);

@@ -112,8 +112,9 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
                                  const c10::optional<at::Tensor>& in_scale, const c10::optional<at::Tensor>& in_shift) {
   const bool fold = in_scale.has_value() && in_scale->defined();
   TORCH_CHECK(!fold || (in_shift.has_value() && in_shift->defined()), "conv_fwd: in_shift required with in_scale");
-  TORCH_CHECK(!fold || x.scalar_type() != at::kFloat, "conv_fwd: the input activation fold is bf16 only");
-  if (x.scalar_type() == at::kFloat) return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats);
+  if (x.scalar_type() == at::kFloat)
+    return f32::conv_fwd(x, w, stride, pad, bias, resid, relu, want_stats, fold ? &*in_scale : nullptr,
+                         fold ? &*in_shift : nullptr);
   return conv_fwd_impl(x, w, stride, pad, bias, resid, relu ? 1 : 0, want_stats, fold ? &*in_scale : nullptr,
                        fold ? &*in_shift : nullptr);
 }

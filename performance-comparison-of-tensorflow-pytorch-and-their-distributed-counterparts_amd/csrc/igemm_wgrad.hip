@@ -119,9 +119,10 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
                 const c10::optional<at::Tensor>& in_shift) {
   const bool fold = fold_x.has_value() && fold_x->defined();
   const bool afold = in_scale.has_value() && in_scale->defined();
-  TORCH_CHECK(!afold || dy.scalar_type() != at::kFloat, "conv_wgrad: the input activation fold is bf16 only");
   TORCH_CHECK(!fold || dy.scalar_type() != at::kFloat, "conv_wgrad: the BatchNorm-backward fold is bf16 only");
-  if (dy.scalar_type() == at::kFloat) return f32::conv_wgrad(dy, x, out, R, S, stride, pad, accumulate);
+  if (dy.scalar_type() == at::kFloat)
+    return f32::conv_wgrad(dy, x, out, R, S, stride, pad, accumulate, afold ? &*in_scale : nullptr,
+                           afold ? &*in_shift : nullptr);
   PCMP_CHECK_CUDA(dy); PCMP_CHECK_BF16(dy); PCMP_CHECK_BF16(x);
   PCMP_CHECK_CONTIG(dy); PCMP_CHECK_CONTIG(x); PCMP_CHECK_F32(out); PCMP_CHECK_CONTIG(out);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3), K = dy.size(3);

@@ -63,12 +63,18 @@ class _Act:
 
 
 def _act_fold_ok(L, z) -> bool:
-    """Should relu(BN(z)) feeding conv ``L`` stay folded?  GPU bf16, 1x1 stride-1 convs with C % 64 == 0,
-    and only the memory-bound shapes whose conv already runs on the register-staged kernel (short
-    reductions of layers 1-2: >= PCMP_ACT_FOLD_MINROWS rows, default 150k; ResNet-50 layer 2 at
-    B=256 has 200,704)."""
+    """Should relu(BN(z)) feeding conv ``L`` stay folded?  GPU bf16: 1x1 stride-1 convs with C % 64 ==
+    0, and only the memory-bound shapes whose conv already runs on the register-staged kernel (short
+    reductions of layers 1-2: >= PCMP_ACT_FOLD_MINROWS rows, default 150k; ResNet-50 layer 2 at B=256
+    has 200,704).  GPU fp32 only with PCMP_ACT_FOLD_F32=1 (every conv with C % 16 == 0): the fp32
+    kernel's staging fold costs more than the bn_apply pass it saves -- TL forward 8.75 -> 9.24 ms,
+    profiles/r5_f32_notes.txt."""
     import os
-    if os.environ.get("PCMP_ACT_FOLD", "1") == "0" or not (z.is_cuda and z.dtype == torch.bfloat16):
+    if os.environ.get("PCMP_ACT_FOLD", "1") == "0" or not z.is_cuda:
+        return False
+    if z.dtype == torch.float32:
+        return os.environ.get("PCMP_ACT_FOLD_F32", "0") == "1" and z.shape[-1] % 16 == 0
+    if z.dtype != torch.bfloat16:
         return False
     if not (L.R == 1 and L.S == 1 and L.stride == 1 and z.shape[-1] % 64 == 0 and z.shape[-1] <= 128):
         return False
@@ -279,7 +285,7 @@ def stem_s2d_wanted(device) -> bool:
 
 
 def stem_s2d_enabled(x, L) -> bool:
-    return (x.dtype == torch.bfloat16 and L.R == 7 and L.S == 7 and L.stride == 2 and
+    return (x.dtype in (torch.bfloat16, torch.float32) and L.R == 7 and L.S == 7 and L.stride == 2 and
             x.shape[-1] in (8, S2D_CH) and stem_s2d_wanted(x.device))
 
 

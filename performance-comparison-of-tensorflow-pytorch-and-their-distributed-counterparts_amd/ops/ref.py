@@ -388,7 +388,8 @@ def nchw_to_nhwc(x, cpad, scale, mean=None, stdv=None):
 
 def image_to_s2d(x, pad, scale, mean=None, stdv=None, nhwc=False):
     """Stem space-to-depth (csrc/elementwise.hip image_to_s2d_kernel):
-    S[n,i,j,(dy*2+dx)*4+c] = X[n,c,2i+dy-pad,2j+dx-pad] (zero outside / c >= Cin)."""
+    S[n,i,j,(dy*2+dx)*4+c] = X[n,c,2i+dy-pad,2j+dx-pad] (zero outside / c >= Cin); bf16 out, except
+    fp32 NHWC in -> fp32 out (the fp32 stem)."""
     if nhwc:
         h = x.float()[..., :4]
     else:
@@ -400,6 +401,8 @@ def image_to_s2d(x, pad, scale, mean=None, stdv=None, nhwc=False):
     Hs, Ws = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
     h = F.pad(h, (0, 4 - C, pad, 2 * Ws - W - pad, pad, 2 * Hs - H - pad))
     h = h.reshape(N, Hs, 2, Ws, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, Hs, Ws, 16)
+    if nhwc and x.dtype == torch.float32:   # fp32 path: fp32 out
+        return h.contiguous()
     return h.to(torch.bfloat16).contiguous()
 
 

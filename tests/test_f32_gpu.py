@@ -59,6 +59,8 @@ def f32_kernel(request):
     (16, 28, 28, 64, 64, 3, 1, 1),     # large grid (the default policy picks the 128x128 kernel)
     (9, 15, 15, 48, 80, 3, 2, 1),      # M / N tails, stride 2, C % 16 == 0, K % 16 == 0
     (7, 9, 9, 20, 36, 3, 1, 1),        # C % 16 != 0 and K % 16 != 0: FWD/DGRAD fall back, WGRAD big
+    (4, 23, 23, 16, 64, 4, 1, 0),      # s2d stem (C = 16: two taps per 32-deep K-step)
+    (6, 12, 12, 16, 48, 3, 1, 1),      # C = K = 16, 3x3: gk = 144 (a half K-step tail)
 ])
 def test_conv_fwd_dgrad_wgrad_f32(gpu, shape, f32_kernel):
     torch.manual_seed(0)
@@ -82,6 +84,31 @@ def test_conv_fwd_dgrad_wgrad_f32(gpu, shape, f32_kernel):
     rel_close(out, outr, 2e-4)
     _ops().conv_wgrad(dy, x, out, R, R, s, p, True)   # accumulate
     rel_close(out, 2 * outr, 2e-4)
+
+
+@pytest.mark.parametrize("shape", [
+    (4, 14, 14, 64, 128, 3, 1, 1),     # 3x3 pad 1: the padding ring must stay zero (not relu(shift))
+    (8, 28, 28, 128, 64, 1, 1, 0),     # 1x1
+    (4, 15, 15, 32, 64, 3, 2, 1),      # stride 2, M tail
+])
+def test_conv_input_fold_f32(gpu, shape, f32_kernel):
+    """conv_fwd / conv_wgrad reading relu(x * in_scale + in_shift) (the unmaterialised BN + ReLU of the
+    producer) == the reference on the materialised activation, on every launch plan (the 64x64
+    kernel materialises it itself)."""
+    torch.manual_seed(4)
+    N, H, W, C, K, R, s, p = shape
+    x = torch.randn(N, H, W, C, device=gpu)
+    w = torch.randn(K, R, R, C, device=gpu) * (2.0 / (R * R * C)) ** 0.5
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    y, st = _ops().conv_fwd(x, w, s, p, None, None, False, True, sc, sh)
+    yr, str_ = ref.conv_fwd(x, w, s, p, None, None, False, True, sc, sh)
+    rel_close(y, yr)
+    rel_close(st.sum(0), str_.sum(0))
+    dy = torch.randn_like(yr)
+    out, outr = torch.zeros(K, R, R, C, device=gpu), torch.zeros(K, R, R, C, device=gpu)
+    _ops().conv_wgrad(dy, x, out, R, R, s, p, False, None, None, sc, sh)
+    ref.conv_wgrad(dy, x, outr, R, R, s, p, False, None, None, sc, sh)
+    rel_close(out, outr, 2e-4)
 
 
 def test_conv_dgrad_bnr_f32(gpu, f32_kernel):

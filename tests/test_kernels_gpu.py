@@ -527,14 +527,17 @@ def test_pool3s2_specialised(gpu, H, W):
     close(partq.sum(0).nan_to_num(0.0), part1.sum(0).nan_to_num(0.0), rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("src", ["f32", "u8", "nhwc"])
+@pytest.mark.parametrize("src", ["f32", "u8", "nhwc", "nhwc_f32"])
 def test_image_to_s2d(gpu, src):
-    """Stem space-to-depth kernel == the PyTorch reference (NCHW f32 / u8 with scale, NHWC bf16)."""
+    """Stem space-to-depth kernel == the PyTorch reference (NCHW f32 / u8 with scale, NHWC bf16, NHWC
+    fp32 -> fp32 for the fp32 stem)."""
     torch.manual_seed(0)
     if src == "f32":
         x, scale, nhwc = torch.rand(3, 3, 37, 30, device=gpu), 1.0, False
     elif src == "u8":
         x, scale, nhwc = torch.randint(0, 256, (3, 3, 30, 37), device=gpu, dtype=torch.uint8), 1 / 255, False
+    elif src == "nhwc_f32":
+        x, scale, nhwc = torch.randn(3, 31, 36, 8, device=gpu), 1.0, True
     else:
         x, scale, nhwc = rnd(3, 31, 36, 8, dev=gpu), 1.0, True
     y = _ops().image_to_s2d(x, 3, scale, None, None, nhwc)

@@ -20,6 +20,7 @@
 #   suite        secondary workloads (tools/bench_suite.py, HIP only)
 #   bert         BERT text-path tests, GEMM / attention micro benchmarks, whole-step A/B (BVARIANTS)
 #   pmc-dgrad    PMC passes over the isolated layer-1 DGRAD + BN-reduce shape
+#   prof-f32     rocprofv3 kernel stats of the fp32 transfer-learning forward (B=64)
 #   f32          fp32 conv micro (tools/f32_conv_micro.py) + the reference-precision ResNet-50 rerun
 #                (pytorch_training_inference.py --dtype fp32: TL forward ms/step, batch-1 p50)
 set -o pipefail
@@ -92,6 +93,15 @@ task_prof_bert() {
   python tools/prof_summary.py gpurun_out/prof_bert --top 45 --step-kernel adam_flat --last-steps 4 > ${O}_prof_bert.txt
   find gpurun_out/prof_bert -name "*kernel_trace.csv" -delete
   sed -n '/per step over/,+12p' ${O}_prof_bert.txt
+}
+task_prof_f32() {   # fp32 transfer-learning forward (B=64): kernel stats over 10 forwards
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_f32 -o run -- \
+    python $R/tools/prof_target.py resnet50_f32_tl 10 > $R/gpurun_out/prof_f32.log 2>&1 || die prof-f32 $R/gpurun_out/prof_f32.log
+  cd $R
+  python tools/prof_summary.py gpurun_out/prof_f32 --top 40 --steps 10 --last-steps 0 > ${O}_prof_f32.txt
+  find gpurun_out/prof_f32 -name "*kernel_trace.csv" -delete
+  head -50 ${O}_prof_f32.txt
 }
 task_prof_infer() {
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_inf -o run -- \

@@ -1,5 +1,7 @@
 """Run N training steps of one secondary workload (for rocprofv3):
-python tools/prof_target.py bert|bert_graph|bilstm|resnet18 [steps]   (bert_graph: GraphedStep replays)"""
+python tools/prof_target.py bert|bert_graph|bilstm|resnet18|resnet50_f32_tl [steps]
+(bert_graph: GraphedStep replays; resnet50_f32_tl: the reference-precision transfer-learning forward,
+fp32, train-mode BatchNorm, batch 64 at 224^2, no gradient through the frozen backbone)"""
 import os
 import sys
 
@@ -27,6 +29,18 @@ if what in ("bert", "bert_graph", "bilstm"):
         m = BiLSTMClassifier().to(dev)
         st = make_state(m, "adamw", lr=1e-3, clip=1.0)
         loss_fn = lambda: cross_entropy(m.forward_logits(ids), y)  # noqa: E731
+elif what == "resnet50_f32_tl":
+    from pcmp.models.resnet import resnet50
+    from pcmp.ops import _lib
+    _lib.set_precision("fp32")
+    m = resnet50(10).to(dev).train()
+    x = torch.rand(64, 3, 224, 224, device=dev)
+    with torch.no_grad():
+        for _ in range(steps):
+            m.forward_logits(x)
+    torch.cuda.synchronize()
+    print("done", what, steps)
+    sys.exit(0)
 else:
     from pcmp.models.resnet import resnet18
     m = resnet18(1000).to(dev)
