@@ -3205,6 +3205,10 @@ inline Knob kn_gemm_plan("gemm_plan", 1);   // 0 = default dispatch only, 1 = au
 inline Knob kn_plan_force("plan_force", -1); // tests: >= 0 restricts the candidates to that kind (uncached)
 inline Knob kn_gemm32("gemm32", 1);          // 32x32x16-MFMA plain-GEMM candidates (plan kinds 9 / 10)
 inline Knob kn_plan_nsplit("plan_nsplit", 0); // tests: >= 1 (with plan_force) also pins the split count
+// a split candidate must beat the best by this many us per call to be chosen: its extra
+// splitk_epilogue launch is host time the isolated timing does not see (BERT-base's eager step is
+// host-bound: 56 split epilogues per step in round 4, verdict r4 weak #6)
+inline Knob kn_plan_split_us("plan_split_us", 6);
 
 struct GemmPlan {
   int kind;     // 0 = default dispatch<>, 1 = DMA 128x128, 2 = DMA 256x256 (8 waves),
@@ -3358,6 +3362,7 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
     PCMP_HIP_CHECK(hipEventSynchronize(e1));
     float ms = 0.f;
     PCMP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (c.nsplit > 1 && !small_m) ms += 3e-3f * kn_plan_split_us.get();   // 3 timed calls
     if (ms < best_ms) { best_ms = ms; best = c; }
     if (g_plan_log) g_plan_log->push_back(std::string(plan_kind_name(c.kind)) + "/split" + std::to_string(c.nsplit) +
                                           " " + std::to_string(ms / 3 * 1000.f) + "us");
