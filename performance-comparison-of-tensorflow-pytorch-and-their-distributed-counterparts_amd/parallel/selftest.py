@@ -109,6 +109,50 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     dist.destroy_process_group()
 
 
+def bucket_timeline_worker(rank, world, port, out, device="cpu"):
+    """Two-step data-parallel run with the per-bucket timeline on (tests/test_ddp_cpu.py,
+    tests/test_ddp_gpu.py): saves comm_report() plus whether average_buffers() made the per-rank
+    BatchNorm running means equal to their mean.  ``device='cuda'``: both ranks share cuda:0 and
+    all-reduce CUDA buckets over gloo (the one-GPU rehearsal of the comm-stream overlap)."""
+    from .. import optim
+    from ..utils.flat import FlatParams
+    from .ddp import DistributedDataParallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(0)
+    model = _build("resnet_syncbn", seed=rank).to(dev)      # plain per-rank BatchNorm (no SyncBN)
+    flat = FlatParams(model.parameters(), shadow_dtype=None if dev.type == "cpu" else torch.bfloat16)
+    ddp = DistributedDataParallel(model, flat, bucket_cap_mb=1.0, first_bucket_mb=0.25, last_bucket_mb=0.25)
+    opt = optim.SGD(flat, lr=0.01)
+    opt.set_grad_scale(ddp.grad_scale())
+    x, y = _batch("resnet_syncbn", 8, seed=10 + rank)       # different data per rank
+    x, y = x.to(dev), y.to(dev)
+    ddp.time_exposed(True)
+    for _ in range(2):
+        opt.zero_grad()
+        _loss(model, "resnet_syncbn", x, y).backward()
+        ddp.finish_gradient_sync()
+        opt.step()
+    rep = ddp.comm_report()
+    rm = [b.detach().cpu().clone() for n_, b in model.named_buffers() if "running_mean" in n_]
+    gathered = [None] * world
+    dist.all_gather_object(gathered, rm)
+    ddp.average_buffers()
+    after = [b.detach().cpu().clone() for n_, b in model.named_buffers() if "running_mean" in n_]
+    all_after = [None] * world
+    dist.all_gather_object(all_after, after)
+    mean_before = [sum(g[i] for g in gathered) / world for i in range(len(rm))]
+    torch.save({"rep": rep, "differ_before": any(not torch.equal(a, b) for a, b in zip(gathered[0], gathered[1])),
+                "equal_after": all(torch.equal(a, b) for a, b in zip(all_after[0], all_after[1])),
+                "is_mean": all(torch.allclose(a, m, rtol=1e-5, atol=1e-6) for a, m in zip(after, mean_before))},
+               os.path.join(out, f"tl{rank}.pt"))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
 def rccl_force_check(kind: str = "resnet18", grad_dtype: str = "fp32", steps: int = 3) -> dict:
     """One-GPU exercise of the RCCL data-parallel path (run in its own process).
 

@@ -146,48 +146,13 @@ def test_sync_autotune_gives_every_rank_rank0_plans(tmp_path, world):
         assert shared == [e for e in res[0]["after"] if "only" not in e]
 
 
-def _timeline_worker(rank, world, port, out):
-    import torch.distributed as dist
-    from pcmp import optim
-    from pcmp.parallel.ddp import DistributedDataParallel
-    from pcmp.parallel.selftest import _batch, _build, _loss
-    from pcmp.utils.flat import FlatParams
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    model = _build("resnet_syncbn", seed=rank)              # plain per-rank BatchNorm (no SyncBN)
-    flat = FlatParams(model.parameters(), shadow_dtype=None)
-    ddp = DistributedDataParallel(model, flat, bucket_cap_mb=1.0, first_bucket_mb=0.25, last_bucket_mb=0.25)
-    opt = optim.SGD(flat, lr=0.01)
-    opt.set_grad_scale(ddp.grad_scale())
-    x, y = _batch("resnet_syncbn", 8, seed=10 + rank)       # different data per rank
-    ddp.time_exposed(True)
-    for _ in range(2):
-        opt.zero_grad()
-        _loss(model, "resnet_syncbn", x, y).backward()
-        ddp.finish_gradient_sync()
-        opt.step()
-    rep = ddp.comm_report()
-    rm = [b.clone() for n_, b in model.named_buffers() if "running_mean" in n_]
-    gathered = [None] * world
-    dist.all_gather_object(gathered, rm)
-    ddp.average_buffers()
-    after = [b.clone() for n_, b in model.named_buffers() if "running_mean" in n_]
-    all_after = [None] * world
-    dist.all_gather_object(all_after, after)
-    mean_before = [sum(g[i] for g in gathered) / world for i in range(len(rm))]
-    torch.save({"rep": rep, "differ_before": any(not torch.equal(a, b) for a, b in zip(gathered[0], gathered[1])),
-                "equal_after": all(torch.equal(a, b) for a, b in zip(all_after[0], all_after[1])),
-                "is_mean": all(torch.allclose(a, m) for a, m in zip(after, mean_before))},
-               os.path.join(out, f"tl{rank}.pt"))
-    dist.destroy_process_group()
-
-
 def test_ddp_bucket_timeline_and_buffer_average(tmp_path):
     """comm_report's per-bucket timeline (launch / done vs end of backward, bytes): the first buckets
     are all-reduced while backward still runs; average_buffers gives every rank the mean BatchNorm
     running statistics before an evaluation (per-rank statistics diverge without SyncBN)."""
     os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
-    mp.spawn(_timeline_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    from pcmp.parallel.selftest import bucket_timeline_worker
+    mp.spawn(bucket_timeline_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
     for r in range(2):
         d = torch.load(tmp_path / f"tl{r}.pt", weights_only=True)
         tl = d["rep"]["bucket_timeline"]

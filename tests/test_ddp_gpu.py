@@ -35,6 +35,22 @@ def test_ddp_equivalence_on_gpu(gpu, tmp_path, kind):
         assert res["nbuckets"] >= 2
 
 
+def test_ddp_bucket_timeline_shared_gpu(gpu, tmp_path):
+    """Two ranks on cuda:0, CUDA buckets over gloo: the first buckets' all-reduces are launched from
+    the comm stream while backward still runs (negative launch time relative to the end of
+    backward in comm_report's bucket timeline), and average_buffers equalises the BN statistics."""
+    from pcmp.parallel.selftest import bucket_timeline_worker
+    os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
+    mp.spawn(bucket_timeline_worker, args=(2, _port(), str(tmp_path), "cuda"), nprocs=2, join=True)
+    for r in range(2):
+        d = torch.load(tmp_path / f"tl{r}.pt", weights_only=True)
+        tl = d["rep"]["bucket_timeline"]
+        assert len(tl) == d["rep"]["buckets"] >= 3, d["rep"]
+        assert tl[0]["launch_ms"] < 0, tl            # first bucket launched before backward ended
+        assert all(t["done_ms"] >= t["launch_ms"] and t["bytes"] > 0 for t in tl), tl
+        assert d["differ_before"] and d["equal_after"] and d["is_mean"], d
+
+
 def test_bench_two_ranks_shared_gpu(gpu):
     env = dict(os.environ, PCMP_DIST_BACKEND="gloo", PCMP_SHARED_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
