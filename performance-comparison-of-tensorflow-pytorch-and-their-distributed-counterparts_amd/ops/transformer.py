@@ -187,7 +187,7 @@ def _wgrad_bias(p, bias, dy, x):
             _wgrad(p, dy, x)
             if bias is not None:
                 emit_grad(bias, lambda o, acc: K.colsum(dy, o, acc))
-        _params.run_on_side(run, (dy, x))
+        _params.run_on_side(run, (dy, x), linear=True)
         return None, None
     gw = _wgrad(p, dy, x)
     gb = emit_grad(bias, lambda o, acc: K.colsum(dy, o, acc)) if bias is not None else None
@@ -219,7 +219,7 @@ class _SideBatch:
                 _wgrad(p, dy, x)
                 if bias is not None:
                     emit_grad(bias, lambda o, acc, dy=dy: K.colsum(dy, o, acc))
-        _params.run_on_side(run, tuple(self.keep))
+        _params.run_on_side(run, tuple(self.keep), linear=True)
         self.jobs, self.keep = [], []
 
 
