@@ -36,8 +36,6 @@ struct ConvP {
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, ksplit, tiles_m, tiles_n;
   int raw;                     // FWD / DGRAD split-K: write raw partials to out + split * gm * gn
-  const float* isc;            // FWD A / WGRAD B operand read as relu(x * isc + ish) (per channel C)
-  const float* ish;
   unsigned a_bytes, b_bytes;   // operand extents (the 128-row kernel's buffer loads; < 2^31)
 };
 
@@ -359,18 +357,9 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
     }
   }
 
+  // one K-step of operand loads in flight (a second register set -- two steps of load latency
+  // hidden -- measured slower: the conv set at B=64 4.95 -> 5.02 ms, TL forward 8.75 -> 9.08 ms)
   float4 ra[BMV], rb[BNV];
-  // input fold (p.isc): channel base of the loaded x chunk(s) and which loads were in bounds; the
-  // BN + ReLU is applied at LDS-store time, when the data has arrived
-  int fold_ok = 0;
-  float4 fsc[MODE == F_FWD ? BMV : BNV], fsh[MODE == F_FWD ? BMV : BNV];   // fold coefficients
-  if (MODE == F_WGRAD && p.isc) {   // WGRAD: the B columns' channels are fixed per thread
-#pragma unroll
-    for (int h = 0; h < BNV; ++h) {
-      fsc[h] = ld4(p.isc + wb_c[h]);
-      fsh[h] = ld4(p.ish + wb_c[h]);
-    }
-  }
   auto load = [&](int k0) {
     if constexpr (MODE == F_FWD) {
       const int y = a_y + wa.r, x = a_x + wa.s;
@@ -379,14 +368,6 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
       const unsigned off = ok ? 4u * (unsigned)((((a_n * p.H + y) * p.W + x) * p.C) + wa.c) : F32_OOB;
 #pragma unroll
       for (int h = 0; h < BMV; ++h) ra[h] = bld4(rsA, off + 16 * h);
-      if (p.isc) {   // loaded with the data (in flight together), applied at LDS-store time
-        fold_ok = ok;
-#pragma unroll
-        for (int h = 0; h < BMV; ++h) {
-          fsc[h] = ld4(p.isc + wa.c + 4 * h);
-          fsh[h] = ld4(p.ish + wa.c + 4 * h);
-        }
-      }
       const int n = n0 + rb_row;
       const unsigned offb = n < p.gn && k0 + rb_k < kend ? 4u * (unsigned)(n * p.gk + k0 + rb_k) : F32_OOB;
 #pragma unroll
@@ -425,37 +406,17 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
       const int rem = mm - n * p.P * p.Q;
       const int pp = rem / p.Q, qq = rem - (rem / p.Q) * p.Q;
       const int y0 = pp * p.stride, x0 = qq * p.stride;
-      fold_ok = 0;
 #pragma unroll
       for (int h = 0; h < BNV; ++h) {
         const int y = y0 + wb_y[h], x = x0 + wb_x[h];
         const bool okb = mok && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
         rb[h] = bld4(rsB, okb ? 4u * (unsigned)(((n * p.H + y) * p.W + x) * p.C + wb_c[h]) : F32_OOB);
-        fold_ok |= okb << h;
       }
     }
     if constexpr (MODE != F_WGRAD) walk_next(wa);
     if constexpr (MODE == F_DGRAD) walk_next(wbk);
   };
-  auto bnrelu = [](float4& v, const float4& a, const float4& b) {
-    v.x = fmaxf(fmaf(v.x, a.x, b.x), 0.f);
-    v.y = fmaxf(fmaf(v.y, a.y, b.y), 0.f);
-    v.z = fmaxf(fmaf(v.z, a.z, b.z), 0.f);
-    v.w = fmaxf(fmaf(v.w, a.w, b.w), 0.f);
-  };
   auto store = [&](int buf) {
-    if (p.isc) {
-      if constexpr (MODE == F_FWD) {
-        if (fold_ok) {
-#pragma unroll
-          for (int h = 0; h < BMV; ++h) bnrelu(ra[h], fsc[h], fsh[h]);
-        }
-      } else if constexpr (MODE == F_WGRAD) {
-#pragma unroll
-        for (int h = 0; h < BNV; ++h)
-          if (fold_ok >> h & 1) bnrelu(rb[h], fsc[h], fsh[h]);
-      }
-    }
     if constexpr (MODE == F_WGRAD) {
 #pragma unroll
       for (int h = 0; h < BMV; ++h) st4(&As[buf][kc_k][sw(kc_k, kc_c + KCS * h)], ra[h]);
@@ -661,7 +622,6 @@ static void geometry(ConvP& p, int N, int H, int W, int C, int K, int R, int S, 
   p.P = (H + 2 * pad - R) / stride + 1;
   p.Q = (W + 2 * pad - S) / stride + 1;
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.relu = 0; p.raw = 0;
-  p.isc = nullptr; p.ish = nullptr;
 }
 
 // Launch plan of one fp32 conv GEMM.  The 32x32x2-MFMA kernel (igemm_f32_big_kernel) wherever its
@@ -759,16 +719,15 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
                     const c10::optional<at::Tensor>& x2, const c10::optional<at::Tensor>& scale2,
                     const c10::optional<at::Tensor>& shift2, bool relu, const c10::optional<at::Tensor>& mbits);
 
-// input fold: the 32x32x2 kernel applies it while staging; the 64x64 kernel gets the materialised
-// relu(x * in_scale + in_shift) instead
-static bool set_fold(ConvP& p, const at::Tensor* isc, const at::Tensor* ish) {
+// input fold (in_scale / in_shift): the fp32 kernels read a materialised relu(x * in_scale +
+// in_shift).  A staging-time fold in the 32x32x2 kernel was measured slower than this bn_apply pass
+// (TL forward 8.75 -> 9.24 ms, profiles/r5_f32_notes.txt) and removed.
+static bool wants_fold(const ConvP& p, const at::Tensor* isc, const at::Tensor* ish) {
   if (!isc) return false;
   TORCH_CHECK(ish, "fp32 conv: in_shift required with in_scale");
   check_f32(*isc, "fp32 conv in_scale");
   check_f32(*ish, "fp32 conv in_shift");
   TORCH_CHECK(isc->numel() == p.C && ish->numel() == p.C, "fp32 conv: in_scale / in_shift size");
-  p.isc = ptr<float>(*isc);
-  p.ish = ptr<float>(*ish);
   return true;
 }
 
@@ -787,7 +746,7 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   p.a = ptr<float>(x); p.b = ptr<float>(w); p.out = ptr<float>(y);
   p.a_bytes = nbytes32(x); p.b_bytes = nbytes32(w);
   const F32Plan pl = plan_f32<F_FWD>(p);
-  if (set_fold(p, in_scale, in_shift) && !pl.big) {
+  if (wants_fold(p, in_scale, in_shift)) {
     at::Tensor xa = bn_apply(x, *in_scale, *in_shift, c10::nullopt, c10::nullopt, c10::nullopt, true, c10::nullopt);
     return conv_fwd(xa, w, stride, pad, bias, resid, relu, want_stats);
   }
@@ -843,7 +802,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
   p.a = ptr<float>(dy); p.b = ptr<float>(x);
   p.a_bytes = nbytes32(dy); p.b_bytes = nbytes32(x);
   const F32Plan pl = plan_f32<F_WGRAD>(p);
-  if (set_fold(p, in_scale, in_shift) && !pl.big) {
+  if (wants_fold(p, in_scale, in_shift)) {
     at::Tensor xa = bn_apply(x, *in_scale, *in_shift, c10::nullopt, c10::nullopt, c10::nullopt, true, c10::nullopt);
     return conv_wgrad(dy, xa, out, R, S, stride, pad, accumulate);
   }

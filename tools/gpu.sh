@@ -163,6 +163,20 @@ task_pmc_wgrad() {   # SHAPE=l3_3x3 ...: three passes (LDS, waits / MFMA, memory
   cd $R
   python tools/pmc_summary.py gpurun_out/pmcw/${sh}_p1 gpurun_out/pmcw/${sh}_p2 gpurun_out/pmcw/${sh}_p3 2>&1 | tail -40
 }
+task_pmc_f32() {   # SHAPE / MODE over tools/f32_pmc.py: two PMC passes (waits / LDS / VALU, MFMA busy)
+  mkdir -p $R/gpurun_out/pmcf; cd /tmp
+  local sh=${SHAPE:-l2_3x3}_${MODE:-fwd}
+  timeout -k 10 120 python -u $R/tools/f32_pmc.py > $R/gpurun_out/pmcf/${sh}_time.txt 2>&1 || die pmcf-time
+  cat $R/gpurun_out/pmcf/${sh}_time.txt
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS \
+    SQ_INSTS_LDS SQ_INSTS_VALU --kernel-trace --output-format csv -d $R/gpurun_out/pmcf/${sh}_p1 -o run -- \
+    python $R/tools/f32_pmc.py > $R/gpurun_out/pmcf/p1.log 2>&1 || die pmcf-p1 $R/gpurun_out/pmcf/p1.log
+  timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM_RD \
+    GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $R/gpurun_out/pmcf/${sh}_p2 -o run -- \
+    python $R/tools/f32_pmc.py > $R/gpurun_out/pmcf/p2.log 2>&1 || die pmcf-p2 $R/gpurun_out/pmcf/p2.log
+  cd $R
+  python tools/pmc_summary.py gpurun_out/pmcf/${sh}_p1 gpurun_out/pmcf/${sh}_p2 2>&1 | tail -40
+}
 task_f32() {
   timeout -k 10 300 python -u tools/f32_conv_micro.py ${F32B:-64} > ${O}_f32_micro.txt 2>&1 || die f32-micro ${O}_f32_micro.txt
   cat ${O}_f32_micro.txt

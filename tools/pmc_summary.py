@@ -13,7 +13,7 @@ for d in sys.argv[1:]:
                 name = r.get("Kernel_Name", r.get("Kernel-Name", "?"))
                 acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for name, ctrs in acc.items():
-    if "igemm" not in name and "bn_" not in name:
+    if "igemm" not in name and "bn_" not in name and "f32" not in name:
         continue
     print(name[:120])
     for k, v in sorted(ctrs.items()):
