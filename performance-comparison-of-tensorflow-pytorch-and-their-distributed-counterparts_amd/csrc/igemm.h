@@ -2499,22 +2499,12 @@ static void launch_cfg(IgemmParams& p, hipStream_t st) {
 // A/B knobs (torch.ops.pcmp.set_knob; tools/gemm_knob_ab.py)
 
 inline Knob kn_wgrad_wgs("wgrad_wgs", 0);   // > 0: fixed split-K workgroup target (side-stream WGRADs)
-static int igemm8_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("PCMP_IGEMM8");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
+inline Knob kn_igemm8("igemm8", 1);
+static int igemm8_mode() { return kn_igemm8.get(); }
 
-// minimum 256x256 tile count for the 8-wave kernel (PCMP_IGEMM8_MINTILES overrides, A/B runs)
-static int igemm8_min_tiles() {
-  static const int v = [] {
-    const char* e = std::getenv("PCMP_IGEMM8_MINTILES");
-    return e ? std::atoi(e) : 160;
-  }();
-  return v;
-}
+// minimum 256x256 tile count for the 8-wave kernel (knob igemm8_min_tiles, A/B runs)
+inline Knob kn_igemm8_min_tiles("igemm8_min_tiles", 160);
+static int igemm8_min_tiles() { return kn_igemm8_min_tiles.get(); }
 
 template <int MODE, int BM, int BN, int WM, int WN, int NTHR, int MINB>
 static void launch_dma(IgemmParams& p, hipStream_t st) {
@@ -2640,23 +2630,13 @@ static void launch_dma32(IgemmParams& p, hipStream_t st) {
 // 4-wave LDS-DMA kernel (2 blocks per CU) in place of the register-staged 4-wave kernel for the
 // FWD/DGRAD GEMMs with the block-uniform tap walk and >= 3 K-tiles (measured
 // profiles/r1_dma4_ab.txt: 3x3 layers 10-16 % faster, e.g. layer4 3x3 DGRAD 97 -> 84 us; GEMMs
-// of 2 K-tiles ran up to 9 % slower).  PCMP_DMA4=0 disables it (A/B runs); PCMP_DMA4_N64 picks
+// of 2 K-tiles ran up to 9 % slower).  Knob dma4 = 0 disables it (A/B runs); knob dma4_n64 picks
 // the narrow-output (gn <= 64) tile: 1 = 128x64 (2x2 waves of 64x32, the default: 6 % faster than
 // 256x64 on the layer1 3x3), 2 = 256x64 (4x1 waves of 64x64), 0 = register-staged kernel.
-static int dma4_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("PCMP_DMA4");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-static int dma4_n64() {
-  static const int v = [] {
-    const char* e = std::getenv("PCMP_DMA4_N64");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
+inline Knob kn_dma4("dma4", 1);
+inline Knob kn_dma4_n64("dma4_n64", 1);
+static int dma4_mode() { return kn_dma4.get(); }
+static int dma4_n64() { return kn_dma4_n64.get(); }
 // 0: register-staged kernel; 1: 128x128; 2: 128x64; 3: 256x64
 static int use_dma4(int mode, const IgemmParams& p) {
   if (!dma4_mode() || mode == MODE_WGRAD || p.nsplit != 1) return 0;
@@ -2798,13 +2778,10 @@ static int use_igemm8(int mode, const IgemmParams& p) {
 // WGRAD tiles with 64x64 wave tiles where one GEMM side is narrow: RSC <= 64 (gn) -> 256x64 with
 // the 4 waves along M; cout <= 64 (gm) -> 64x256 with the waves along N, only for the Cin=8 stem
 // (measured profiles/r1_wgrad_wide_ab.txt: stem -7 %, 1x1 64->256 -5 %, but the layer1 3x3 and
-// 1x1 256->64 WGRADs ran 5-16 % slower on 64x256).  PCMP_WG64=0 disables them (A/B runs).
+// 1x1 256->64 WGRADs ran 5-16 % slower on 64x256).  Knob wg64 = 0 disables them (A/B runs).
+inline Knob kn_wg64("wg64", 1);
 static int wgrad_wide(const IgemmParams& p) {
-  static const int v = [] {
-    const char* e = std::getenv("PCMP_WG64");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (!v) return 0;
+  if (!kn_wg64.get()) return 0;
   if (p.gm > 32 && p.gm <= 64 && p.gn >= 256 && (p.C == 8 || p.C == 16)) return 1;   // 64 x 256 (stem)
   if (p.gn > 32 && p.gn <= 64 && p.gm >= 256) return 2;   // 256 x 64
   return 0;
@@ -2825,15 +2802,12 @@ static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
 }
 
 // FWD/DGRAD grids of fewer 128x128 tiles than CUs (BERT-base's M=4096 token GEMMs with N=768:
-// 192 tiles) run 64x128 tiles instead: twice the workgroups, every CU busy.  PCMP_BM64_SMALLGRID=0
-// disables it (A/B runs).
+// 192 tiles) run 64x128 tiles instead: twice the workgroups, every CU busy.  Knob bm64_smallgrid =
+// 0 disables it (A/B runs).
+inline Knob kn_bm64_smallgrid("bm64_smallgrid", 1);
 static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
-  static const int v = [] {
-    const char* e = std::getenv("PCMP_BM64_SMALLGRID");
-    return e ? std::atoi(e) : 1;
-  }();
   if (!(mode != MODE_WGRAD && p.nsplit == 1 && p.gm > 64 && p.gn > 64)) return false;
-  return v && ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
+  return kn_bm64_smallgrid.get() && ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
 }
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)

@@ -5,6 +5,9 @@
 
 namespace pcmp {
 
+static Knob kn_fwd_split_target("fwd_split_target", 256);
+static Knob kn_fwd_split_mink("fwd_split_mink", 4);
+
 // x: [N,H,W,C] bf16, w: [K,R,S,C] bf16 -> y [N,P,Q,K] bf16.  Optional bias (f32 [K]), residual
 // (bf16 [N,P,Q,K]) and activation (act: IgemmParams::relu) fused; optional stats output
 // [tiles_m,2,K] f32 (returned).  act 2 (GELU) also returns the pre-activation u.
@@ -74,10 +77,10 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
   const int tiles = ceil_div(p.gm, BMsel) * ceil_div(p.gn, BNsel);
   const int ksteps = ceil_div(p.gk, BK);
   int nsplit = 1;
-  // PCMP_FWD_SPLIT_TARGET / PCMP_FWD_SPLIT_MINK: grid target and minimum K-steps per split (A/B-only knobs of
-  // the round-1 heuristic; numerics at high split counts are covered by the plan_force small-M tests)
-  static const int split_target = [] { const char* e = getenv("PCMP_FWD_SPLIT_TARGET"); return e ? std::max(1, atoi(e)) : 256; }();
-  static const int split_mink = [] { const char* e = getenv("PCMP_FWD_SPLIT_MINK"); return e ? std::max(1, atoi(e)) : 4; }();
+  // knobs fwd_split_target / fwd_split_mink: grid target and minimum K-steps per split (A/B-only knobs
+  // of the round-1 heuristic; numerics at high split counts are covered by the plan_force small-M tests)
+  const int split_target = std::max(1, kn_fwd_split_target.get());
+  const int split_mink = std::max(1, kn_fwd_split_mink.get());
   if (!want_stats && tiles < 128 && ksteps >= 8)
     nsplit = std::max(1, std::min({ceil_div(split_target, tiles), ksteps / split_mink, 32}));
   if (!want_stats && tiles < 128 && ksteps >= 8 && kn_gemm_plan.get()) {

@@ -30,6 +30,8 @@ __device__ __forceinline__ void stv8(__bf16* p, const float* v) {
   for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
   *reinterpret_cast<u16x8*>(p) = u;
 }
+static Knob kn_ln_blocks("ln_blocks", 256);
+static Knob kn_ln_rpb("ln_rpb", 8);
 static int egrid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256)); }
 
 // ------------------------------------------------------------------------------- LayerNorm
@@ -464,124 +466,6 @@ __device__ __forceinline__ float drop_scale(const AttnParams& p, int bh, int q, 
   return uniform01(dropout_seed(p.seed, p.salt), p.offset + idx) >= p.p_drop ? 1.f / (1.f - p.p_drop) : 0.f;
 }
 
-// stage rows [S][64] of a qkv section into LDS (row-major, padded) and optionally transposed
-__device__ __forceinline__ void stage_head(const __bf16* src, int ldsrc, int S, __bf16* dst, __bf16* dstT) {
-  for (int i = threadIdx.x; i < S * (AD / 8); i += blockDim.x) {
-    const int s = i / (AD / 8), c8 = i % (AD / 8);
-    const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)s * ldsrc + c8 * 8);
-    if (dst) *reinterpret_cast<uint4*>(dst + s * ADP + c8 * 8) = v;
-    if (dstT) {
-      const unsigned short* u = reinterpret_cast<const unsigned short*>(&v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) reinterpret_cast<unsigned short*>(dstT)[(c8 * 8 + e) * ASP + s] = u[e];
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) attention_fwd_kernel(const AttnParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-  const int S = p.S, D3 = 3 * p.D;
-  __bf16* sQ = reinterpret_cast<__bf16*>(smem);          // [S][ADP]
-  __bf16* sK = sQ + AS * ADP;                             // [S][ADP]
-  __bf16* sVt = sK + AS * ADP;                            // [AD][ASP]
-  __bf16* sP = sVt + AD * ASP;                            // [4 waves][32][ASP]
-  float* sMask = reinterpret_cast<float*>(sP + 4 * 32 * ASP);  // [S]
-  const __bf16* base = p.qkv + (size_t)b * S * D3 + h * AD;
-  stage_head(base, D3, S, sQ, nullptr);
-  stage_head(base + p.D, D3, S, sK, nullptr);
-  stage_head(base + 2 * p.D, D3, S, nullptr, sVt);
-  for (int s = threadIdx.x; s < S; s += blockDim.x)
-    sMask[s] = (p.ids && p.ids[(size_t)b * S + s] <= 0) ? -1e30f : 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int NT = S / 16;  // key tiles (<= 8)
-  {
-    const int q0 = w * 32;
-    const bool act = q0 < S;  // all waves reach the barrier below
-    f32x4 acc[2][8];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-    __bf16* P = sP + w * 32 * ASP;
-    if (act) {
-#pragma unroll
-    for (int kk = 0; kk < AD; kk += 32) {
-      const int k0 = kk + 8 * (lane >> 4);
-      bf16x8 a0 = frag_row(sQ, ADP, q0 + (lane & 15), k0), a1 = frag_row(sQ, ADP, q0 + 16 + (lane & 15), k0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < NT) {
-          const bf16x8 bb = frag_row(sK, ADP, j * 16 + (lane & 15), k0);
-          acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb, acc[0][j], 0, 0, 0);
-          acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb, acc[1][j], 0, 0, 0);
-        }
-    }
-    // softmax over keys for rows (i, e): row = q0 + 16i + 4*(lane>>4) + e ; key = 16j + (lane&15)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < NT) {
-            const float v = acc[i][j][e] * p.scale + sMask[j * 16 + (lane & 15)];
-            acc[i][j][e] = v;
-            mx = fmaxf(mx, v);
-          }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        float sum = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < NT) { const float ev = __expf(acc[i][j][e] - mx); acc[i][j][e] = ev; sum += ev; }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
-        const float inv = 1.f / sum;
-        const int rl = 16 * i + 4 * (lane >> 4) + e;
-        const int q = q0 + rl;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < NT) {
-            const int key = j * 16 + (lane & 15);
-            const float pv = acc[i][j][e] * inv * drop_scale(p, bh, q, key);
-            reinterpret_cast<unsigned short*>(P)[rl * ASP + key] = f2bf(pv);
-          }
-        if ((lane & 15) == 0) p.lse[(size_t)bh * S + q] = mx + __logf(sum);
-      }
-    }
-    __syncthreads();
-    if (!act) return;
-    // O[32][64] = P[32][S] V[S][64] ; B fragment from V^T rows
-    f32x4 o[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[i][j] = f32x4{0, 0, 0, 0};
-    for (int kk = 0; kk < S; kk += 32) {
-      const int k0 = kk + 8 * (lane >> 4);
-      const bf16x8 a0 = frag_row(P, ASP, lane & 15, k0), a1 = frag_row(P, ASP, 16 + (lane & 15), k0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bf16x8 bb = frag_row(sVt, ASP, j * 16 + (lane & 15), k0);
-        o[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb, o[0][j], 0, 0, 0);
-        o[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb, o[1][j], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = q0 + 16 * i + 4 * (lane >> 4) + e;
-          const int d = 16 * j + (lane & 15);
-          reinterpret_cast<unsigned short*>(p.out)[((size_t)b * S + q) * p.D + h * AD + d] = f2bf(o[i][j][e]);
-        }
-  }
-}
 
 
 // Forward, register-resident design (default): block = 4 waves x 16 queries of one (batch, head),
@@ -818,181 +702,6 @@ __global__ void __launch_bounds__(512) attention_bwd2_kernel(const AttnParams p)
   }
 }
 
-__global__ void __launch_bounds__(256) attention_bwd_kernel(const AttnParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-  const int S = p.S, D3 = 3 * p.D;
-  // Q, K, V, dO row-major; their transposed operands are read with frag_tr
-  __bf16* sQ = reinterpret_cast<__bf16*>(smem);   // [S][ADP]
-  __bf16* sK = sQ + AS * ADP;                      // [S][ADP]
-  __bf16* sV = sK + AS * ADP;                      // [S][ADP]
-  __bf16* sdO = sV + AS * ADP;                     // [S][ADP]
-  __bf16* sT = sdO + AS * ADP;                     // [S keys][ASP] : Pd^T then dS^T tiles (wave w: keys 32w..)
-  float* sL = reinterpret_cast<float*>(sT + AS * ASP);  // lse [S]
-  float* sDd = sL + AS;                                  // D [S]
-  float* sMask = sDd + AS;                               // [S]
-  const __bf16* base = p.qkv + (size_t)b * S * D3 + h * AD;
-  stage_head(base, D3, S, sQ, nullptr);
-  stage_head(base + p.D, D3, S, sK, nullptr);
-  stage_head(base + 2 * p.D, D3, S, sV, nullptr);
-  stage_head(p.dout + (size_t)b * S * p.D + h * AD, p.D, S, sdO, nullptr);
-  for (int s = threadIdx.x; s < S; s += blockDim.x) {
-    sL[s] = p.lse[(size_t)bh * S + s];
-    sMask[s] = (p.ids && p.ids[(size_t)b * S + s] <= 0) ? -1e30f : 0.f;
-    // D = rowsum(dO * O)
-    float acc = 0.f;
-    const __bf16* orow = p.o + ((size_t)b * S + s) * p.D + h * AD;
-    const __bf16* drow = p.dout + ((size_t)b * S + s) * p.D + h * AD;
-    for (int d = 0; d < AD; d += 8) {
-      float a[8], c[8];
-      ldv8(orow + d, a);
-      ldv8(drow + d, c);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc += a[e] * c[e];
-    }
-    sDd[s] = acc;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int NT = S / 16;
-  const int kw0 = w * 32;           // this wave's keys
-  const bool active = kw0 < S;
-  __bf16* T = sT + kw0 * ASP;       // [32 keys][ASP]
-  f32x4 dk[2][4], dv[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { dk[i][j] = f32x4{0, 0, 0, 0}; dv[i][j] = f32x4{0, 0, 0, 0}; }
-  f32x4 sacc[2][8], pacc[2][8];
-  if (active) {
-    // S^T[key][q] = K_w Q^T ; dP^T[key][q] = V_w dO^T
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { sacc[i][j] = f32x4{0, 0, 0, 0}; pacc[i][j] = f32x4{0, 0, 0, 0}; }
-#pragma unroll
-    for (int kk = 0; kk < AD; kk += 32) {
-      const int k0 = kk + 8 * (lane >> 4);
-      const bf16x8 ka0 = frag_row(sK, ADP, kw0 + (lane & 15), k0), ka1 = frag_row(sK, ADP, kw0 + 16 + (lane & 15), k0);
-      const bf16x8 va0 = frag_row(sV, ADP, kw0 + (lane & 15), k0), va1 = frag_row(sV, ADP, kw0 + 16 + (lane & 15), k0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < NT) {
-          const bf16x8 qb = frag_row(sQ, ADP, j * 16 + (lane & 15), k0);
-          const bf16x8 ob = frag_row(sdO, ADP, j * 16 + (lane & 15), k0);
-          sacc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka0, qb, sacc[0][j], 0, 0, 0);
-          sacc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka1, qb, sacc[1][j], 0, 0, 0);
-          pacc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va0, ob, pacc[0][j], 0, 0, 0);
-          pacc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va1, ob, pacc[1][j], 0, 0, 0);
-        }
-    }
-    // P^T = exp(S^T*scale + mask[key] - lse[q]); write Pd^T (dropout applied) to T; dS^T kept in sacc
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kl = 16 * i + 4 * (lane >> 4) + e;
-        const int key = kw0 + kl;
-        const float mk = sMask[key];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < NT) {
-            const int q = j * 16 + (lane & 15);
-            const float pr = __expf(sacc[i][j][e] * p.scale + mk - sL[q]);
-            const float ds = drop_scale(p, bh, q, key);
-            reinterpret_cast<unsigned short*>(T)[kl * ASP + q] = f2bf(pr * ds);
-            const float dP = pacc[i][j][e] * ds;
-            sacc[i][j][e] = pr * (dP - sDd[q]);  // dS^T (unscaled)
-          }
-      }
-    __builtin_amdgcn_s_waitcnt(0);
-  }
-  __syncthreads();
-  if (active) {
-    // dV[key][d] = sum_q Pd^T[key][q] dO[q][d]  : A = T rows (k = q), B from dO^T rows
-    for (int kk = 0; kk < S; kk += 32) {
-      const int k0 = kk + 8 * (lane >> 4);
-      const bf16x8 a0 = frag_row(T, ASP, lane & 15, k0), a1 = frag_row(T, ASP, 16 + (lane & 15), k0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bf16x8 bb = frag_tr(sdO, ADP, kk, j * 16);
-        dv[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb, dv[0][j], 0, 0, 0);
-        dv[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb, dv[1][j], 0, 0, 0);
-      }
-    }
-  }
-  __syncthreads();
-  if (active) {
-    // overwrite T with dS^T (bf16)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kl = 16 * i + 4 * (lane >> 4) + e;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < NT) reinterpret_cast<unsigned short*>(T)[kl * ASP + j * 16 + (lane & 15)] = f2bf(sacc[i][j][e]);
-      }
-  }
-  __syncthreads();
-  if (active) {
-    // dK[key][d] = sum_q dS^T[key][q] Q[q][d] * scale : A = T rows, B from Q^T rows
-    for (int kk = 0; kk < S; kk += 32) {
-      const int k0 = kk + 8 * (lane >> 4);
-      const bf16x8 a0 = frag_row(T, ASP, lane & 15, k0), a1 = frag_row(T, ASP, 16 + (lane & 15), k0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bf16x8 bb = frag_tr(sQ, ADP, kk, j * 16);
-        dk[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb, dk[0][j], 0, 0, 0);
-        dk[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb, dk[1][j], 0, 0, 0);
-      }
-    }
-    // write dK, dV
-    __bf16* dst = p.dqkv + (size_t)b * S * D3 + h * AD;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int key = kw0 + 16 * i + 4 * (lane >> 4) + e;
-          const int d = 16 * j + (lane & 15);
-          reinterpret_cast<unsigned short*>(dst)[(size_t)key * D3 + p.D + d] = f2bf(dk[i][j][e] * p.scale);
-          reinterpret_cast<unsigned short*>(dst)[(size_t)key * D3 + 2 * p.D + d] = f2bf(dv[i][j][e]);
-        }
-  }
-  // dQ[q][d] = sum_key dS[q][key] K[key][d] * scale ; wave w takes queries 32w.. ; A[q][key] = dS^T[key][q]
-  if (active) {
-    const int q0 = w * 32;
-    f32x4 dq[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dq[i][j] = f32x4{0, 0, 0, 0};
-    for (int kk = 0; kk < S; kk += 32) {
-      const bf16x8 a0 = frag_tr(sT, ASP, kk, q0), a1 = frag_tr(sT, ASP, kk, q0 + 16);
-      bf16x8 bb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bb[j] = frag_tr(sK, ADP, kk, j * 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        dq[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bb[j], dq[0][j], 0, 0, 0);
-        dq[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bb[j], dq[1][j], 0, 0, 0);
-      }
-    }
-    __bf16* dst = p.dqkv + (size_t)b * S * D3 + h * AD;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = q0 + 16 * i + 4 * (lane >> 4) + e;
-          const int d = 16 * j + (lane & 15);
-          reinterpret_cast<unsigned short*>(dst)[(size_t)q * D3 + d] = f2bf(dq[i][j][e] * p.scale);
-        }
-  }
-}
 
 // ------------------------------------------------------------------------------- host
 std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& r, const at::Tensor& g,
@@ -1009,8 +718,7 @@ std::vector<at::Tensor> layernorm_fwd(const at::Tensor& x, const c10::optional<a
   at::Tensor xs = (hr || p > 0.0) ? at::empty_like(x) : x;
   auto f32 = x.options().dtype(at::kFloat);
   auto mean = at::empty({M}, f32), rstd = at::empty({M}, f32);
-  static const bool v1 = [] { const char* e = std::getenv("PCMP_LN_FWD_V1"); return e && e[0] == '1'; }();
-  if (!v1 && D % 256 == 0 && D <= 1024) {
+  if (D % 256 == 0 && D <= 1024) {   // lane-dense kernel; the generic one below for other widths
     const __bf16* rp = hr ? ptr<__bf16>(*r) : nullptr;
     __bf16* xsp = (hr || p > 0.0) ? ptr<__bf16>(xs) : nullptr;
     const int64_t* sp = p > 0.0 ? salt_ptr(salt) : nullptr;
@@ -1089,17 +797,13 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& xs, const at::T
                          bool accumulate) {
   if (xs.scalar_type() == at::kFloat) return f32::layernorm_bwd(dy, xs, mean, rstd, g, dg, db, accumulate);
   const int D = xs.size(-1);
-  static const bool v1 = [] { const char* e = std::getenv("PCMP_LN_BWD_V1"); return e && e[0] == '1'; }();
-  if (!v1 && D % 256 == 0 && D <= 1024)   // the lane-dense kernel (no dropout, no bias output)
+  if (D % 256 == 0 && D <= 1024)   // the lane-dense kernel (no dropout, no bias output)
     return layernorm_bwd_fused(dy, xs, mean, rstd, g, dg, db, c10::nullopt, accumulate ? 3 : 0, 0.0, 0, 0,
                                c10::nullopt)[0];
   auto dyc = dy.contiguous();
   const int M = xs.numel() / D;
   auto dx = at::empty_like(xs);
-  static const int target_blocks = [] {   // PCMP_LN_BLOCKS overrides (A/B runs)
-    const char* e = std::getenv("PCMP_LN_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : 256;
-  }();
+  const int target_blocks = std::max(1, kn_ln_blocks.get());   // knob ln_blocks (A/B runs)
   const int rpb = std::max(4, ceil_div(M, target_blocks));
   const int T = ceil_div(M, rpb);
   auto part = at::empty({T, 2, D}, mean.options());
@@ -1153,10 +857,7 @@ std::vector<at::Tensor> layernorm_bwd_fused(const at::Tensor& dy, const at::Tens
     }
   }
   const int np = outs[2] ? 3 : 2;
-  static const int rpb = [] {   // PCMP_LN_RPB: rows per block (A/B runs)
-    const char* e = std::getenv("PCMP_LN_RPB");
-    return e ? std::max(4, std::atoi(e)) : 8;
-  }();
+  const int rpb = std::max(4, kn_ln_rpb.get());   // knob ln_rpb: rows per block (A/B runs)
   const int T = ceil_div(M, rpb);
   auto part = at::empty({T, np, D}, mean.options());
   auto st = cur_stream();
@@ -1219,8 +920,6 @@ at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b) {
   return y;
 }
 
-static size_t attn_fwd_smem() { return ((size_t)2 * AS * ADP + AD * ASP + 4 * 32 * ASP) * 2 + AS * 4; }
-static size_t attn_bwd_smem() { return ((size_t)4 * AS * ADP + AS * ASP) * 2 + 3 * AS * 4; }
 
 // qkv [B*S][3D] bf16 -> [ctx [B*S][D] bf16, lse [B*H][S] f32]
 std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& ids, int64_t B,
@@ -1239,18 +938,13 @@ std::vector<at::Tensor> attention_fwd(const at::Tensor& qkv, const c10::optional
   AttnParams p{ptr<__bf16>(qkv), idc.defined() ? idc.data_ptr<int64_t>() : nullptr, ptr<__bf16>(ctx), ptr<float>(lse),
                nullptr, nullptr, nullptr, (int)B, (int)S, (int)H, D, 0.125f, (float)p_drop, (uint64_t)seed,
                (uint64_t)offset, salt_ptr(salt)};
-  static const bool v1 = [] { const char* e = std::getenv("PCMP_ATTN_FWD_V1"); return e && e[0] == '1'; }();
   const int nt = (int)S / 16;
-  if (v1) {   // round-2 block-per-(batch, head) kernel (A/B runs)
-    hipLaunchKernelGGL(attention_fwd_kernel, dim3(B * H), dim3(256), attn_fwd_smem(), cur_stream(), p);
-  } else {
-    const dim3 grid((unsigned)(B * H * ((S + 63) / 64)));
-    switch (nt) {
-      case 2: hipLaunchKernelGGL(attention_fwd2_kernel<2>, grid, dim3(256), 0, cur_stream(), p); break;
-      case 4: hipLaunchKernelGGL(attention_fwd2_kernel<4>, grid, dim3(256), 0, cur_stream(), p); break;
-      case 6: hipLaunchKernelGGL(attention_fwd2_kernel<6>, grid, dim3(256), 0, cur_stream(), p); break;
-      default: hipLaunchKernelGGL(attention_fwd2_kernel<8>, grid, dim3(256), 0, cur_stream(), p); break;
-    }
+  const dim3 grid((unsigned)(B * H * ((S + 63) / 64)));
+  switch (nt) {
+    case 2: hipLaunchKernelGGL(attention_fwd2_kernel<2>, grid, dim3(256), 0, cur_stream(), p); break;
+    case 4: hipLaunchKernelGGL(attention_fwd2_kernel<4>, grid, dim3(256), 0, cur_stream(), p); break;
+    case 6: hipLaunchKernelGGL(attention_fwd2_kernel<6>, grid, dim3(256), 0, cur_stream(), p); break;
+    default: hipLaunchKernelGGL(attention_fwd2_kernel<8>, grid, dim3(256), 0, cur_stream(), p); break;
   }
   PCMP_LAUNCH_CHECK();
   return {ctx, lse};
@@ -1274,16 +968,11 @@ at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at
   AttnParams p{ptr<__bf16>(qkv), idc.defined() ? idc.data_ptr<int64_t>() : nullptr, nullptr, ptr<float>(lse),
                ptr<__bf16>(dc), ptr<__bf16>(ctx), ptr<__bf16>(dqkv), (int)B, (int)S, (int)H, D, 0.125f,
                (float)p_drop, (uint64_t)seed, (uint64_t)offset, salt_ptr(salt)};
-  static const bool v1 = [] { const char* e = std::getenv("PCMP_ATTN_BWD_V1"); return e && e[0] == '1'; }();
-  if (v1) {   // round-2 key-parallel 4-wave kernel (A/B runs)
-    hipLaunchKernelGGL(attention_bwd_kernel, dim3(B * H), dim3(256), attn_bwd_smem(), cur_stream(), p);
-  } else {
-    switch ((int)S / 16) {
-      case 2: hipLaunchKernelGGL(attention_bwd2_kernel<2>, dim3(B * H), dim3(128), 0, cur_stream(), p); break;
-      case 4: hipLaunchKernelGGL(attention_bwd2_kernel<4>, dim3(B * H), dim3(256), 0, cur_stream(), p); break;
-      case 6: hipLaunchKernelGGL(attention_bwd2_kernel<6>, dim3(B * H), dim3(384), 0, cur_stream(), p); break;
-      default: hipLaunchKernelGGL(attention_bwd2_kernel<8>, dim3(B * H), dim3(512), 0, cur_stream(), p); break;
-    }
+  switch ((int)S / 16) {
+    case 2: hipLaunchKernelGGL(attention_bwd2_kernel<2>, dim3(B * H), dim3(128), 0, cur_stream(), p); break;
+    case 4: hipLaunchKernelGGL(attention_bwd2_kernel<4>, dim3(B * H), dim3(256), 0, cur_stream(), p); break;
+    case 6: hipLaunchKernelGGL(attention_bwd2_kernel<6>, dim3(B * H), dim3(384), 0, cur_stream(), p); break;
+    default: hipLaunchKernelGGL(attention_bwd2_kernel<8>, dim3(B * H), dim3(512), 0, cur_stream(), p); break;
   }
   PCMP_LAUNCH_CHECK();
   return dqkv;

@@ -32,5 +32,5 @@ def bench(fn, iters=50):
     return (time.perf_counter() - t) / iters * 1e6
 
 
-print(f"blocks={os.environ.get('PCMP_LN_BLOCKS', 'default')} fwd {bench(lambda: ops.layernorm_fwd(x, r, g, b, 1e-12)):.1f} us  "
+print(f"blocks={torch.ops.pcmp.set_knob('ln_blocks', torch.ops.pcmp.set_knob('ln_blocks', 0))} fwd {bench(lambda: ops.layernorm_fwd(x, r, g, b, 1e-12)):.1f} us  "
       f"bwd {bench(lambda: ops.layernorm_bwd(dy, xs, mean, rstd, g, dg, db, False)):.1f} us")
