@@ -19,6 +19,7 @@
 #include "f32.h"
 
 #include <algorithm>
+#include <climits>
 
 namespace pcmp {
 namespace f32 {
@@ -1159,6 +1160,55 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const float* __restric
   }
 }
 
+// Vector form (C % 4, < 2^31 float4 outputs): thread = one output pixel x 4 channels, float4 loads,
+// 32-bit index math, the optional BN + ReLU coefficients loaded once per thread.  The same window
+// order and strict '>' as the scalar kernel, so values and argmax indices are identical.
+__global__ __launch_bounds__(256) void maxpool_fwd4_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                                                           const float* __restrict__ sf, float* __restrict__ y,
+                                                           uint8_t* __restrict__ idx, int total4, int H, int W,
+                                                           int C, int P, int Q, int k, int s, int pad) {
+  const int C4 = C / 4;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total4; t += gridDim.x * blockDim.x) {
+    const int c4 = t % C4;
+    int r = t / C4;
+    const int q = r % Q;
+    r /= Q;
+    const int pp = r % P;
+    const int n = r / P;
+    float4 a = make_float4(1.f, 1.f, 1.f, 1.f), b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (sc) {
+      a = ld4(sc + 4 * c4);
+      b = ld4(sf + 4 * c4);
+    }
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int bi[4] = {0, 0, 0, 0};
+    for (int i = 0; i < k; ++i) {
+      const int h = pp * s - pad + i;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int j = 0; j < k; ++j) {
+        const int w = q * s - pad + j;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float4 v = ld4(x + (((size_t)n * H + h) * W + w) * C + 4 * c4);
+        if (sc) {
+          v.x = fmaxf(v.x * a.x + b.x, 0.f);
+          v.y = fmaxf(v.y * a.y + b.y, 0.f);
+          v.z = fmaxf(v.z * a.z + b.z, 0.f);
+          v.w = fmaxf(v.w * a.w + b.w, 0.f);
+        }
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (e[u] > best[u]) { best[u] = e[u]; bi[u] = i * k + j; }
+      }
+    }
+    st4(y + (size_t)t * 4, make_float4(best[0], best[1], best[2], best[3]));
+    if (idx) {
+      const unsigned packed = (unsigned)bi[0] | ((unsigned)bi[1] << 8) | ((unsigned)bi[2] << 16) | ((unsigned)bi[3] << 24);
+      *reinterpret_cast<unsigned*>(idx + (size_t)t * 4) = packed;
+    }
+  }
+}
+
 std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t pad, bool want_idx,
                                     const c10::optional<at::Tensor>& scale, const c10::optional<at::Tensor>& shift) {
   check_f32(x, "maxpool_fwd(fp32)");
@@ -1168,7 +1218,12 @@ std::vector<at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, i
   at::Tensor idx;
   if (want_idx) idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
   const bool bn = scale.has_value() && scale->defined();
-  if (y.numel())
+  if (y.numel() && C % 4 == 0 && y.numel() / 4 < (int64_t)INT_MAX) {
+    const int total4 = (int)(y.numel() / 4);
+    hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3(grid_n(total4)), dim3(256), 0, cur_stream(), ptr<float>(x),
+                       bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr, ptr<float>(y),
+                       want_idx ? idx.data_ptr<uint8_t>() : nullptr, total4, H, W, C, P, Q, (int)k, (int)s, (int)pad);
+  } else if (y.numel())
     hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_n(y.numel())), dim3(256), 0, cur_stream(), ptr<float>(x),
                        bn ? ptr<float>(*scale) : nullptr, bn ? ptr<float>(*shift) : nullptr, ptr<float>(y),
                        want_idx ? idx.data_ptr<uint8_t>() : nullptr, N, H, W, C, P, Q, (int)k, (int)s, (int)pad);
