@@ -630,13 +630,22 @@ static void geometry(ConvP& p, int N, int H, int W, int C, int K, int R, int S, 
 // halved per dimension (N first, then M) while the grid has fewer than f32_blocks (256 = one per
 // CU) tiles -- or the dimension is <= 64; else the 64x64 16x16x4 kernel.  The reduction is split
 // (FWD / DGRAD: partials + splitk_epilogue_kernel, >= f32_split_steps (4) K-steps per split; WGRAD: partials +
-// splitk_sum_kernel, >= 32 K-steps per split, toward 512 blocks) while the grid is below that.
+// splitk_sum_kernel, >= 32 K-steps per split, toward f32_wgrad_blocks) while the grid is below that.
 // Batch-1 inference is the case this serves: layer-4 FWD has 8 tiles of 64 x 64 against 288
 // K-steps.  Knobs: f32_big = 0 (always the 64x64 kernel), f32_split = 0 (no FWD / DGRAD split).
 static Knob kn_f32_big("f32_big", 1);
 static Knob kn_f32_split("f32_split", 1);
 static Knob kn_f32_blocks("f32_blocks", 256);
 static Knob kn_f32_split_steps("f32_split_steps", 4);
+// FWD / DGRAD with <= f32_shortk K-steps (1x1 convs over <= 128 channels) take 64x64 tiles: a short
+// main loop cannot hide the operand latency at 2 blocks / CU, five 64x64 blocks / CU can
+// (l1 1x1 64->256 FWD 139 -> 116 us, 256->64 DGRAD 139 -> 113 us at B=64).  WGRAD splits toward
+// f32_wgrad_blocks workgroups (>= 32 K-steps per split; f32_wgrad_blocks_1x1 for 1x1 filters): the
+// long pixel reductions of the 3x3 layers ran 20-25 % faster at 64x64 x ~1800 blocks than at 540
+// (profiles/r5_f32_micro_rules.txt).
+static Knob kn_f32_shortk("f32_shortk", 4);
+static Knob kn_f32_wgrad_blocks("f32_wgrad_blocks", 2048);
+static Knob kn_f32_wgrad_blocks_1x1("f32_wgrad_blocks_1x1", 512);   // 1x1: 2048 ran 5-30 % slower
 
 struct F32Plan {
   bool big;
@@ -651,17 +660,21 @@ static F32Plan plan_f32(ConvP& p) {
   if constexpr (MODE == F_DGRAD) ok = ok && p.K % 16 == 0;
   const int64_t target = std::max<int64_t>(1, kn_f32_blocks.get());
   auto tiles = [&] { return (int64_t)ceil_div(p.gm, pl.bm) * ceil_div(p.gn, pl.bn); };
+  const int nk = ceil_div(p.gk, GBK);
+  const int64_t wtarget =
+      std::max<int64_t>(1, p.R * p.S > 1 ? kn_f32_wgrad_blocks.get() : kn_f32_wgrad_blocks_1x1.get());
   if (ok) {
     pl.big = true;
     pl.bm = p.gm <= 64 ? 64 : 128;
     pl.bn = p.gn <= 64 ? 64 : 128;
-    if (tiles() < target && pl.bn == 128) pl.bn = 64;
-    if (tiles() < target && pl.bm == 128) pl.bm = 64;
+    const bool shortk = MODE != F_WGRAD && nk <= kn_f32_shortk.get();
+    const int64_t tt = MODE == F_WGRAD ? wtarget : target;
+    if ((shortk || tiles() < tt) && pl.bn == 128) pl.bn = 64;
+    if ((shortk || tiles() < tt) && pl.bm == 128) pl.bm = 64;
   }
-  const int nk = ceil_div(p.gk, GBK);
   int ns = 1;
   if (MODE == F_WGRAD)
-    ns = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(2 * target, tiles()), ceil_div(nk, 32)));
+    ns = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(wtarget, tiles()), ceil_div(nk, 32)));
   else if (kn_f32_split.get() && tiles() < target)
     ns = (int)std::max<int64_t>(
         1, std::min<int64_t>(ceil_div(target, tiles()), nk / std::max(1, kn_f32_split_steps.get())));

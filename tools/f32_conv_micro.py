@@ -2,7 +2,7 @@
 64 at 224^2 by default): time per call and TF/s of FWD (+BN stats), DGRAD and WGRAD with the 128x128
 32x32x2-MFMA kernel (f32_big = 1) against the 64x64 16x16x4 kernel (f32_big = 0).
 
-Usage: python tools/f32_conv_micro.py [batch]
+Usage: python tools/f32_conv_micro.py [batch] [knob=value,...]   (second column: those knobs instead of f32_big=0)
 """
 import os
 import sys
@@ -16,6 +16,8 @@ from pcmp.ops import _lib  # noqa: E402
 assert _lib.load(), _lib.load_error()
 ops = torch.ops.pcmp
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+# optional "knob=value,knob=value": the second column times the 32x32x2 kernel with these knobs
+VARIANT = dict((k, int(v)) for k, v in (kv.split("=") for kv in sys.argv[2].split(","))) if len(sys.argv) > 2 else {}
 dev = torch.device("cuda")
 # name, H (input), C, K, R, stride, pad
 LAYERS = [
@@ -62,9 +64,15 @@ for name, H, C, K, R, s, p in LAYERS:
                      ("wgrad", lambda: ops.conv_wgrad(dy, x, dw, R, R, s, p, False))):
         res = []
         for big in (1, 0):
-            old = ops.set_knob("f32_big", big)
-            t = timed(fn)
-            ops.set_knob("f32_big", old)
+            if VARIANT and big == 0:   # second column: the 32x32x2 kernel under the VARIANT knobs instead
+                olds = {k: ops.set_knob(k, v) for k, v in VARIANT.items()}
+                t = timed(fn)
+                for k, v in olds.items():
+                    ops.set_knob(k, v)
+            else:
+                old = ops.set_knob("f32_big", big)
+                t = timed(fn)
+                ops.set_knob("f32_big", old)
             tot[big] += t
             res.append(f"{t:8.1f}us {flops / t / 1e6:5.0f}TF")
         row += f" | {mode} " + " ".join(res)
