@@ -978,9 +978,56 @@ at::Tensor attention_bwd(const at::Tensor& dctx, const at::Tensor& qkv, const at
   return dqkv;
 }
 
+// ---- fused BERT sublayer forwards: one op dispatch per post-LN sublayer (the eager step is host-
+// bound on slow hosts: every Python -> C++ op call costs ~10 us of enqueue, profiles/r5_bert_host.txt).
+// Same kernels and order as the op-by-op BertAttentionBlockFn / BertFFNBlockFn forwards
+// (ops/transformer.py); the dropout seeds / offsets come from the Python RNG as before.
+std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                                 const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& resid,
+                                 bool relu, bool want_stats, const c10::optional<at::Tensor>& in_scale,
+                                 const c10::optional<at::Tensor>& in_shift);
+std::vector<at::Tensor> linear_gelu_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias);
+
+static at::Tensor linear_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias) {
+  const int64_t M = x.size(0), C = x.size(1), N = w.size(0);
+  return conv_fwd(x.view({M, 1, 1, C}), w.view({N, 1, 1, C}), 1, 0, bias, c10::nullopt, false, false, c10::nullopt,
+                  c10::nullopt)[0].view({M, N});
+}
+
+// h1 = LayerNorm(h + dropout(attn_out(attention(qkv(h)))))  -> [h1, qkv, ctx, lse, xs, mean, rstd]
+std::vector<at::Tensor> bert_attn_fwd(const at::Tensor& h, const c10::optional<at::Tensor>& ids, const at::Tensor& wq,
+                                      const at::Tensor& bq, const at::Tensor& wo, const at::Tensor& bo,
+                                      const at::Tensor& g, const at::Tensor& b, int64_t B, int64_t S, int64_t H,
+                                      double p_attn, int64_t seed_a, int64_t off_a, double p_hid, int64_t seed_h,
+                                      int64_t off_h, double eps, const c10::optional<at::Tensor>& salt) {
+  at::Tensor qkv = linear_fwd(h, wq, bq);
+  auto at_ = attention_fwd(qkv, ids, B, S, H, p_attn, seed_a, off_a, salt);
+  at::Tensor a = linear_fwd(at_[0], wo, bo);
+  auto ln = layernorm_fwd(a, h, g, b, eps, p_hid, seed_h, off_h, salt);
+  return {ln[0], qkv, at_[0], at_[1], ln[1], ln[2], ln[3]};
+}
+
+// h2 = LayerNorm(h1 + dropout(ffn2(gelu(ffn1(h1)))))  -> [h2, g, u, xs, mean, rstd]
+std::vector<at::Tensor> bert_ffn_fwd(const at::Tensor& h1, const at::Tensor& w1, const at::Tensor& b1,
+                                     const at::Tensor& w2, const at::Tensor& b2, const at::Tensor& g,
+                                     const at::Tensor& b, double p_hid, int64_t seed_h, int64_t off_h, double eps,
+                                     const c10::optional<at::Tensor>& salt) {
+  auto gu = linear_gelu_fwd(h1, w1, b1);
+  at::Tensor f = linear_fwd(gu[0], w2, b2);
+  auto ln = layernorm_fwd(f, h1, g, b, eps, p_hid, seed_h, off_h, salt);
+  return {ln[0], gu[0], gu[1], ln[1], ln[2], ln[3]};
+}
+
 }  // namespace pcmp
 
 TORCH_LIBRARY_FRAGMENT(pcmp, m) {
+  m.def("bert_attn_fwd(Tensor h, Tensor? ids, Tensor wq, Tensor bq, Tensor wo, Tensor bo, Tensor g, Tensor b, int B, "
+        "int S, int H, float p_attn, int seed_a, int off_a, float p_hid, int seed_h, int off_h, float eps, "
+        "Tensor? salt=None) -> Tensor[]",
+        &pcmp::bert_attn_fwd);
+  m.def("bert_ffn_fwd(Tensor h1, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor g, Tensor b, float p_hid, "
+        "int seed_h, int off_h, float eps, Tensor? salt=None) -> Tensor[]",
+        &pcmp::bert_ffn_fwd);
   m.def("layernorm_fwd(Tensor x, Tensor? r, Tensor g, Tensor b, float eps, float p=0., int seed=0, int offset=0, "
         "Tensor? salt=None) -> Tensor[]", &pcmp::layernorm_fwd);
   m.def("layernorm_bwd_fused(Tensor dy, Tensor xs, Tensor mean, Tensor rstd, Tensor g, Tensor(a!)? dg, "

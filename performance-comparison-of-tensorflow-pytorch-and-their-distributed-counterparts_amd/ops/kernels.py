@@ -26,7 +26,7 @@ OP_NAMES = (
     "masked_mean_fwd", "masked_mean_bwd",
     "layernorm_fwd", "embed_layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd",
     "linear_gelu_fwd", "linear_dgrad_gelu", "attention_fwd", "attention_bwd", "tanh_fwd", "tanh_bwd", "add_bf16",
-    "topk_rows", "synth_images",
+    "topk_rows", "synth_images", "bert_attn_fwd", "bert_ffn_fwd",
 )
 
 

@@ -748,3 +748,30 @@ def synth_images(labels, color, freq, S, seed, noise):
     u = torch.from_numpy(u).view(B, C, S, S)
     x = 0.5 * color[y].float().cpu().view(B, C, 1, 1) + 0.25 * (pat.unsqueeze(1) + 1.0) * 0.5 + noise * u
     return x.clamp_(0.0, 1.0).to(labels.device)
+
+
+# ------------------------------------------------------------------------------ fused BERT sublayers
+def _linear(x, w, bias):
+    M, C = x.shape
+    N = w.shape[0]
+    return conv_fwd(x.reshape(M, 1, 1, C), w.reshape(N, 1, 1, C), 1, 0, bias)[0].reshape(M, N)
+
+
+def bert_attn_fwd(h, ids, wq, bq, wo, bo, g, b, B, S, H, p_attn, seed_a, off_a, p_hid, seed_h, off_h, eps,
+                  salt=None):
+    """csrc/transformer.hip bert_attn_fwd: [h1, qkv, ctx, lse, xs, mean, rstd] of
+    h1 = LayerNorm(h + dropout(attn_out(attention(qkv(h)))))."""
+    qkv = _linear(h, wq, bq)
+    ctx, lse = attention_fwd(qkv, ids, B, S, H, p_attn, seed_a, off_a, salt)
+    a = _linear(ctx, wo, bo)
+    y, xs, mean, rstd = layernorm_fwd(a, h, g, b, eps, p_hid, seed_h, off_h, salt)
+    return [y, qkv, ctx, lse, xs, mean, rstd]
+
+
+def bert_ffn_fwd(h1, w1, b1, w2, b2, g, b, p_hid, seed_h, off_h, eps, salt=None):
+    """csrc/transformer.hip bert_ffn_fwd: [h2, gelu(u), u, xs, mean, rstd] of
+    h2 = LayerNorm(h1 + dropout(ffn2(gelu(ffn1(h1)))))."""
+    gu, u = linear_gelu_fwd(h1, w1, b1)
+    f = _linear(gu, w2, b2)
+    y, xs, mean, rstd = layernorm_fwd(f, h1, g, b, eps, p_hid, seed_h, off_h, salt)
+    return [y, gu, u, xs, mean, rstd]

@@ -152,12 +152,6 @@ def attention(qkv, ids, B, S, H, p_drop=0.0):
 # Reference: BertLayer = BertAttention(BertSelfAttention + BertSelfOutput) + BertIntermediate +
 # BertOutput of the HF model the reference fine-tunes (pytorch_on_language_distr.py:151-161).
 
-def _gemm(x, w, bias):
-    M, C = x.shape
-    N = w.shape[0]
-    return K.conv_fwd(x.reshape(M, 1, 1, C), w.reshape(N, 1, 1, C), 1, 0, bias, None, False, False)[0].reshape(M, N)
-
-
 def _dgrad(dy, w, wt, resid=None):
     M, N = dy.shape
     C = w.shape[1]
@@ -223,14 +217,6 @@ class _SideBatch:
         self.jobs, self.keep = [], []
 
 
-def _ln_fwd(ctx, a, resid, gamma, beta, eps, p):
-    seed, off = dropout_rng.next(a.numel()) if p > 0 else (0, 0)
-    salt = dropout_rng.salt if p > 0 else None
-    y, xs, mean, rstd = K.layernorm_fwd(a, resid, gamma.detach(), beta.detach(), eps, p, seed, off, salt)
-    ctx.ln = (p, seed, off, salt)
-    return y, xs, mean, rstd
-
-
 def _ln_bwd(ctx, dy, xs, mean, rstd, gamma, beta, bias):
     """-> (dresid, dbranch); gamma / beta / the branch bias gradients emitted."""
     p, seed, off, salt = ctx.ln
@@ -250,14 +236,17 @@ class BertAttentionBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, ids, wqkv, bqkv, wo, bo, gamma, beta, B, S, H, p_attn, p_hid, eps):
+        # one native op for the four kernels (qkv GEMM, attention, out GEMM, dropout+residual+LN):
+        # one Python -> C++ dispatch per sublayer on the host-bound eager path
         dt = h.dtype
         wq, wo_c = compute_weight(wqkv, dt), compute_weight(wo, dt)
-        qkv = _gemm(h, wq, bqkv.detach().float())
         seed, off = dropout_rng.next(B * H * S * S) if p_attn > 0 else (0, 0)
-        salt = dropout_rng.salt if p_attn > 0 else None
-        out, lse = K.attention_fwd(qkv, ids, B, S, H, p_attn, seed, off, salt)
-        a = _gemm(out, wo_c, bo.detach().float())
-        y, xs, mean, rstd = _ln_fwd(ctx, a, h, gamma, beta, eps, p_hid)
+        seed_h, off_h = dropout_rng.next(h.numel()) if p_hid > 0 else (0, 0)
+        salt = dropout_rng.salt if (p_attn > 0 or p_hid > 0) else None
+        y, qkv, out, lse, xs, mean, rstd = K.bert_attn_fwd(
+            h.contiguous(), ids, wq, bqkv.detach().float(), wo_c, bo.detach().float(), gamma.detach(), beta.detach(),
+            B, S, H, p_attn, seed, off, p_hid, seed_h, off_h, eps, salt)
+        ctx.ln = (p_hid, seed_h, off_h, salt if p_hid > 0 else None)
         ctx.save_for_backward(h, qkv, out, lse, ids if ids is not None else torch.empty(0), xs, mean, rstd)
         ctx.attn = (B, S, H, p_attn, seed, off, ids is not None, salt)
         ctx.params = (wqkv, bqkv, wo, bo, gamma, beta)
@@ -289,9 +278,11 @@ class BertFFNBlockFn(torch.autograd.Function):
     def forward(ctx, h1, w1, b1, w2, b2, gamma, beta, p_hid, eps):
         dt = h1.dtype
         w1c, w2c = compute_weight(w1, dt), compute_weight(w2, dt)
-        g, u = K.linear_gelu_fwd(h1, w1c, b1.detach().float())
-        f = _gemm(g, w2c, b2.detach().float())
-        y, xs, mean, rstd = _ln_fwd(ctx, f, h1, gamma, beta, eps, p_hid)
+        seed_h, off_h = dropout_rng.next(h1.numel()) if p_hid > 0 else (0, 0)
+        salt = dropout_rng.salt if p_hid > 0 else None
+        y, g, u, xs, mean, rstd = K.bert_ffn_fwd(h1.contiguous(), w1c, b1.detach().float(), w2c, b2.detach().float(),
+                                                 gamma.detach(), beta.detach(), p_hid, seed_h, off_h, eps, salt)
+        ctx.ln = (p_hid, seed_h, off_h, salt)
         ctx.save_for_backward(h1, g, u, xs, mean, rstd)
         ctx.params = (w1, b1, w2, b2, gamma, beta)
         return y

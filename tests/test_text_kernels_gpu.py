@@ -272,6 +272,42 @@ def test_bert_fused_sublayers_native(gpu, monkeypatch):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bert_fused_sublayer_ops_match_op_sequence(gpu, dtype):
+    """bert_attn_fwd / bert_ffn_fwd (one native dispatch per sublayer) == the same kernels issued one op
+    at a time (Linear, attention, Linear, dropout + residual + LayerNorm; Linear+GELU, Linear, LN),
+    bitwise, with dropout on, in bf16 and fp32."""
+    torch.manual_seed(6)
+    B, S, H, D, F = 4, 128, 12, 768, 3072
+    M = B * S
+    o = ops()
+    h = (torch.randn(M, D, device=gpu) * 0.5).to(dtype)
+    ids = _ids(B, S, 1000, gpu, lens=[128, 90, 33, 5])
+    wq, bq = (torch.randn(3 * D, D, device=gpu) * 0.02).to(dtype), torch.randn(3 * D, device=gpu) * 0.02
+    wo, bo = (torch.randn(D, D, device=gpu) * 0.02).to(dtype), torch.randn(D, device=gpu) * 0.02
+    w1, b1 = (torch.randn(F, D, device=gpu) * 0.02).to(dtype), torch.randn(F, device=gpu) * 0.02
+    w2, b2 = (torch.randn(D, F, device=gpu) * 0.02).to(dtype), torch.randn(D, device=gpu) * 0.02
+    g, b = torch.rand(D, device=gpu) + 0.5, torch.randn(D, device=gpu) * 0.1
+
+    def lin(x, w, bias):
+        return o.conv_fwd(x.view(M, 1, 1, -1), w.view(w.shape[0], 1, 1, -1), 1, 0, bias, None, False, False)[0].view(M, -1)
+
+    fa = o.bert_attn_fwd(h, ids, wq, bq, wo, bo, g, b, B, S, H, 0.1, 11, 3 << 32, 0.1, 11, 4 << 32, 1e-12)
+    qkv = lin(h, wq, bq)
+    ctx, lse = o.attention_fwd(qkv, ids, B, S, H, 0.1, 11, 3 << 32)
+    y = o.layernorm_fwd(lin(ctx, wo, bo), h, g, b, 1e-12, 0.1, 11, 4 << 32)
+    for u, v in zip(fa, [y[0], qkv, ctx, lse] + list(y[1:])):
+        assert torch.equal(u, v)
+    h1 = fa[0]
+    ff = o.bert_ffn_fwd(h1, w1, b1, w2, b2, g, b, 0.1, 11, 5 << 32, 1e-12)
+    gu, uu = o.linear_gelu_fwd(h1, w1, b1)
+    y2 = o.layernorm_fwd(lin(gu, w2, b2), h1, g, b, 1e-12, 0.1, 11, 5 << 32)
+    for u, v in zip(ff, [y2[0], gu, uu] + list(y2[1:])):
+        assert torch.equal(u, v)
+    r = ref.bert_ffn_fwd(h1, w1, b1, w2, b2, g, b, 0.1, 11, 5 << 32, 1e-12)
+    close(ff[0], r[0], rtol=5e-2 if dtype == torch.bfloat16 else 1e-3, atol=5e-2 if dtype == torch.bfloat16 else 1e-3)
+
+
 def test_graphed_bert_step_matches_eager_without_dropout(gpu):
     """GraphedStep (whole training step as one hipGraph) == eager steps bitwise-close when dropout is
     off: same losses over 4 steps with AdamW + clipping + a linear LR schedule run between replays;
