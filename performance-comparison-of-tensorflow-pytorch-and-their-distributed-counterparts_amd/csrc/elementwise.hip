@@ -1149,6 +1149,29 @@ at::Tensor resize_image(const at::Tensor& x, int64_t Ho, int64_t Wo, int64_t mod
   return out;
 }
 
+// fp32 form for the fp32 (reference-precision) stem: NCHW f32 / u8 images -> [N, Hs, Ws, 16] fp32 in
+// one pass (no 8-channel NHWC intermediate)
+at::Tensor image_to_s2d_f32(const at::Tensor& x, int64_t pad, double scale) {
+  PCMP_CHECK_CUDA(x); PCMP_CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4 && x.size(1) <= 4 && pad >= 0, "image_to_s2d_f32: NCHW input, at most 4 channels");
+  const int N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int Hs = (H + 2 * pad + 1) / 2, Ws = (W + 2 * pad + 1) / 2;
+  auto y = at::empty({N, Hs, Ws, 16}, x.options().dtype(at::kFloat));
+  const int64_t total = (int64_t)N * Hs * Ws;
+  if (x.scalar_type() == at::kFloat) {
+    hipLaunchKernelGGL((image_to_s2d_kernel<float, false, float>), dim3(grid_for(total, 256, INT_MAX)), dim3(256), 0,
+                       cur_stream(), ptr<float>(x), ptr<float>(y), N, Cin, H, W, 0, Hs, Ws, (int)pad, (float)scale,
+                       nullptr, nullptr);
+  } else {
+    TORCH_CHECK(x.scalar_type() == at::kByte, "image_to_s2d_f32: f32 or u8 NCHW input");
+    hipLaunchKernelGGL((image_to_s2d_kernel<uint8_t, false, float>), dim3(grid_for(total, 256, INT_MAX)), dim3(256),
+                       0, cur_stream(), ptr<uint8_t>(x), ptr<float>(y), N, Cin, H, W, 0, Hs, Ws, (int)pad,
+                       (float)scale, nullptr, nullptr);
+  }
+  PCMP_LAUNCH_CHECK();
+  return y;
+}
+
 at::Tensor image_to_s2d(const at::Tensor& x, int64_t pad, double scale, const c10::optional<at::Tensor>& mean,
                         const c10::optional<at::Tensor>& stdv, bool nhwc) {
   PCMP_CHECK_CUDA(x); PCMP_CHECK_CONTIG(x);
@@ -1385,6 +1408,7 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("resize_image(Tensor x, int Ho, int Wo, int mode, int cpad, float scale, Tensor? mean, Tensor? stdv) -> Tensor",
         &pcmp::resize_image);
   m.def("image_to_s2d(Tensor x, int pad, float scale, Tensor? mean, Tensor? stdv, bool nhwc) -> Tensor", &pcmp::image_to_s2d);
+  m.def("image_to_s2d_f32(Tensor x, int pad, float scale) -> Tensor", &pcmp::image_to_s2d_f32);
   m.def("topk_rows(Tensor x, int k, bool want_values) -> Tensor[]", &pcmp::topk_rows);
   m.def("synth_images(Tensor labels, Tensor color, Tensor freq, int S, int seed, float noise) -> Tensor", &pcmp::synth_images);
 }

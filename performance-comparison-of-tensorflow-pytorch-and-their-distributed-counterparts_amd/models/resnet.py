@@ -140,7 +140,10 @@ class ResNet(nn.Module):
                 h = K.nchw_to_nhwc(x.contiguous(), STEM_CIN_PAD, scale, None, None)
         else:  # fp32 (the reference precision; CPU and --dtype fp32 on the GPU): no bf16 rounding
             scale = 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0
-            h = K.nchw_to_nhwc_f32(x.contiguous(), STEM_CIN_PAD, scale)
+            if x.shape[1] <= 4 and stem_s2d_wanted(x.device):
+                h = K.image_to_s2d_f32(x.contiguous(), self.stem.conv.pad, scale)   # fp32 s2d stem image
+            else:
+                h = K.nchw_to_nhwc_f32(x.contiguous(), STEM_CIN_PAD, scale)
         return h if h.dtype == dt else h.to(dt)
 
     # ---- forward ----------------------------------------------------------------------------

@@ -386,7 +386,12 @@ def nchw_to_nhwc(x, cpad, scale, mean=None, stdv=None):
     return y.to(torch.bfloat16).contiguous()
 
 
-def image_to_s2d(x, pad, scale, mean=None, stdv=None, nhwc=False):
+def image_to_s2d_f32(x, pad, scale):
+    """csrc/elementwise.hip image_to_s2d_f32: image_to_s2d of an NCHW f32 / u8 image, fp32 out."""
+    return image_to_s2d(x.float(), pad, scale, None, None, False, keep_f32=True)
+
+
+def image_to_s2d(x, pad, scale, mean=None, stdv=None, nhwc=False, keep_f32=False):
     """Stem space-to-depth (csrc/elementwise.hip image_to_s2d_kernel):
     S[n,i,j,(dy*2+dx)*4+c] = X[n,c,2i+dy-pad,2j+dx-pad] (zero outside / c >= Cin); bf16 out, except
     fp32 NHWC in -> fp32 out (the fp32 stem)."""
@@ -401,7 +406,7 @@ def image_to_s2d(x, pad, scale, mean=None, stdv=None, nhwc=False):
     Hs, Ws = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
     h = F.pad(h, (0, 4 - C, pad, 2 * Ws - W - pad, pad, 2 * Hs - H - pad))
     h = h.reshape(N, Hs, 2, Ws, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(N, Hs, Ws, 16)
-    if nhwc and x.dtype == torch.float32:   # fp32 path: fp32 out
+    if keep_f32 or (nhwc and x.dtype == torch.float32):   # fp32 path: fp32 out
         return h.contiguous()
     return h.to(torch.bfloat16).contiguous()
 

@@ -544,6 +544,11 @@ def test_image_to_s2d(gpu, src):
     yr = ref.image_to_s2d(x, 3, scale, None, None, nhwc)
     assert y.shape == yr.shape
     assert torch.equal(y, yr)
+    if not nhwc:   # the fp32 stem's one-pass form: NCHW f32 / u8 -> fp32 space-to-depth image
+        yf = _ops().image_to_s2d_f32(x, 3, scale)
+        yfr = ref.image_to_s2d_f32(x, 3, scale)
+        assert yf.dtype == torch.float32
+        torch.testing.assert_close(yf, yfr, rtol=1e-6, atol=1e-7)
 
 
 def test_splitk_fwd_repeated(gpu):
