@@ -1034,9 +1034,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
                                                        const float* __restrict__ sc2, const float* __restrict__ sf2,
                                                        int relu, float* __restrict__ y, uint8_t* __restrict__ bits,
                                                        int64_t n8, int C) {
+  // channel of the first element: 32-bit math (the host checks n8 < 2^31); C a power of two -> mask
+  const unsigned cmask = (C & (C - 1)) == 0 ? (unsigned)C - 1 : 0u;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const size_t off = (size_t)i * 8;
-    const int c = (int)(off % C);
+    const unsigned o32 = (unsigned)i * 8u;
+    const int c = (int)(cmask ? (o32 & cmask) : o32 % (unsigned)C);
     unsigned byte = 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1083,6 +1086,7 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
   }
   const int64_t n8 = x.numel() / 8;
   if (n8 == 0) return y;
+  TORCH_CHECK(x.numel() < (int64_t(1) << 32), "bn_apply(fp32): more than 2^32 elements");
   hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_n(n8)), dim3(256), 0, cur_stream(), ptr<float>(x), ptr<float>(scale),
                      ptr<float>(shift), px2, ps2, pf2, relu ? 1 : 0, ptr<float>(y), bits, n8, C);
   PCMP_LAUNCH_CHECK();
