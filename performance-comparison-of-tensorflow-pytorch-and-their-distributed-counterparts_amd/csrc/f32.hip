@@ -37,6 +37,8 @@ struct ConvP {
   int N, H, W, C, K, R, S, P, Q, stride, pad;
   int relu, ksplit, tiles_m, tiles_n;
   int raw;                     // FWD / DGRAD split-K: write raw partials to out + split * gm * gn
+  const float* isc;            // FWD (32x32x2 kernel): A operand read as relu(x * isc + ish) per channel
+  const float* ish;
   unsigned a_bytes, b_bytes;   // operand extents (the 128-row kernel's buffer loads; < 2^31)
 };
 
@@ -361,6 +363,12 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
   // one K-step of operand loads in flight (a second register set -- two steps of load latency
   // hidden -- measured slower: the conv set at B=64 4.95 -> 5.02 ms, TL forward 8.75 -> 9.08 ms)
   float4 ra[BMV], rb[BNV];
+  // input fold (FWD, p.isc): a wave's A chunk covers the same 4 * BMV channels for all its rows
+  // (ra_k is uniform per wave), so the BN coefficients are loaded once per wave from a
+  // readfirstlane'd (wave-uniform) channel index -- scalar loads, SGPR operands -- and applied at
+  // LDS-store time to the in-bounds rows (padding stays zero)
+  float4 fsc[BMV], fsh[BMV];
+  bool fold_ok = false;
   auto load = [&](int k0) {
     if constexpr (MODE == F_FWD) {
       const int y = a_y + wa.r, x = a_x + wa.s;
@@ -369,6 +377,15 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
       const unsigned off = ok ? 4u * (unsigned)((((a_n * p.H + y) * p.W + x) * p.C) + wa.c) : F32_OOB;
 #pragma unroll
       for (int h = 0; h < BMV; ++h) ra[h] = bld4(rsA, off + 16 * h);
+      if (p.isc) {
+        fold_ok = ok;
+        const int cu = __builtin_amdgcn_readfirstlane(wa.c);
+#pragma unroll
+        for (int h = 0; h < BMV; ++h) {
+          fsc[h] = ld4(p.isc + cu + 4 * h);
+          fsh[h] = ld4(p.ish + cu + 4 * h);
+        }
+      }
       const int n = n0 + rb_row;
       const unsigned offb = n < p.gn && k0 + rb_k < kend ? 4u * (unsigned)(n * p.gk + k0 + rb_k) : F32_OOB;
 #pragma unroll
@@ -418,6 +435,16 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
     if constexpr (MODE == F_DGRAD) walk_next(wbk);
   };
   auto store = [&](int buf) {
+    if (MODE == F_FWD && p.isc) {
+#pragma unroll
+      for (int h = 0; h < BMV; ++h) {
+        float4& v = ra[h];
+        v.x = fold_ok ? fmaxf(fmaf(v.x, fsc[h].x, fsh[h].x), 0.f) : 0.f;
+        v.y = fold_ok ? fmaxf(fmaf(v.y, fsc[h].y, fsh[h].y), 0.f) : 0.f;
+        v.z = fold_ok ? fmaxf(fmaf(v.z, fsc[h].z, fsh[h].z), 0.f) : 0.f;
+        v.w = fold_ok ? fmaxf(fmaf(v.w, fsc[h].w, fsh[h].w), 0.f) : 0.f;
+      }
+    }
     if constexpr (MODE == F_WGRAD) {
 #pragma unroll
       for (int h = 0; h < BMV; ++h) st4(&As[buf][kc_k][sw(kc_k, kc_c + KCS * h)], ra[h]);
@@ -623,6 +650,7 @@ static void geometry(ConvP& p, int N, int H, int W, int C, int K, int R, int S, 
   p.P = (H + 2 * pad - R) / stride + 1;
   p.Q = (W + 2 * pad - S) / stride + 1;
   p.bias = nullptr; p.resid = nullptr; p.stats = nullptr; p.relu = 0; p.raw = 0;
+  p.isc = nullptr; p.ish = nullptr;
 }
 
 // Launch plan of one fp32 conv GEMM.  The 32x32x2-MFMA kernel (igemm_f32_big_kernel) wherever its
@@ -736,6 +764,7 @@ at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tens
 // input fold (in_scale / in_shift): the fp32 kernels read a materialised relu(x * in_scale +
 // in_shift).  A staging-time fold in the 32x32x2 kernel was measured slower than this bn_apply pass
 // (TL forward 8.75 -> 9.24 ms, profiles/r5_f32_notes.txt) and removed.
+static Knob kn_f32_fold("f32_fold", 1);   // 0: always materialise the folded activation (A/B)
 static bool wants_fold(const ConvP& p, const at::Tensor* isc, const at::Tensor* ish) {
   if (!isc) return false;
   TORCH_CHECK(ish, "fp32 conv: in_shift required with in_scale");
@@ -760,7 +789,10 @@ std::vector<at::Tensor> conv_fwd(const at::Tensor& x, const at::Tensor& w, int64
   p.a = ptr<float>(x); p.b = ptr<float>(w); p.out = ptr<float>(y);
   p.a_bytes = nbytes32(x); p.b_bytes = nbytes32(w);
   const F32Plan pl = plan_f32<F_FWD>(p);
-  if (wants_fold(p, in_scale, in_shift)) {
+  if (wants_fold(p, in_scale, in_shift) && pl.big && kn_f32_fold.get()) {
+    p.isc = ptr<float>(*in_scale);
+    p.ish = ptr<float>(*in_shift);
+  } else if (wants_fold(p, in_scale, in_shift)) {
     at::Tensor xa = bn_apply(x, *in_scale, *in_shift, c10::nullopt, c10::nullopt, c10::nullopt, true, c10::nullopt);
     return conv_fwd(xa, w, stride, pad, bias, resid, relu, want_stats);
   }
