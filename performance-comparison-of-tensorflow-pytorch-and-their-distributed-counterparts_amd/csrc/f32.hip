@@ -263,12 +263,16 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const ConvP p) {
 // transposed; a wave writes 64 consecutive rows of one k -> conflict-free) and k-col (B of DGRAD,
 // A and B of WGRAD: 256 / BK threads per k row).  LDS rows are unpadded; odd k rows are stored with
 // column ^ 32, so the two k rows one MFMA reads (lanes 0-31 / 32-63) sit on disjoint bank halves
-// (64 KB at 128x128: 2 blocks / CU).  Optional FWD input fold (BN + ReLU of the producer, scalar-
+// (one stage -- F32_NBUF -- of 32 KB at 128x128: 3 blocks / CU, two barriers per K-step; the
+// double-buffered form ran the conv set at 4.72 vs 4.52 ms, profiles/r5_f32_nbuf*_micro.txt).  Optional FWD input fold (BN + ReLU of the producer, scalar-
 // loaded coefficients).  Epilogue on the 32x32 accumulator: lane = output column, register r -> row
 // 8 * (r / 4) + 4 * (lane / 32) + r % 4 -> 128-B row segments per store and in-lane BN sums; split-K
 // partials (p.raw) go to a workspace reduced by splitk_epilogue_kernel / splitk_sum_kernel.
 #ifndef F32_BK
 #define F32_BK 32
+#endif
+#ifndef F32_NBUF
+#define F32_NBUF 1   // one LDS stage: 32 KB at 128x128 -> 3 blocks / CU; 2 stages measured 4 % slower
 #endif
 constexpr int GBK = F32_BK;
 constexpr unsigned F32_OOB = 0x80000000u;   // buffer offset past num_records: the load returns 0
@@ -289,8 +293,9 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
   constexpr int KCT = 256 / GBK, KCS = 4 * KCT;      // k-col role: threads per k row, column stride
   // unpadded rows; odd k rows stored with column ^ 32 (sw()), so the two k rows one MFMA reads
   // (lanes 0-31 / 32-63) sit on disjoint bank halves
-  __shared__ __attribute__((aligned(16))) float As[2][GBK][BM];
-  __shared__ __attribute__((aligned(16))) float Bs[2][GBK][BN];
+  // F32_NBUF = 1 (compile-time A/B): one LDS stage, two barriers per K-step, half the LDS
+  __shared__ __attribute__((aligned(16))) float As[F32_NBUF][GBK][BM];
+  __shared__ __attribute__((aligned(16))) float Bs[F32_NBUF][GBK][BN];
   auto sw = [](int k, int col) { return col ^ ((k & 1) << 5); };
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, wr = wid >> 1, wc = wid & 1;
   const int tiles_mn = p.tiles_m * p.tiles_n;
@@ -480,7 +485,7 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
     store(0);
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
+      const int buf = F32_NBUF == 2 ? (t & 1) : 0;
       const bool nxt = t + 1 < nk;
       if (nxt) load(kbeg + (t + 1) * GBK);
       // LDS fragments in two register sets (ping-pong): the reads of step k2 + 1 are issued before
@@ -506,7 +511,8 @@ __global__ __launch_bounds__(256) void igemm_f32_big_kernel(const ConvP p) {
         if (k2 + 1 < GBK / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
       }
-      if (nxt) store(buf ^ 1);
+      if (F32_NBUF == 1 && nxt) __syncthreads();   // every wave is done reading the single stage
+      if (nxt) store(F32_NBUF == 2 ? buf ^ 1 : 0);
       __syncthreads();
     }
   }

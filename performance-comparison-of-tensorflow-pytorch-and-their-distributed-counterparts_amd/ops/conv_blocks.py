@@ -66,15 +66,16 @@ def _act_fold_ok(L, z) -> bool:
     """Should relu(BN(z)) feeding conv ``L`` stay folded?  GPU bf16: 1x1 stride-1 convs with C % 64 ==
     0, and only the memory-bound shapes whose conv already runs on the register-staged kernel (short
     reductions of layers 1-2: >= PCMP_ACT_FOLD_MINROWS rows, default 150k; ResNet-50 layer 2 at B=256
-    has 200,704).  GPU fp32: every conv with C % 16 == 0 (PCMP_ACT_FOLD_F32=0 disables): the fp32
-    32x32x2 kernel applies relu(scale * z + shift) to its A operand while staging it, the BN
-    coefficients read once per wave with scalar loads -- TL forward -0.1 ms (8.58 -> 8.47-8.51,
-    profiles/r5_f32_notes.txt); its WGRAD materialises the activation."""
+    has 200,704).  GPU fp32 only with PCMP_ACT_FOLD_F32=1 (every conv with C % 16 == 0): the fp32
+    32x32x2 kernel then applies relu(scale * z + shift) to its A operand while staging it (BN
+    coefficients read once per wave with scalar loads).  With the single-stage LDS main loop the
+    staging sits between the two barriers of a K-step and the fold loses: TL forward 8.41 ms off vs
+    8.90 ms on, same box (profiles/r5_f32_nbuf_fold_tl_ab.txt)."""
     import os
     if os.environ.get("PCMP_ACT_FOLD", "1") == "0" or not z.is_cuda:
         return False
     if z.dtype == torch.float32:
-        return os.environ.get("PCMP_ACT_FOLD_F32", "1") != "0" and z.shape[-1] % 16 == 0
+        return os.environ.get("PCMP_ACT_FOLD_F32", "0") == "1" and z.shape[-1] % 16 == 0
     if z.dtype != torch.bfloat16:
         return False
     if not (L.R == 1 and L.S == 1 and L.stride == 1 and z.shape[-1] % 64 == 0 and z.shape[-1] <= 128):
