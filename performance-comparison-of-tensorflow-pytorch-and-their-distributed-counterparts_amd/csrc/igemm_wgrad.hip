@@ -2,6 +2,7 @@
 // Kernels, launchers, dispatch and the GEMM planner live in igemm.h; this translation unit holds the
 // WGRAD entry points (split from igemm.hip in round 4 so the three modes compile in parallel).
 #include "igemm.h"
+#include "wgrad32.h"
 
 namespace pcmp {
 
@@ -13,17 +14,19 @@ static void wgrad_run(IgemmParams p, int nsplit, float* out, bool accumulate, co
   nsplit = ceil_div(ksteps, steps_per);
   p.ksplit = steps_per * BK;
   p.nsplit = nsplit;
+  const bool dma32 = use_wgrad_dma32(p);
   if (nsplit == 1) {
     p.out = out;
     p.accumulate = accumulate;
-    dispatch<MODE_WGRAD>(p, st);
+    if (dma32) launch_wgrad_dma32(p, st); else dispatch<MODE_WGRAD>(p, st);
     return;
   }
   const int64_t n = (int64_t)p.gm * p.gn;
   TORCH_CHECK(n % 4 == 0, "conv_wgrad: numel % 4");
   auto ws = at::empty({(int64_t)nsplit, n}, fopts);
   p.out = ws.data_ptr();
-  dispatch<MODE_WGRAD>(p, st);
+  p.accumulate = 0;
+  if (dma32) launch_wgrad_dma32(p, st); else dispatch<MODE_WGRAD>(p, st);
   if (n / 4 < (1ll << 31)) {
     const int n4 = (int)(n / 4);
     const int SL = nsplit <= 8 ? 1 : (nsplit <= 32 ? 4 : 16);
@@ -73,8 +76,8 @@ static int wgrad_nsplit(const IgemmParams& p, int tiles, const at::TensorOptions
   auto& mu = g_plan_mu;
   auto& cache = g_wsplit_cache;
   char key[160];
-  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
-           cap);
+  snprintf(key, sizeof(key), "%d,%d,%d,%d,%d,%d,%d,%d,%d,%d%s", p.N, p.H, p.W, p.C, p.K, p.R, p.S, p.stride, p.pad,
+           cap, use_wgrad_dma32(p) ? ",d32" : "");
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = cache.find(key);
@@ -150,7 +153,7 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
     p.act_sc = ptr<float>(*in_scale); p.act_sh = ptr<float>(*in_shift);
   }
   int BM, BN;
-  wgrad_tile(p, BM, BN);
+  if (use_wgrad_dma32(p)) wgrad_dma32_tile(p, BM, BN); else wgrad_tile(p, BM, BN);
   const int tiles = ceil_div(p.gm, BM) * ceil_div(p.gn, BN);
   auto st = cur_stream();
   const int nsplit = wgrad_nsplit(p, tiles, out.options(), st);
