@@ -58,7 +58,10 @@ def _local_includes(path: pathlib.Path, seen=None) -> set:
     for line in path.read_text(errors="ignore").splitlines():
         line = line.strip()
         if line.startswith("#include \""):
-            h = (path.parent / line.split('"')[1]).resolve()
+            name = line.split('"')[1]
+            h = (path.parent / name).resolve()
+            if not h.exists():   # -I csrc: "runtime/x.h" from csrc/runtime/*.cpp
+                h = (CSRC / name).resolve()
             if h.exists() and h not in seen:
                 seen.add(h)
                 _local_includes(h, seen)

@@ -197,94 +197,10 @@ __global__ __launch_bounds__(1024) void bn_finalize_wide_kernel(const PT* __rest
   }
 }
 
-// ---- one-launch finalize for many partial rows (layers 1-2: 1,568-14,336 rows) -----------------
-// Stage 1 is partials_reduce_kernel's arithmetic (grid (ceil(C/32), G): 64 columns = sums 0 and 1 of 32
-// channels x 4 row lanes, rpb rows per block); the LAST of a channel group's G blocks to arrive runs
-// the finalize over the G fp64 rows in bn_finalize_kernel's order, so the result is bitwise that of
-// the two-launch path whichever block arrives last.  Hand-off without an agent-scope release or
-// acquire (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms, table row 1): every byte
-// handed over is stored write-through (sc1: 8-byte agent-scope atomic stores), each storing wave
-// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier, ONE lane then takes a
-// relaxed agent-scope ticket, the block whose ticket came last reads the rows with sc1 (agent-scope
-// atomic) loads after a workgroup barrier.  Round 4's version paid a release (buffer_wbl2: the XCD's
-// L2 written back) per block and an acquire in the last one, and lost 3.2 % of the step.
-// The last arriver resets its counter slot to zero for the slot's next use.
-typedef __attribute__((address_space(1))) unsigned long long gu64;   // global (not flat) words
-typedef __attribute__((address_space(1))) int gi32;
-template <bool BWD, typename FA>
-__global__ __launch_bounds__(256) void bn_finalize_lastblock_kernel(const float* __restrict__ part, int T, int C,
-                                                                    int rpb, double* __restrict__ red,
-                                                                    int* __restrict__ cnt, FA fa) {
-  __shared__ double sh[4][64];
-  __shared__ double shf[2][4][32];
-  __shared__ int flag;
-  const int j = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int cb = blockIdx.x * 32;
-  const int cj = cb + (j & 31);
-  const int L = 2 * C;
-  const int col = (j < 32) ? cj : C + cj;
-  const bool ok = cj < C;
-  const int r0 = blockIdx.y * rpb, r1 = min(T, r0 + rpb);
-  double s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (ok) {
-    int r = r0 + g;
-    for (; r + 28 < r1; r += 32) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + 4 * u) * L + col];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s8[u] += v[u];
-    }
-    for (; r < r1; r += 4) s8[0] += part[(size_t)r * L + col];
-  }
-  const double s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-  sh[g][j] = s;
-  __syncthreads();
-  gu64* redg = (gu64*)red;
-  if (g == 0 && ok)
-    __hip_atomic_store(redg + (size_t)blockIdx.y * L + col,
-                       (unsigned long long)__double_as_longlong(s + sh[1][j] + sh[2][j] + sh[3][j]),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
-  __syncthreads();
-  gi32* my = (gi32*)cnt + blockIdx.x;
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(my, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag = (t == (int)gridDim.y - 1) ? 1 : 0;
-  }
-  __syncthreads();
-  if (!flag) return;
-  const int G = gridDim.y;
-  const int q = threadIdx.x & 31, lane = (threadIdx.x >> 5) & 3;
-  const int c = cb + q;
-  if (threadIdx.x < 128) {
-    // all (<= 16 + 16) sc1 loads in flight first, then the ordered sums (G <= 64 by construction)
-    double va[16], vb[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int t = lane + 4 * k;
-      const bool in = c < C && t < G;
-      va[k] = in ? __longlong_as_double((long long)__hip_atomic_load(redg + (size_t)t * L + c, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
-      vb[k] = in ? __longlong_as_double((long long)__hip_atomic_load(redg + (size_t)t * L + C + c, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT)) : 0.0;
-    }
-    double a = 0, b = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (lane + 4 * k < G) { a += va[k]; b += vb[k]; }
-    shf[0][lane][q] = a;
-    shf[1][lane][q] = b;
-  }
-  __syncthreads();
-  if (threadIdx.x < 32 && c < C) {
-    double a = shf[0][0][q], b = shf[1][0][q];
-    for (int k = 1; k < 4; ++k) { a += shf[0][k][q]; b += shf[1][k][q]; }
-    if constexpr (BWD) bn_bwd_finalize_channel(c, a, b, fa);
-    else bn_finalize_channel(c, a, b, fa);
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(my, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// (Round 5's one-launch last-arriver finalize for > 512 partial rows -- sc1 write-through hand-off
+// without release / acquire, off by default and 0.1-0.4 % slower in the step, profiles/
+// r5_bn_lastblock_ab.txt -- was removed in round 6: its correctness rested on ISA-level ordering
+// arguments, not on the memory model.  Above bn_wide_rows the two-launch path runs.)
 
 // ---- finalize: partials [T][2][C] -> mean, invstd, scale, shift; running stats update --------
 // block = 256 threads handles 64 channels (4 row-groups of partials).
@@ -778,35 +694,6 @@ static at::Tensor reduce_partials(const at::Tensor& part, int& T_out) {
 // Partial-row count up to which the finalize is one wide launch (knob bn_wide_rows; <= 64 rows the
 // 256-thread finalize reads them directly, above bn_wide_rows the two-stage path runs).
 static Knob kn_bn_wide_rows("bn_wide_rows", 512);
-// Above bn_wide_rows: the one-launch last-arriver finalize (knob bn_lastblock; 0 = two launches).
-static Knob kn_bn_lastblock("bn_lastblock", 0);   // whole-step A/B: -0.1 to -0.4 % (profiles/r5_bn_lastblock_ab.txt)
-
-// Zero-initialised int32 ticket counters: a per-device ring over one persistent buffer; the last user
-// of a slot resets it, so a slot is zero again once the kernel that used it has finished (stream
-// order).  nullptr when the buffer does not exist yet and a graph is being captured.
-static int* counter_slots(int n, int device) {
-  constexpr int kSlots = 1 << 20;
-  static std::mutex mu;
-  static std::unordered_map<int, std::pair<int*, int>> bufs;   // device -> (buffer, cursor)
-  std::lock_guard<std::mutex> g(mu);
-  auto it = bufs.find(device);
-  if (it == bufs.end()) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* buf = nullptr;
-    PCMP_HIP_CHECK(hipMalloc(&buf, sizeof(int) * kSlots));
-    PCMP_HIP_CHECK(hipMemset(buf, 0, sizeof(int) * kSlots));
-    PCMP_HIP_CHECK(hipDeviceSynchronize());
-    it = bufs.emplace(device, std::make_pair(buf, 0)).first;
-  }
-  auto& e = it->second;
-  if (n > kSlots) return nullptr;
-  if (e.second + n > kSlots) e.second = 0;
-  int* r = e.first + e.second;
-  e.second += n;
-  return r;
-}
-
 template <bool BWD, typename FA>
 static bool wide_finalize(const at::Tensor& part, const FA& fa) {
   const int T = part.size(0), C = part.size(2);
@@ -817,18 +704,7 @@ static bool wide_finalize(const at::Tensor& part, const FA& fa) {
     PCMP_LAUNCH_CHECK();
     return true;
   }
-  if (!kn_bn_lastblock.get()) return false;
-  const int rpb = std::max(16, ceil_div(T, 64));
-  const int G = ceil_div(T, rpb);   // <= 64: the last arriver holds 16 rows per lane in registers
-  TORCH_CHECK(G <= 64, "bn finalize: too many row groups");
-  const int nb = ceil_div(C, 32);
-  int* cnt = counter_slots(nb, part.get_device());
-  if (!cnt) return false;
-  auto red = at::empty({G, 2 * (int64_t)C}, part.options().dtype(at::kDouble));
-  hipLaunchKernelGGL((bn_finalize_lastblock_kernel<BWD, FA>), dim3(nb, G), dim3(256), 0, cur_stream(),
-                     ptr<float>(part), T, C, rpb, ptr<double>(red), cnt, fa);
-  PCMP_LAUNCH_CHECK();
-  return true;
+  return false;
 }
 
 // partials -> (mean, invstd, scale, shift) ; updates running stats in place when given.

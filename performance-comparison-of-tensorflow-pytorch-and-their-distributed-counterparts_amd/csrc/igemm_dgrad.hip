@@ -2,6 +2,7 @@
 // Kernels, launchers, dispatch and the GEMM planner live in igemm.h; this translation unit holds the
 // DGRAD entry points (split from igemm.hip in round 4 so the three modes compile in parallel).
 #include "igemm.h"
+#include "bnr_stream.h"
 
 namespace pcmp {
 
@@ -191,6 +192,16 @@ static std::vector<at::Tensor> dgrad_impl(const at::Tensor& dy, const at::Tensor
   at::Tensor part, part2;
   if (bn) {
     set_bn(p);   // before igemm_bm: the kernel choice depends on the epilogue variant
+    if (use_bnr_stream(p)) {   // memory-bound short-K 1x1: the streaming kernel (bnr_stream.h)
+      const int T = bnr_stream_groups(p);
+      part = at::empty({T, 2, C}, fopts);
+      p.stats_cap = T;
+      p.stats = ptr<float>(part);
+      if (two) { part2 = at::empty({T, 2, C}, fopts); p.stats2 = ptr<float>(part2); }
+      launch_bnr_stream(p, st);
+      if (two) return {dx, part, part2};
+      return {dx, part};
+    }
     const int T = ceil_div(p.gm, igemm_bm(MODE_DGRAD, p));
     part = at::empty({T, 2, C}, fopts);
     p.stats_cap = T;

@@ -46,20 +46,54 @@ def _native():
     return _lib.load() and hasattr(torch.ops.pcmp, "text_encode")
 
 
+_CJK = ((0x4E00, 0x9FFF), (0x3400, 0x4DBF), (0x20000, 0x2A6DF), (0x2A700, 0x2B73F), (0x2B740, 0x2B81F),
+        (0x2B820, 0x2CEAF), (0xF900, 0xFAFF), (0x2F800, 0x2FA1F))
+_WS = {0x9, 0xA, 0xB, 0xC, 0xD, 0x20, 0x85, 0xA0, 0x1680, *range(0x2000, 0x200B), 0x2028, 0x2029, 0x202F, 0x205F,
+       0x3000}
+
+
+def _is_punct(ch):
+    import unicodedata
+    cp = ord(ch)
+    return (33 <= cp <= 47) or (58 <= cp <= 64) or (91 <= cp <= 96) or (123 <= cp <= 126) or \
+        unicodedata.category(ch).startswith("P")
+
+
 def _py_basic(text, lower=True, strip=True):
+    """Pure-Python twin of the native basic tokenizer (csrc/runtime/text_core.h): HuggingFace
+    BertNormalizer (clean text, isolate CJK ideographs, strip accents + lowercase) + BertPreTokenizer
+    (whitespace split, punctuation isolated)."""
+    import unicodedata
     if strip:
         text = rm_tags(text)
+    buf = []
+    for ch in text:
+        cp = ord(ch)
+        if ch in "\t\n\r":
+            buf.append(" ")
+            continue
+        if cp == 0 or cp == 0xFFFD or unicodedata.category(ch)[0] == "C":
+            continue
+        if cp in _WS:
+            buf.append(" ")
+        elif any(lo <= cp <= hi for lo, hi in _CJK):
+            buf.append(" " + ch + " ")
+        else:
+            buf.append(ch)
+    text = "".join(buf)
+    if lower:
+        text = "".join(c.lower() for c in unicodedata.normalize("NFD", text) if unicodedata.category(c) != "Mn")
     out, cur = [], []
     for ch in text:
-        if ch.isspace():
+        if ch == " ":
             if cur:
                 out.append("".join(cur)); cur = []
-        elif ch in string.punctuation:
+        elif _is_punct(ch):
             if cur:
                 out.append("".join(cur)); cur = []
             out.append(ch)
         else:
-            cur.append(ch.lower() if lower and ord(ch) < 128 else ch)
+            cur.append(ch)
     if cur:
         out.append("".join(cur))
     return out
@@ -99,7 +133,7 @@ def load_vocab(path):
 
 
 def _py_wordpiece(word, vmap, unk):
-    if len(word) > 100:
+    if len(word) > 100:   # code points
         return [unk]
     out, start = [], 0
     while start < len(word):

@@ -42,6 +42,7 @@ Stream ordering (MI355X: compute stream + WGRAD side stream + RCCL's internal st
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import os
 import time
@@ -97,6 +98,8 @@ def _plan_greedy(sizes, first_bucket_elems, bucket_elems):
 
 
 class DistributedDataParallel(torch.nn.Module):
+    TIMED_STEPS_KEPT = 256   # time_exposed keeps the most recent timed steps' events
+
     def __init__(self, module: torch.nn.Module, flat: FlatParams, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 4.0, broadcast_buffers: bool | str = "init", average: bool = True,
                  last_bucket_mb: float = 4.0, force: bool | None = None, grad_dtype: torch.dtype | str | None = None):
@@ -142,8 +145,10 @@ class DistributedDataParallel(torch.nn.Module):
             p._grad_ready_hook = self._on_grad_ready
         self._next_launch = 0
         self._timing = False
-        self._exposed = []      # per step: (compute-done event, comm-done event) or host seconds
-        self._timeline = []     # per step: [(bucket, launch, done)] events (GPU) / seconds vs finish (CPU)
+        # per step: (compute-done event, comm-done event) or host seconds / [(bucket, launch, done)]
+        # events (GPU) or seconds vs finish (CPU); the last TIMED_STEPS_KEPT steps (time_exposed)
+        self._exposed = collections.deque(maxlen=self.TIMED_STEPS_KEPT)
+        self._timeline = collections.deque(maxlen=self.TIMED_STEPS_KEPT)
         self._tl_stream = None
         self._ev_ref = None
         if broadcast_buffers is True:
@@ -160,8 +165,10 @@ class DistributedDataParallel(torch.nn.Module):
         the compute stream reaching ``finish_gradient_sync`` to the last collective (and its bf16
         cast-back) finishing on the comm stream.  CUDA events (no host sync); host seconds on CPU."""
         self._timing = bool(on)
-        self._exposed = []
-        self._timeline = []
+        # the most recent timed steps only (each holds CUDA events until comm_report): a long timed
+        # run keeps a bounded number of events alive
+        self._exposed = collections.deque(maxlen=self.TIMED_STEPS_KEPT)
+        self._timeline = collections.deque(maxlen=self.TIMED_STEPS_KEPT)
         if on and self._comm_stream is not None and self._tl_stream is None:
             self._tl_stream = torch.cuda.Stream(self.flat.grad.device)
 
@@ -433,27 +440,31 @@ def sync_autotune(process_group=None) -> int:
     return int(torch.ops.pcmp.autotune_load(table[0]))
 
 
-_SYNCED_MAX = [-1]   # the largest plan-table size any rank had at the last sync
+_SYNCED_SIZE = [-1]   # THIS rank's plan-table size right after the last sync
 
 
 def sync_autotune_if_grown(process_group=None) -> int:
-    """Run :func:`sync_autotune` again when some rank planned shapes after the last sync (a last
-    partial batch, other text batch shapes, the first eval batches): one all-reduce of the table
-    sizes decides, so every rank takes the same branch.  Called at epoch ends by the training
-    loops; returns the entries applied (0 when nothing grew)."""
+    """Run :func:`sync_autotune` again when ANY rank planned shapes after the last sync (a last
+    partial batch, other text batch shapes, the first eval batches): each rank compares its table
+    with its own size right after the last sync, and one MAX all-reduce of the growth decides, so
+    every rank takes the same branch -- growth on a rank that is not the largest is seen too.
+    Called at epoch ends by the training loops; returns the entries applied (0 when nothing grew)."""
     if not dist.is_initialized() or dist.get_world_size(process_group) <= 1:
         return 0
     from ..ops import _lib
-    n = len(torch.ops.pcmp.autotune_table()) if _lib.load() else 0
+    have = _lib.load()
+    n = len(torch.ops.pcmp.autotune_table()) if have else 0
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(process_group) == "nccl" \
         else torch.device("cpu")
-    t = torch.tensor([n], dtype=torch.int64, device=dev)
+    t = torch.tensor([n - _SYNCED_SIZE[0]], dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=process_group)
-    m = int(t.item())
-    if m <= _SYNCED_MAX[0]:
+    if int(t.item()) <= 0:
         return 0
-    _SYNCED_MAX[0] = m
-    return sync_autotune(process_group)
+    applied = sync_autotune(process_group)
+    # remembered AFTER the merge: rank 0's entries now count as this rank's own, so the next epoch
+    # does not see them as growth (no redundant second sync)
+    _SYNCED_SIZE[0] = len(torch.ops.pcmp.autotune_table()) if have else 0
+    return applied
 
 
 def step_time_spread(seconds: float, process_group=None) -> dict:

@@ -38,8 +38,17 @@ int main() {
   basic_tokenize("The Movie,was GREAT!", true, t);
   CHECK(t.size() == 6 && t[0] == "the" && t[2] == "," && t[5] == "!");
   t.clear();
-  basic_tokenize(std::string("caf\xc3\xa9 \x00x", 8), true, t);   // bytes >= 0x80 stay in the word, NUL dropped
-  CHECK(t.size() == 2 && t[0] == "caf\xc3\xa9" && t[1] == "x");
+  basic_tokenize(std::string("caf\xc3\xa9 \x00x", 8), true, t);   // accent stripped (lower), NUL dropped
+  CHECK(t.size() == 2 && t[0] == "cafe" && t[1] == "x");
+  t.clear();
+  basic_tokenize(std::string("caf\xc3\xa9", 5), false, t);   // no lower-casing: accents kept
+  CHECK(t.size() == 1 && t[0] == "caf\xc3\xa9");
+  t.clear();
+  basic_tokenize("\xe4\xb8\xad\xe5\x9b\xbd" "ab\xe2\x80\x94" "c \xc3\x80", true, t);   // CJK isolated, em dash is P*
+  CHECK(t.size() == 6 && t[2] == "ab" && t[3] == "\xe2\x80\x94" && t[4] == "c" && t[5] == "a");
+  t.clear();
+  basic_tokenize(std::string("a\xe2\x80\x8b" "b\xc3", 6), true, t);   // zero-width space (Cf) dropped, truncated UTF-8 dropped
+  CHECK(t.size() == 1 && t[0] == "ab");
 
   std::vector<int64_t> wp;
   wordpiece("unbelievable", v, wp);

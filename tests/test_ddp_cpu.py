@@ -160,3 +160,44 @@ def test_ddp_bucket_timeline_and_buffer_average(tmp_path):
         assert tl[0]["launch_ms"] < 0 and tl[1]["launch_ms"] < 0, tl     # launched before backward ended
         assert all(t["done_ms"] >= t["launch_ms"] and t["bytes"] > 0 for t in tl), tl
         assert d["differ_before"] and d["equal_after"] and d["is_mean"], d
+
+
+def _grown_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from pcmp.ops import _lib
+    from pcmp.parallel import ddp as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    assert _lib.load(), _lib.load_error()
+    ops = torch.ops.pcmp
+    D._SYNCED_SIZE[0] = -1
+    # the last rank keeps 5 shapes of its own, so it holds the largest table after the first sync
+    extra = [f"W;own{rank}-{i};2" for i in range(5)] if rank == world - 1 else []
+    ops.autotune_load([f"W;first;{rank + 1}"] + extra)
+    first = D.sync_autotune_if_grown()
+    # only rank 0 (NOT the largest table) plans new shapes; a max-size test would miss this growth
+    if rank == 0:
+        ops.autotune_load(["W;late-a;7", "W;late-b;9"])
+    second = D.sync_autotune_if_grown()
+    third = D.sync_autotune_if_grown()   # nothing new anywhere: no sync (and no redundant one)
+    table = list(ops.autotune_table())
+    torch.save({"first": first, "second": second, "third": third, "table": table},
+               os.path.join(out, f"g{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_sync_autotune_if_grown_sees_growth_on_any_rank(tmp_path):
+    """growth of a rank whose table is not the largest triggers the re-sync, and the
+    merge itself does not trigger a second, redundant one."""
+    from pcmp.ops import _lib
+    if not _lib.load():
+        pytest.skip(f"native library not built: {_lib.load_error()}")
+    os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
+    world = 3
+    mp.spawn(_grown_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(world)]
+    for r, d in enumerate(res):
+        assert d["first"] > 0 and d["second"] > 0, (r, d)
+        assert d["third"] == 0, (r, d)
+        assert "W;late-a;7" in d["table"] and "W;late-b;9" in d["table"], (r, d["table"])
+        assert "W;first;1" in d["table"], (r, d["table"])   # rank 0's choice everywhere

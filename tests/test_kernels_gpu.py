@@ -206,10 +206,9 @@ def test_bn_forward_backward(gpu, C):
 @pytest.mark.parametrize("T,C", [(65, 64), (392, 256), (512, 2048), (300, 72), (1568, 2048), (6272, 64), (14336, 64), (785, 136)])
 def test_bn_wide_finalize(gpu, T, C):
     """One-launch finalize: the wide kernel (64 < T <= bn_wide_rows partial rows) == the two-stage
-    path (bn_wide_rows = 64) to fp64 rounding; the last-arriver kernel (T > bn_wide_rows, sc1 hand-off
-    without release / acquire fences) == the two-stage path bitwise; for the forward (mean / invstd /
-    scale / shift / running stats) and backward (dgamma / dbeta / coef) finalize; against an fp64 torch
-    reduction; repeated calls (counter slots reused) bitwise equal."""
+    path (bn_wide_rows = 64) to fp64 rounding; above bn_wide_rows the two-stage path runs; for the
+    forward (mean / invstd / scale / shift / running stats) and backward (dgamma / dbeta / coef)
+    finalize; against an fp64 torch reduction; repeated calls bitwise equal."""
     ops = _ops()
     g = torch.Generator(device=gpu).manual_seed(T + C)
     part = torch.randn(T, 2, C, device=gpu, generator=g)
@@ -220,12 +219,10 @@ def test_bn_wide_finalize(gpu, T, C):
     count = T * 16
     outs = {}
     prev = ops.set_knob("bn_wide_rows", 512)
-    prevl = ops.set_knob("bn_lastblock", 1)
     try:
-        # (wide rows, last-arriver): two-stage path, default path (twice), last-arriver off
-        for v in ((64, 0), (512, 1), (512, 1), (512, 0)):
-            ops.set_knob("bn_wide_rows", v[0])
-            ops.set_knob("bn_lastblock", v[1])
+        # two-stage path, default path (twice)
+        for v in (64, 512, 512):
+            ops.set_knob("bn_wide_rows", v)
             rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
             fwd = ops.bn_finalize(part, count, gam, bet, rm, rv, 0.1, 1e-5)
             dg, db = torch.full((C,), 0.5, device=gpu), torch.full((C,), 0.25, device=gpu)
@@ -233,18 +230,14 @@ def test_bn_wide_finalize(gpu, T, C):
             outs.setdefault(v, []).append([t.clone() for t in (*fwd, rm, rv, dg, db, coef)])
     finally:
         ops.set_knob("bn_wide_rows", prev)
-        ops.set_knob("bn_lastblock", prevl)
-    base = outs[(512, 1)][0]
-    for a, b in zip(base, outs[(512, 1)][1]):
+    base = outs[512][0]
+    for a, b in zip(base, outs[512][1]):
         assert torch.equal(a, b)
-    for a, b in zip(base, outs[(64, 0)][0]):
-        if T > 512:   # the last-arriver finalize sums in the two-stage path's order: bitwise equal
+    for a, b in zip(base, outs[64][0]):
+        if T > 512:   # both the two-stage path
             assert torch.equal(a, b)
         else:
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
-    if T > 512:
-        for a, b in zip(outs[(512, 0)][0], outs[(64, 0)][0]):
-            assert torch.equal(a, b)
     s = part.double().sum(0)
     m = s[0] / count
     var = (s[1] / count - m * m).clamp_min(0)
