@@ -36,7 +36,7 @@
 namespace pcmp {
 
 inline Knob kn_bnr_stream("bnr_stream", 1);
-inline Knob kn_bnr_stream_wgs("bnr_stream_wgs", 1024);   // workgroups (a multiple of the channel tiles)
+inline Knob kn_bnr_stream_wgs("bnr_stream_wgs", 512);   // workgroups: 512 vs 1024 +0.2 % in the step (profiles/r6_bnr_stream_step_ab.txt)
 
 template <int BN, int GK, bool FOLD, bool DUAL>
 __global__ void __launch_bounds__(256, 2) bnr_stream_kernel(const IgemmParams p, int groups) {
