@@ -36,7 +36,9 @@
 namespace pcmp {
 
 inline Knob kn_bnr_stream("bnr_stream", 1);
-inline Knob kn_bnr_stream_wgs("bnr_stream_wgs", 512);   // workgroups: 512 vs 1024 +0.2 % in the step (profiles/r6_bnr_stream_step_ab.txt)
+// workgroups: 256 (one per CU, ~2x the tiles per workgroup of 512) streams layers 1-3 at 3.5-5.5 TB/s
+// (profiles/r6_bnr_stream_micro_v2.txt)
+inline Knob kn_bnr_stream_wgs("bnr_stream_wgs", 256);
 
 template <int BN, int GK, bool FOLD, bool DUAL>
 __global__ void __launch_bounds__(256, 2) bnr_stream_kernel(const IgemmParams p, int groups) {
@@ -206,14 +208,6 @@ __global__ void __launch_bounds__(256, 2) bnr_stream_kernel(const IgemmParams p,
       wait_vm_b<NEL + NCH>();
       lds_sync_b();
     }
-    __builtin_amdgcn_sched_barrier(0);
-    // the next tile's operands, issued unconditionally (after the last tile through zero-record
-    // descriptors: no traffic) so the vmcnt counts are the same on every path
-    const bool more = j + 1 < nmine;
-    issue_a(S ^ 1, pt + groups, more);
-    __builtin_amdgcn_sched_barrier(0);   // the count above needs the DMAs ahead of the loads
-    issue_e(std::integral_constant<int, S ^ 1>{}, pt + groups, more);
-    __builtin_amdgcn_sched_barrier(0);
     char* sA = sS + S * STAGE;
     if constexpr (FOLD) {   // dz = k1*g + k2*x + k3 in place (bn_bwd_apply's rounding)
 #pragma unroll
@@ -236,6 +230,15 @@ __global__ void __launch_bounds__(256, 2) bnr_stream_kernel(const IgemmParams p,
       }
       lds_sync_b();
     }
+    // the next tile's operands, issued unconditionally (after the last tile through zero-record
+    // descriptors: no traffic) so the vmcnt counts are the same on every path; after the in-place
+    // fold, whose LDS writes the compiler would otherwise order behind the DMA (a vmcnt(0) wait)
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more = j + 1 < nmine;
+    issue_a(S ^ 1, pt + groups, more);
+    __builtin_amdgcn_sched_barrier(0);   // the count above needs the DMAs ahead of the loads
+    issue_e(std::integral_constant<int, S ^ 1>{}, pt + groups, more);
+    __builtin_amdgcn_sched_barrier(0);
     // GEMM: wave w < NWT computes pixels 0..31 x channels 32w..32w+31 of the tile
     if (wid < NWT) {
       f32x16 acc;
@@ -296,10 +299,14 @@ __global__ void __launch_bounds__(256, 2) bnr_stream_kernel(const IgemmParams p,
       *reinterpret_cast<uint4*>(out + o) = uint4{ov[0], ov[1], ov[2], ov[3]};
     }
   };
-  for (int j = 0; j < nmine; j += 2) {
+  // (the back edge always runs both stages: a path that skipped stage 1 would leave its register set's
+  //  loads pending at the loop head, and the compiler would wait for them there)
+  int j = 0;
+  for (; j + 1 < nmine; j += 2) {
     tile(std::integral_constant<int, 0>{}, j);
-    if (j + 1 < nmine) tile(std::integral_constant<int, 1>{}, j + 1);
+    tile(std::integral_constant<int, 1>{}, j + 1);
   }
+  if (j < nmine) tile(std::integral_constant<int, 0>{}, j);
 
   // ---- column sums: [RPP rows][NS][BN] through LDS, then one row of the partial buffers --------------
   __syncthreads();
@@ -391,6 +398,251 @@ static void launch_bnr_stream(IgemmParams& p, hipStream_t st) {
     if (p.gk == 64) PCMP_BNRS(128, 64); else if (p.gk == 128) PCMP_BNRS(128, 128); else PCMP_BNRS(128, 256);
   }
 #undef PCMP_BNRS
+}
+
+}  // namespace pcmp
+
+namespace pcmp {
+
+// ------------------------------------------------------------------------------------------------
+// The same streaming structure for the expanding 1x1 FWD convs with BatchNorm statistics (the conv3
+// of every bottleneck of layers 1-3 and the stride-1 layer-1 downsample: K = 64 / 128 / 256 input
+// channels -> 4x as many outputs):
+//   y[m][n] = bf16( sum_k a[m][k] * W[n][k] ),  a = x  or  relu(scale[k] * z[m][k] + shift[k])
+//   part[grp][0][n] += y,  part[grp][1][n] += y * y
+// The one-tile kernels (igemm_kernel<MODE_FWD, ..., EPI_STATS> / igemm_dma32_kernel) write one
+// partial-statistics row per 128-pixel tile and pay each tile's operand latency serially; here the
+// next tile's operand is DMA'd while the current tile's output streams out, Wt stays in LDS, the
+// BatchNorm-forward fold (the previous BN's relu(scale * z + shift), in-place on the LDS operand) is
+// applied once per operand element, and each thread's per-channel sums stay in registers for all of
+// its tiles (one statistics row per workgroup group).
+inline Knob kn_fwd_stream("fwd_stream", 1);
+inline Knob kn_fwd_stream_wgs("fwd_stream_wgs", 512);   // 512 > 256 (profiles/r6_fwd_stream_micro.txt)
+
+template <int BN, int GK, bool FOLD>
+__global__ void __launch_bounds__(256, 2) fwd_stream_kernel(const IgemmParams p, int groups) {
+  constexpr int BM = 32, NTHR = 256;
+  constexpr int KB = GK / 64;
+  constexpr int A_IMG = BM * GK * 2;
+  constexpr int STAGE = A_IMG;
+  constexpr int W_BYTES = BN * GK * 2;
+  constexpr int CS = BN + 8;
+  constexpr int CPR = BN / 8;
+  constexpr int NCH = BM * BN / 8 / NTHR;           // 2 (BN 128) or 4 (BN 256)
+  constexpr int RPP = NTHR / CPR;
+  constexpr int NWT = BN / 32;                      // 32x32 output tiles
+  constexpr int TPW = NWT > 4 ? NWT / 4 : 1;        // tiles per GEMM wave
+  constexpr int NAI = A_IMG / 1024 / 4;
+  constexpr int NWI = W_BYTES / 1024 / 4;
+  static_assert(NCH >= 1 && NAI >= 1 && NWI >= 1 && (NWT <= 4 || NWT % 4 == 0), "fwd_stream tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sW = smem;
+  char* sS = smem + W_BYTES;
+  float* sC = reinterpret_cast<float*>(smem + W_BYTES + 2 * STAGE);
+  float* sK = sC + BM * CS;                         // act-fold coefficients [2][GK]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = p.gn / BN;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = lin / ntn, n0 = (lin - grp * ntn) * BN;
+  const int npt = p.gm / BM;
+  const int nmine = grp < npt ? (npt - 1 - grp) / groups + 1 : 0;
+
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(p.a, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsW = make_rsrc(p.b, p.b_bytes);
+  const __amdgpu_buffer_rsrc_t rsZ = make_rsrc(p.a, 0u);
+  const int lch = (lane & 7) ^ ((lane >> 3) & 7);
+  int a_vo[NAI];
+#pragma unroll
+  for (int i = 0; i < NAI; ++i) {
+    const int u = wid * NAI + i;
+    const int row = (u & 3) * 8 + (lane >> 3);
+    a_vo[i] = (row * GK + (u >> 2) * 64 + lch * 8) * 2;
+  }
+  auto issue_a = [&](int s, int pt, bool live) {
+    char* dst = sS + s * STAGE;
+    const int so = live ? pt * BM * GK * 2 : 0;
+    const __amdgpu_buffer_rsrc_t ra = live ? rsA : rsZ;
+#pragma unroll
+    for (int i = 0; i < NAI; ++i) {
+      const int vo = a_vo[i];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(dst + (wid * NAI + i) * 1024),
+                                               16, vo, so, 0, 0);
+    }
+  };
+  {
+    int w_vo[NWI];
+#pragma unroll
+    for (int i = 0; i < NWI; ++i) {
+      const int u = wid * NWI + i;
+      const int row = (u % (BN / 8)) * 8 + (lane >> 3);
+      w_vo[i] = ((n0 + row) * GK + (u / (BN / 8)) * 64 + lch * 8) * 2;
+    }
+#pragma unroll
+    for (int i = 0; i < NWI; ++i) {
+      const int vo = w_vo[i];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (__attribute__((address_space(3))) void*)(sW + (wid * NWI + i) * 1024),
+                                               16, vo, 0, 0, 0);
+    }
+  }
+  if constexpr (FOLD) {
+    for (int i = tid; i < 2 * GK; i += NTHR) sK[i] = i < GK ? p.act_sc[i] : p.act_sh[i - GK];
+  }
+  const int c8 = tid % CPR, r0 = tid / CPR;
+  float sm[2][8];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm[q][e] = 0.f;
+  const int pt0 = grp;
+  issue_a(0, pt0, nmine > 0);
+  wait_vm_b<0>();
+  lds_sync_b();
+
+  auto tile = [&](auto sel, int j) {
+    constexpr int S = decltype(sel)::value;
+    const int pt = pt0 + j * groups;
+    if (j > 0) {
+      wait_vm_b<NCH>();   // stage S landed: issued after its DMA were tile j-1's stores
+      lds_sync_b();
+    }
+    char* sA = sS + S * STAGE;
+    if constexpr (FOLD) {   // a = relu(scale * z + shift), bf16-rounded as bn_apply rounds it
+#pragma unroll
+      for (int i = 0; i < KB; ++i) {
+        const int row = tid >> 3;
+        const int kc = i * 64 + (((tid & 7) ^ (row & 7)) << 3);
+        char* zp = sA + i * (BM * 128) + tid * 16;
+        float a[8], b[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 u = *reinterpret_cast<const f32x4*>(sK + kc + 4 * h);
+          const f32x4 v = *reinterpret_cast<const f32x4*>(sK + GK + kc + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { a[4 * h + e] = u[e]; b[4 * h + e] = v[e]; }
+        }
+        *reinterpret_cast<uint4*>(zp) = fold_act(*reinterpret_cast<const uint4*>(zp), a, b, true);
+      }
+      lds_sync_b();
+    }
+    // next tile's operand (after the in-place fold: see bnr_stream_kernel)
+    __builtin_amdgcn_sched_barrier(0);
+    issue_a(S ^ 1, pt + groups, j + 1 < nmine);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wid < NWT) {
+#pragma unroll
+      for (int tt = 0; tt < TPW; ++tt) {
+        const int ct = wid + 4 * tt;   // channel tile
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < GK / 16; ++ks) {
+          const int ch = ks * 2 + (lane >> 5);
+          const int kb = ch >> 3, cc = ch & 7;
+          const bf16x8 fa = *reinterpret_cast<const bf16x8*>(sA + kb * (BM * 128) + rr_off(lane & 31, cc));
+          const bf16x8 fb = *reinterpret_cast<const bf16x8*>(sW + kb * (BN * 128) + rr_off(ct * 32 + (lane & 31), cc));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sC[(8 * (r >> 2) + 4 * (lane >> 5) + (r & 3)) * CS + ct * 32 + (lane & 31)] = acc[r];
+      }
+    }
+    lds_sync_b();
+    __bf16* out = reinterpret_cast<__bf16*>(p.out);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int row = r0 + k * RPP;
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(sC + row * CS + c8 * 8);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(sC + row * CS + c8 * 8 + 4);
+      const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      unsigned ov[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned u = f2bf2(av[2 * q], av[2 * q + 1]);
+        const float y0 = __uint_as_float(u << 16), y1 = __uint_as_float(u & 0xffff0000u);
+        sm[0][2 * q] += y0;
+        sm[0][2 * q + 1] += y1;
+        sm[1][2 * q] += y0 * y0;
+        sm[1][2 * q + 1] += y1 * y1;
+        ov[q] = u;
+      }
+      const size_t o = (size_t)(pt * BM + row) * p.gn + n0 + c8 * 8;
+      *reinterpret_cast<uint4*>(out + o) = uint4{ov[0], ov[1], ov[2], ov[3]};
+    }
+  };
+  // (the back edge always runs both stages: a path that skipped stage 1 would leave its register set's
+  //  loads pending at the loop head, and the compiler would wait for them there)
+  int j = 0;
+  for (; j + 1 < nmine; j += 2) {
+    tile(std::integral_constant<int, 0>{}, j);
+    tile(std::integral_constant<int, 1>{}, j + 1);
+  }
+  if (j < nmine) tile(std::integral_constant<int, 0>{}, j);
+
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(sS);   // stages / result tile dead (launch sizes LDS for it)
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    *reinterpret_cast<f32x4*>(red + (r0 * 2 + q) * BN + c8 * 8) = f32x4{sm[q][0], sm[q][1], sm[q][2], sm[q][3]};
+    *reinterpret_cast<f32x4*>(red + (r0 * 2 + q) * BN + c8 * 8 + 4) = f32x4{sm[q][4], sm[q][5], sm[q][6], sm[q][7]};
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * BN; i += NTHR) {
+    const int q = i / BN, c = i - q * BN;
+    float t = 0.f;
+    for (int r = 0; r < RPP; ++r) t += red[(r * 2 + q) * BN + c];
+    p.stats[(size_t)grp * 2 * p.gn + q * p.gn + n0 + c] = t;
+  }
+}
+
+// eligible (called for a training FWD, i.e. with statistics): a 1x1 stride-1 conv expanding K = 64 /
+// 128 / 256 channels into more outputs (a 128-multiple), no bias / residual / activation
+static bool use_fwd_stream(const IgemmParams& p) {
+  if (!kn_fwd_stream.get() || p.bias || p.resid || p.relu) return false;
+  if (p.R != 1 || p.S != 1 || p.stride != 1 || p.pad != 0) return false;
+  // (K = 256, the layer-3 conv3, measured 48 -> 54 us on the stream: the one-tile kernel keeps it)
+  if (!(p.gk == 64 || p.gk == 128) || p.gk >= p.gn || p.gn % 128 || p.gm % 32) return false;
+  return (int64_t)p.gm * p.gn * 2 < (1ll << 31);
+}
+static int fwd_stream_bn(const IgemmParams& p) { return (p.gk == 64 && p.gn % 256 == 0) ? 256 : 128; }
+static int fwd_stream_groups(const IgemmParams& p) {
+  const int ntn = p.gn / fwd_stream_bn(p);
+  return std::max(1, std::min(p.gm / 32, std::max(1, kn_fwd_stream_wgs.get() / ntn)));
+}
+
+template <int BN, int GK, bool FOLD>
+static void launch_fwd_stream_cfg(IgemmParams& p, hipStream_t st) {
+  constexpr int BM = 32;
+  const int ntn = p.gn / BN;
+  const int groups = fwd_stream_groups(p);
+  TORCH_CHECK(p.stats && p.stats_cap >= groups, "fwd_stream: partial-stats buffer");
+  constexpr size_t body = (size_t)2 * BM * GK * 2 + (size_t)BM * (BN + 8) * 4 + (FOLD ? 2 * GK * 4 : 0);
+  constexpr size_t red = (size_t)(256 / (BN / 8)) * 2 * BN * 4;
+  constexpr size_t smem = (size_t)BN * GK * 2 + std::max(body, red);
+  static_assert(smem <= 160 * 1024, "fwd_stream: LDS");
+  auto kf = &fwd_stream_kernel<BN, GK, FOLD>;
+  static bool attr = false;
+  if (!attr) {
+    PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kf, dim3(groups * ntn), dim3(256), smem, st, p, groups);
+  PCMP_LAUNCH_CHECK();
+}
+
+static void launch_fwd_stream(IgemmParams& p, hipStream_t st) {
+  const bool fold = p.act_sc != nullptr;
+  if (fwd_stream_bn(p) == 256) {
+    if (fold) launch_fwd_stream_cfg<256, 64, true>(p, st); else launch_fwd_stream_cfg<256, 64, false>(p, st);
+  } else if (p.gk == 64) {
+    if (fold) launch_fwd_stream_cfg<128, 64, true>(p, st); else launch_fwd_stream_cfg<128, 64, false>(p, st);
+  } else {
+    if (fold) launch_fwd_stream_cfg<128, 128, true>(p, st); else launch_fwd_stream_cfg<128, 128, false>(p, st);
+  }
 }
 
 }  // namespace pcmp

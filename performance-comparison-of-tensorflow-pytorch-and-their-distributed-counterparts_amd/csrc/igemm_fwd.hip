@@ -2,6 +2,7 @@
 // Kernels, launchers, dispatch and the GEMM planner live in igemm.h; this translation unit holds the
 // FWD entry points (split from igemm.hip in round 4 so the three modes compile in parallel).
 #include "igemm.h"
+#include "bnr_stream.h"
 
 namespace pcmp {
 
@@ -56,12 +57,19 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
   const int BMsel = p.gm <= 32 ? 32 : (p.gm <= 64 ? 64 : 128);
   const int BNsel = p.gn <= 64 ? 64 : 128;
   at::Tensor stats;
+  auto st = cur_stream();
   if (want_stats) {
+    if (use_fwd_stream(p)) {   // expanding 1x1 conv: the streaming kernel (bnr_stream.h)
+      p.stats_cap = fwd_stream_groups(p);
+      stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
+      p.stats = ptr<float>(stats);
+      launch_fwd_stream(p, st);
+      return {y, stats};
+    }
     p.stats_cap = ceil_div(p.gm, igemm_bm(MODE_FWD, p));
     stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
     p.stats = ptr<float>(stats);
   }
-  auto st = cur_stream();
   if (in_scale) {   // BatchNorm-forward fold (act_sc / act_sh set above)
     dispatch<MODE_FWD>(p, st);
     if (want_stats) return {y, stats};

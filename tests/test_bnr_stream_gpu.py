@@ -118,10 +118,46 @@ def test_bnr_stream_workgroup_counts(gpu):
     """Any workgroup count (more groups than tiles, uneven tiles per group) gives the same sums."""
     a = _operands(gpu, 2, 28, 64, 256, True, False, "full", "bits", 9)
     outs = []
-    for wgs in (2, 6, 64, 1024, 8192):
+    for wgs in (2, 6, 64, 256, 1024, 8192):
         with _Knob("bnr_stream", 1), _Knob("bnr_stream_wgs", wgs):
             r = _call(_ops().conv_dgrad_bnr, 28, a, False)
         outs.append(r)
     for r in outs[1:]:
         assert torch.equal(r[0], outs[0][0])
         torch.testing.assert_close(r[1].double().sum(0), outs[0][1].double().sum(0), rtol=1e-5, atol=1e-3)
+
+
+# name, N, H, K (input channels), C (output channels), act fold
+FWD_CASES = [
+    ("l1_conv3_fold", 4, 56, 64, 256, True),
+    ("l1_down", 4, 56, 64, 256, False),
+    ("l2_conv3_fold", 8, 28, 128, 512, True),
+    ("k64_c128_fold", 8, 14, 64, 128, True),
+]
+
+
+@pytest.mark.parametrize("case", FWD_CASES, ids=lambda c: c[0])
+def test_fwd_stream_matches(gpu, case):
+    """Streaming 1x1 FWD + BatchNorm statistics (fwd_stream_kernel) == the one-tile kernels and the
+    reference (conv + relu(scale * z + shift) fold), statistics summed over the partial rows."""
+    name, N, H, K, C, fold = case
+    torch.manual_seed(3)
+    z = rnd(N, H, H, K, dev=gpu, scale=2.0)
+    w = rnd(C, 1, 1, K, dev=gpu, scale=(2.0 / K) ** 0.5)
+    sc = sh = None
+    if fold:
+        sc, sh = torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.5
+    with _Knob("fwd_stream", 1):
+        new = _ops().conv_fwd(z, w, 1, 0, None, None, False, True, sc, sh)
+        again = _ops().conv_fwd(z, w, 1, 0, None, None, False, True, sc, sh)
+    with _Knob("fwd_stream", 0):
+        old = _ops().conv_fwd(z, w, 1, 0, None, None, False, True, sc, sh)
+    rr = ref.conv_fwd(z, w, 1, 0, None, None, False, True, sc, sh)
+    for t0, t1 in zip(new, again):
+        assert torch.equal(t0, t1), "fwd_stream: not run-to-run deterministic"
+    close(new[0], rr[0])
+    d = (new[0].float() - old[0].float()).abs()
+    assert int((d > 1e-2 * old[0].float().abs() + 1e-3 * old[0].float().abs().max()).sum()) == 0
+    torch.testing.assert_close(new[1].double().sum(0), old[1].double().sum(0), rtol=2e-3, atol=5e-1)
+    torch.testing.assert_close(new[1].double().sum(0), rr[1].double().sum(0), rtol=1e-2, atol=2.0)
+    assert new[1].shape[0] <= 512   # the streaming kernel ran (one statistics row per workgroup group)

@@ -25,6 +25,9 @@ CASES = [
     ("l2b1_conv1_dual", 256, 28, 128, 512, False, True, "full", "bits"),        # 1
     ("l3b0_conv1_sub", 256, 28, 256, 512, False, False, "sub", "bits"),         # 1
     ("l2_conv3_mfx", 256, 28, 512, 128, False, False, "none", "mfx"),           # (K=512: not eligible)
+    ("l3_conv1", 256, 14, 256, 1024, False, False, "full", "bits"),             # 4
+    ("l3b1_conv1_dual", 256, 14, 256, 1024, False, True, "full", "bits"),       # 1
+    ("l3_conv3_mfx", 256, 14, 1024, 256, False, False, "none", "mfx"),          # (K=1024: not eligible)
 ]
 
 
@@ -73,7 +76,8 @@ def timeit(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--wgs", default="1024")
+    ap.add_argument("--wgs", default="512")
+    ap.add_argument("--only", default="")
     a = ap.parse_args()
     assert _lib.load(), _lib.load_error()
     ops = torch.ops.pcmp
@@ -83,6 +87,8 @@ def main():
     print(f"{'case':26s} " + " ".join(f"{n:>22s}" for n, _ in variants))
     tot = {n: 0.0 for n, _ in variants}
     for case in CASES:
+        if a.only and not any(o in case[0] for o in a.only.split(",")):
+            continue
         args, nbytes = operands(dev, *case[1:])
         best = {n: 1e30 for n, _ in variants}
         for _ in range(a.rounds):
