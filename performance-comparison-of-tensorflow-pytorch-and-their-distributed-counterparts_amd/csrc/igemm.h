@@ -3406,5 +3406,10 @@ void conv_wgrad(const at::Tensor& dy, const at::Tensor& x, at::Tensor out, int64
                 int64_t stride, int64_t pad, bool accumulate, const c10::optional<at::Tensor>& fold_x,
                 const c10::optional<at::Tensor>& fold_coef, const c10::optional<at::Tensor>& in_scale,
                 const c10::optional<at::Tensor>& in_shift);
+std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& g, const c10::optional<at::Tensor>& fold_x,
+                                          const c10::optional<at::Tensor>& fold_coef, const at::Tensor& wt,
+                                          const at::Tensor& z, const at::Tensor& scale, const at::Tensor& shift,
+                                          const at::Tensor& mean, const at::Tensor& invstd, at::Tensor dw,
+                                          bool accumulate);
 
 }  // namespace pcmp

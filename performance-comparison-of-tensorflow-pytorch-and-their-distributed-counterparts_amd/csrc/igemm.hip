@@ -108,6 +108,9 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("conv_wgrad(Tensor dy, Tensor x, Tensor(a!) out, int R, int S, int stride, int pad, bool accumulate, "
         "Tensor? fold_x=None, Tensor? fold_coef=None, Tensor? in_scale=None, Tensor? in_shift=None) -> ()",
         &pcmp::conv_wgrad);
+  m.def("conv1x1_bwd_fused(Tensor g, Tensor? fold_x, Tensor? fold_coef, Tensor wt, Tensor z, Tensor scale, "
+        "Tensor shift, Tensor mean, Tensor invstd, Tensor(a!) dw, bool accumulate) -> Tensor[]",
+        &pcmp::conv1x1_bwd_fused);
   m.def("linear_gelu_fwd(Tensor x, Tensor w, Tensor? bias) -> Tensor[]", &pcmp::linear_gelu_fwd);
   m.def("linear_dgrad_gelu(Tensor dy, Tensor w, Tensor u, Tensor? wt=None) -> Tensor", &pcmp::linear_dgrad_gelu);
 }

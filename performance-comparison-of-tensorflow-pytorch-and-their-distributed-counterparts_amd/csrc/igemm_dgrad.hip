@@ -3,6 +3,7 @@
 // DGRAD entry points (split from igemm.hip in round 4 so the three modes compile in parallel).
 #include "igemm.h"
 #include "bnr_stream.h"
+#include "bwd_fused.h"
 
 namespace pcmp {
 
@@ -292,6 +293,69 @@ std::vector<at::Tensor> conv_dgrad_bnr(const at::Tensor& dy, const at::Tensor& w
     a.fold_x = ptr<__bf16>(*fold_x); a.fold_coef = ptr<float>(*fold_coef);
   }
   return dgrad_impl(dy, w, H, W, stride, pad, resid, &a, wt, nullptr, resid_sub);
+}
+
+// Fused backward of a 1x1 stride-1 conv whose input is relu(BN(z)) (bwd_fused.h): returns [g_in, part]
+// (conv_dgrad_bnr's outputs for that BN, mask recomputed from z) and writes dW into `dw` (fp32
+// [K,1,1,C], accumulate optional).  g: [N,H,W,K] masked BN-input gradient with fold_x / fold_coef (the
+// BatchNorm-backward fold of the conv's output BN), or dz itself; wt: [C,1,1,K] transposed weight.
+std::vector<at::Tensor> conv1x1_bwd_fused(const at::Tensor& g, const c10::optional<at::Tensor>& fold_x,
+                                          const c10::optional<at::Tensor>& fold_coef, const at::Tensor& wt,
+                                          const at::Tensor& z, const at::Tensor& scale, const at::Tensor& shift,
+                                          const at::Tensor& mean, const at::Tensor& invstd, at::Tensor dw,
+                                          bool accumulate) {
+  PCMP_CHECK_CUDA(g); PCMP_CHECK_BF16(g); PCMP_CHECK_CONTIG(g);
+  PCMP_CHECK_BF16(wt); PCMP_CHECK_CONTIG(wt); PCMP_CHECK_BF16(z); PCMP_CHECK_CONTIG(z);
+  PCMP_CHECK_F32(dw); PCMP_CHECK_CONTIG(dw);
+  for (const at::Tensor* t : {&scale, &shift, &mean, &invstd}) { PCMP_CHECK_F32(*t); PCMP_CHECK_CONTIG(*t); }
+  const int64_t KC = g.size(-1), CC = z.size(-1);
+  const int64_t M = g.numel() / KC;
+  TORCH_CHECK(KC == 256 && CC == 64, "conv1x1_bwd_fused: the 64 -> 256 channel geometry only");
+  TORCH_CHECK(z.numel() == M * CC && wt.numel() == KC * CC && dw.numel() == KC * CC && M % 32 == 0,
+              "conv1x1_bwd_fused: shapes");
+  const bool fold = fold_x.has_value() && fold_x->defined();
+  if (fold) {
+    PCMP_CHECK_BF16(*fold_x); PCMP_CHECK_CONTIG(*fold_x);
+    TORCH_CHECK(fold_x->numel() == g.numel() && fold_coef.has_value() && fold_coef->numel() == 3 * KC,
+                "conv1x1_bwd_fused: fold_x / fold_coef");
+  }
+  BwdFusedParams p;
+  p.g = ptr<__bf16>(g);
+  p.fx = fold ? ptr<__bf16>(*fold_x) : nullptr;
+  p.fcoef = fold ? ptr<float>(*fold_coef) : nullptr;
+  p.wt = ptr<__bf16>(wt); p.z = ptr<__bf16>(z);
+  p.sc = ptr<float>(scale); p.sh = ptr<float>(shift); p.mean = ptr<float>(mean); p.istd = ptr<float>(invstd);
+  p.M = (int)M;
+  p.g_bytes = tensor_bytes(g); p.z_bytes = tensor_bytes(z); p.wt_bytes = tensor_bytes(wt);
+  const int groups = std::max(1, std::min((int)(M / 32), kn_bwd_fused_wgs.get()));
+  auto gout = at::empty_like(z);
+  auto part = at::empty({groups, 2, CC}, g.options().dtype(at::kFloat));
+  auto ws = at::empty({groups, KC * CC}, g.options().dtype(at::kFloat));
+  p.gout = ptr<__bf16>(gout); p.part = ptr<float>(part); p.dw = ptr<float>(ws);
+  constexpr size_t smem = (size_t)64 * 256 * 2 + 2 * ((size_t)32 * 256 * 2 * 2 + 32 * 64 * 2) + 32 * 64 * 2 +
+                          (size_t)32 * 72 * 4 + 3 * 256 * 4;
+  static_assert(smem <= 160 * 1024, "bwd_fused: LDS");
+  auto st = cur_stream();
+  auto launch = [&](auto kf) {
+    static bool attr = false;
+    if (!attr) {
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(kf, dim3(groups), dim3(256), smem, st, p, groups);
+    PCMP_LAUNCH_CHECK();
+  };
+  if (fold) launch(&bwd_fused_kernel<256, 64, true>); else launch(&bwd_fused_kernel<256, 64, false>);
+  // dW = sum of the workgroup partials, in a fixed order (deterministic)
+  const int n4 = (int)(KC * CC / 4);
+  const int SL = groups <= 8 ? 1 : (groups <= 32 ? 4 : 16);
+  const dim3 grid(ceil_div(n4, 256 / SL));
+  if (SL == 1) hipLaunchKernelGGL(splitk_reduce2_kernel<1>, grid, dim3(256), 0, st, ptr<float>(ws), ptr<float>(dw), n4, groups, (int)accumulate);
+  else if (SL == 4) hipLaunchKernelGGL(splitk_reduce2_kernel<4>, grid, dim3(256), 0, st, ptr<float>(ws), ptr<float>(dw), n4, groups, (int)accumulate);
+  else hipLaunchKernelGGL(splitk_reduce2_kernel<16>, grid, dim3(256), 0, st, ptr<float>(ws), ptr<float>(dw), n4, groups, (int)accumulate);
+  PCMP_LAUNCH_CHECK();
+  return {gout, part};
 }
 
 }  // namespace pcmp

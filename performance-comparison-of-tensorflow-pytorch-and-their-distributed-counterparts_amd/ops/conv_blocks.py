@@ -245,6 +245,37 @@ def _bn_backward(dy, ymask, x, mean, invstd, L, x2=None, mean2=None, invstd2=Non
     return outs, grads
 
 
+def _fused_conv_bwd(L, dh, a, st, grads):
+    """The layer-1 conv3 backward as ONE kernel (``conv1x1_bwd_fused``, csrc/bwd_fused.h): its DGRAD with
+    the previous BN's reduction AND its WGRAD, reading dz (or its BatchNorm-backward fold g, x) and the
+    folded input relu(BN(z)) once instead of once per GEMM (the layer is HBM-bound; the separate
+    side-stream WGRAD re-read 1.15 KB per pixel).  Returns conv_dgrad_bnr's [g, part] (the weight
+    gradient is emitted here), or None where the shape / path does not apply.  PCMP_BWD_FUSED=0: off."""
+    if os.environ.get("PCMP_BWD_FUSED", "1") == "0" or not isinstance(a, _Act):
+        return None
+    if not (L.R == 1 and L.S == 1 and L.stride == 1 and L.pad == 0):
+        return None
+    g, fx, fc = _fold_args(dh)
+    if not (g.is_cuda and g.dtype == torch.bfloat16 and g.shape[-1] == 256 and a.z.shape[-1] == 64
+            and (g.numel() // 256) % 32 == 0):
+        return None
+    w = L.weight
+    if not w.requires_grad:
+        return None
+    wt = compute_weight_t(w, g.dtype)
+    if wt is None:   # no flat arena: transpose the (small) compute weight here
+        wc = compute_weight(w, g.dtype)
+        wt = wc.reshape(wc.shape[0], -1).t().contiguous()
+    mean, istd = st
+    res = []
+
+    def fill(out, acc):
+        res.append(K.conv1x1_bwd_fused(g, fx, fc, wt, a.z, a.scale, a.shift, mean, istd, out, acc))
+
+    grads[w] = emit_grad(w, fill)
+    return res[0]
+
+
 def _bnr_ok(L):
     """Fused dgrad+BN-reduce needs every input pixel produced by an epilogue (stride-2 sub-pixel
     classes without taps would be skipped)."""
@@ -531,7 +562,9 @@ class ResidualBlockFn(torch.autograd.Function):
                                           (dcd, wd, wdt))
         for i in range(len(main) - 1, -1, -1):
             L = main[i]
-            _wgrad(L, dh, acts[i], grads)
+            r_fused = _fused_conv_bwd(L, dh, acts[i], stats[i - 1], grads) if (i > 0 and _bnr_ok(L)) else None
+            if r_fused is None:
+                _wgrad(L, dh, acts[i], grads)
             dtype = _fold_args(dh)[0].dtype
             wcomp = compute_weight(L.weight, dtype)
             wt = compute_weight_t(L.weight, dtype)
@@ -543,8 +576,11 @@ class ResidualBlockFn(torch.autograd.Function):
                     # the ReLU mask of acts[i] = relu(cs[i-1] * scale + shift) is recomputed from cs[i-1]
                     sc_prev, sh_prev = ctx.coefs[i - 1]
                     g, fx, fc = _fold_args(dh)
-                    r = K.conv_dgrad_bnr(g, wcomp, Hi, Wi, L.stride, L.pad, None, None, cs[i - 1],
-                                         m_prev, is_prev, None, None, None, sc_prev, sh_prev, wt, None, fx, fc)
+                    if r_fused is not None:
+                        r = r_fused
+                    else:
+                        r = K.conv_dgrad_bnr(g, wcomp, Hi, Wi, L.stride, L.pad, None, None, cs[i - 1],
+                                             m_prev, is_prev, None, None, None, sc_prev, sh_prev, wt, None, fx, fc)
                     # conv1's dz folds when every consumer can: its WGRAD, and its DGRAD only on the
                     # fused into-previous-block path
                     fold = (i - 1 == 0 and _fold_ok(main[0], r[0]) and (not need_dx or prev0 is not None))

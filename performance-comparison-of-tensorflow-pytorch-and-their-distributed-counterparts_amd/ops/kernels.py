@@ -16,7 +16,7 @@ from . import _lib, ref
 TRACE = [] if os.environ.get("PCMP_TRACE_OPS") else None
 
 OP_NAMES = (
-    "conv_fwd", "conv_dgrad", "conv_dgrad_bnr", "conv_wgrad",
+    "conv_fwd", "conv_dgrad", "conv_dgrad_bnr", "conv_wgrad", "conv1x1_bwd_fused",
     "bn_partials", "bn_finalize", "bn_eval_coeff", "bn_apply", "bn_bwd_reduce", "bn_bwd_finalize",
     "bn_bwd_apply",
     "maxpool_fwd", "maxpool_bwd", "maxpool_bwd_bnr", "gap_fwd", "gap_bwd", "softmax_xent", "loss_mean", "xent_grad_scale", "log_softmax_bwd", "dropout", "relu_bwd", "colsum",

@@ -100,6 +100,18 @@ def conv_wgrad(dy, x, out, R, S, stride, pad, accumulate, fold_x=None, fold_coef
         out.copy_(dw)
 
 
+def conv1x1_bwd_fused(g, fold_x, fold_coef, wt, z, scale, shift, mean, invstd, dw, accumulate):
+    """Fused 1x1 conv backward (csrc/bwd_fused.h): the DGRAD + BN-reduce of the input BN (mask
+    recomputed from z) and the WGRAD against relu(scale * z + shift), from the same dz."""
+    dz = fold_dz(g, fold_x, fold_coef) if fold_x is not None else g
+    K, C = dz.shape[-1], z.shape[-1]
+    w = wt.reshape(C, K).t().contiguous().reshape(K, 1, 1, C)
+    r = conv_dgrad_bnr(dz, w, z.shape[1], z.shape[2], 1, 0, None, None, z, mean, invstd, None, None, None,
+                       scale, shift)
+    conv_wgrad(dz, z, dw, 1, 1, 1, 0, accumulate, None, None, scale, shift)
+    return r
+
+
 # ------------------------------------------------------------------------------ batchnorm
 def bn_partials(x):
     xr = x.float().reshape(-1, x.shape[-1])

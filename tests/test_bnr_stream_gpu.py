@@ -161,3 +161,43 @@ def test_fwd_stream_matches(gpu, case):
     torch.testing.assert_close(new[1].double().sum(0), old[1].double().sum(0), rtol=2e-3, atol=5e-1)
     torch.testing.assert_close(new[1].double().sum(0), rr[1].double().sum(0), rtol=1e-2, atol=2.0)
     assert new[1].shape[0] <= 512   # the streaming kernel ran (one statistics row per workgroup group)
+
+
+@pytest.mark.parametrize("fold", [True, False])
+@pytest.mark.parametrize("acc", [False, True])
+def test_conv1x1_bwd_fused_matches(gpu, fold, acc):
+    """conv1x1_bwd_fused (csrc/bwd_fused.h) == the reference composition (DGRAD + BN reduce with the mask
+    recomputed from z, WGRAD against relu(scale * z + shift)) and == the separate HIP kernels."""
+    torch.manual_seed(7)
+    N, H, K, C = 4, 28, 256, 64
+    g = rnd(N, H, H, K, dev=gpu)
+    fx = coef = None
+    if fold:
+        fx = rnd(N, H, H, K, dev=gpu, scale=2.0) + 0.5
+        coef = torch.stack([torch.rand(K, device=gpu) + 0.5, torch.randn(K, device=gpu) * 0.05,
+                            torch.randn(K, device=gpu) * 0.1]).contiguous()
+    w = rnd(K, 1, 1, C, dev=gpu, scale=(2.0 / K) ** 0.5)
+    wt = w.reshape(K, C).t().contiguous().reshape(C, 1, 1, K)
+    z = rnd(N, H, H, C, dev=gpu, scale=2.0)
+    sc, sh = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu) * 0.5
+    mean, istd = torch.randn(C, device=gpu) * 0.1, torch.rand(C, device=gpu) + 0.5
+    base = torch.randn(K, 1, 1, C, device=gpu) if acc else torch.zeros(K, 1, 1, C, device=gpu)
+    dw = base.clone()
+    r = _ops().conv1x1_bwd_fused(g, fx, coef, wt, z, sc, sh, mean, istd, dw, acc)
+    dw2 = base.clone()
+    r2 = _ops().conv1x1_bwd_fused(g, fx, coef, wt, z, sc, sh, mean, istd, dw2, acc)
+    assert torch.equal(r[0], r2[0]) and torch.equal(r[1], r2[1]) and torch.equal(dw, dw2), "not deterministic"
+    dwr = base.clone()
+    rr = ref.conv1x1_bwd_fused(g, fx, coef, wt, z, sc, sh, mean, istd, dwr, acc)
+    close(r[0], rr[0])
+    torch.testing.assert_close(r[1].double().sum(0), rr[1].double().sum(0), rtol=1e-2, atol=1.0)
+    close(dw, dwr, rtol=1e-2, atol=1e-2)
+    # the separate kernels (the path this replaces)
+    dws = base.clone()
+    _ops().conv_wgrad(g, z, dws, 1, 1, 1, 0, acc, fx, coef, sc, sh)
+    rs = _ops().conv_dgrad_bnr(g, w, H, H, 1, 0, None, None, z, mean, istd, None, None, None, sc, sh, wt, None, fx,
+                               coef)
+    d = (r[0].float() - rs[0].float()).abs()
+    assert int((d > 1e-2 * rs[0].float().abs() + 1e-3 * rs[0].float().abs().max()).sum()) == 0
+    torch.testing.assert_close(r[1].double().sum(0), rs[1].double().sum(0), rtol=2e-3, atol=2e-1)
+    close(dw, dws, rtol=2e-3, atol=2e-3)

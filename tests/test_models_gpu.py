@@ -204,3 +204,35 @@ def test_bottleneck_dz_fold_matches(gpu, monkeypatch, cfg):
     assert _rel(outs["1"][1], outs["0"][1]) < 2e-2
     for n, gr in outs["0"][2].items():
         assert _rel(outs["1"][2][n], gr) < 2e-2, (n, _rel(outs["1"][2][n], gr))
+
+
+@pytest.mark.parametrize("fold", ["0", "1"])
+def test_bottleneck_fused_conv3_backward_matches(gpu, monkeypatch, fold):
+    """The fused conv3 backward (conv1x1_bwd_fused: DGRAD + BN reduce + WGRAD in one streaming kernel,
+    PCMP_BWD_FUSED) == the separate conv_dgrad_bnr + side-stream conv_wgrad, to bf16 / summation-order
+    noise, on two chained layer-1 bottlenecks with the forward activation fold (and with / without the
+    BatchNorm-backward fold of the conv3 gradient)."""
+    from pcmp.models.resnet import Bottleneck
+    torch.manual_seed(1)
+    b1 = Bottleneck(64, 64, 1).to(gpu).train()
+    b2 = Bottleneck(256, 64, 1).to(gpu).train()
+    x = (torch.randn(4, 28, 28, 64, device=gpu) * 0.5).to(torch.bfloat16).requires_grad_(True)
+    g = torch.randn(4, 28, 28, 256, device=gpu).to(torch.bfloat16)
+    params = list(b1.named_parameters()) + [("b2." + n, p) for n, p in b2.named_parameters()]
+    monkeypatch.setenv("PCMP_DZ_FOLD_MINROWS", "0")
+    monkeypatch.setenv("PCMP_ACT_FOLD_MINROWS", "0")
+    monkeypatch.setenv("PCMP_DZ_FOLD", fold)
+    monkeypatch.setenv("PCMP_ACT_FOLD", "1")
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("PCMP_BWD_FUSED", v)
+        for _, p in params:
+            p.grad = None
+        x.grad = None
+        y = b2(b1(x))
+        y.backward(g)
+        torch.cuda.synchronize()
+        outs[v] = (x.grad.detach().clone(), {n: p.grad.detach().clone() for n, p in params if p.grad is not None})
+    assert _rel(outs["1"][0], outs["0"][0]) < 1e-2
+    for n, gr in outs["0"][1].items():
+        assert _rel(outs["1"][1][n], gr) < 1e-2, (n, _rel(outs["1"][1][n], gr))
