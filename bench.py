@@ -32,7 +32,8 @@ status: a ``--gpus 8`` run never reports a one-GPU number.  Under a launcher, ``
 ``WORLD_SIZE`` or the run fails.  The JSON line proves the communicator's size (``comm.world_check``
 = an all-reduce of ones over the process group) and reports the gradient buckets and the exposed
 (non-overlapped) all-reduce time per step (``comm.exposed_ms``: from the compute stream reaching
-the end of backward to the last collective finishing, CUDA events, mean over the timed steps).
+the end of backward to the last bucket's collective and optimizer update finishing, CUDA events,
+mean over 4 instrumented steps run AFTER the timed loop -- the timing events cost step time).
 
 The learning rate ramps linearly over the warm-up steps to ``--lr`` and stays constant in the timed
 steps (no per-step host work in the timed region); ``final_loss`` (the loss of the last timed step on
@@ -80,6 +81,9 @@ def parse():
                          "after warm-up and replay it (hip impl, one rank)")
     ap.add_argument("--ddp-force", action="store_true",
                     help="RCCL process group + bucket all-reduces even at one rank (exercises the comm path)")
+    ap.add_argument("--opt-after-join", action="store_true",
+                    help="DDP: one whole-arena SGD update after the last all-reduce instead of the per-bucket "
+                         "update as each all-reduce completes (the A/B baseline of the per-bucket optimizer)")
     ap.add_argument("--grad-dtype", default=None, choices=["fp32", "bf16"],
                     help="gradient all-reduce dtype (default fp32, exact)")
     ap.add_argument("--infer-images", type=int, default=200,
@@ -157,7 +161,7 @@ def build_hip(args, env):
     opt = SGD(flat, lr=args.lr, momentum=0.9, weight_decay=5e-5)
     use_ddp = env.world_size > 1 or (args.ddp_force and env.backend is not None)
     ddp = DistributedDataParallel(model, flat, force=args.ddp_force, grad_dtype=args.grad_dtype) if use_ddp else None
-    if ddp is not None:
+    if ddp is not None and args.opt_after_join:
         opt.set_grad_scale(ddp.grad_scale())
 
     # host run-ahead bound (PCMP_MAX_INFLIGHT steps): keeps the caching allocator's footprint at a
@@ -179,9 +183,12 @@ def build_hip(args, env):
         logits = model.forward_logits(x)
         loss = cross_entropy(logits, y)
         loss.backward()
-        if ddp is not None:
-            ddp.finish_gradient_sync()
-        opt.step()
+        if ddp is not None and not args.opt_after_join:
+            ddp.finish_gradient_sync(opt=opt)   # per-bucket SGD as each all-reduce completes
+        else:
+            if ddp is not None:
+                ddp.finish_gradient_sync()
+            opt.step()
         throttle.tick()
         return loss
 
@@ -297,8 +304,6 @@ def main():
         sync_autotune()
     if opt is not None:
         opt.set_lr(args.lr)
-    if ddp is not None:
-        ddp.time_exposed(True)
     graphed = bool(args.graph and args.impl == "hip" and env.world_size == 1 and env.device.type == "cuda")
     if graphed:
         step = graph_step(step, x, y)
@@ -317,8 +322,17 @@ def main():
     sync()
     dt = time.perf_counter() - t0
     comm = {"backend": env.backend, "world_check": world_check}
-    if ddp is not None:
+    if ddp is not None and not graphed:
+        # the exposed-communication / per-bucket timeline instrumentation (timing events on the
+        # compute, comm and timeline streams) runs on extra steps AFTER the timed loop: inside it,
+        # it slowed the forced-RCCL step 18.6 -> 28.0 ms (profiles/r6_rccl_steps.txt)
+        ddp.time_exposed(True)
+        for _ in range(4):
+            step(x, y)           # final_loss stays the last TIMED step's
+        sync()
         comm.update(ddp.comm_report())
+        comm["comm_timing_steps"] = "4 extra steps after the timed loop"
+        ddp.time_exposed(False)
     if prof is not None:
         prof.__exit__(None, None, None)
         prof.export_chrome_trace(args.profile)

@@ -173,6 +173,28 @@ std::vector<at::Tensor> grad_clip_coef(const at::Tensor& g, double pre_scale, do
   return {out[0], out[1]};
 }
 
+// Two-phase global-norm clip for the per-bucket optimizer (parallel/ddp.py): each gradient bucket's
+// block partial sums of squares go to part[offset, offset + flat_grid(n)) as soon as that bucket's
+// all-reduce completes; clip_coef_parts then reduces every bucket's partials in one launch.
+void grad_sumsq_parts(const at::Tensor& g, at::Tensor part, int64_t offset) {
+  PCMP_CHECK_F32(g); PCMP_CHECK_F32(part);
+  const int64_t n = g.numel();
+  TORCH_CHECK(n % 4 == 0, "grad_sumsq_parts: numel % 4");
+  const int nb = flat_grid(n);
+  TORCH_CHECK(offset >= 0 && offset + nb <= part.numel(), "grad_sumsq_parts: partial buffer too small");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, cur_stream(), ptr<float>(g), n, ptr<float>(part) + offset);
+  PCMP_LAUNCH_CHECK();
+}
+
+std::vector<at::Tensor> clip_coef_parts(const at::Tensor& part, double pre_scale, double max_norm, double post_scale) {
+  PCMP_CHECK_F32(part);
+  auto out = at::empty({2}, part.options());
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, cur_stream(), ptr<float>(part), (int)part.numel(),
+                     (float)pre_scale, (float)max_norm, (float)post_scale, ptr<float>(out), ptr<float>(out) + 1);
+  PCMP_LAUNCH_CHECK();
+  return {out[0], out[1]};
+}
+
 void cast_to_bf16(const at::Tensor& x, at::Tensor y) {
   PCMP_CHECK_F32(x); PCMP_CHECK_BF16(y);
   TORCH_CHECK(x.numel() == y.numel() && x.is_contiguous() && y.is_contiguous(), "cast_to_bf16: shapes");
@@ -193,5 +215,8 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
         &pcmp::adam_flat);
   m.def("grad_clip_coef(Tensor g, float pre_scale, float max_norm, float post_scale) -> Tensor[]",
         &pcmp::grad_clip_coef);
+  m.def("grad_sumsq_parts(Tensor g, Tensor(a!) part, int offset) -> ()", &pcmp::grad_sumsq_parts);
+  m.def("clip_coef_parts(Tensor part, float pre_scale, float max_norm, float post_scale) -> Tensor[]",
+        &pcmp::clip_coef_parts);
   m.def("cast_to_bf16(Tensor x, Tensor(a!) y) -> ()", &pcmp::cast_to_bf16);
 }

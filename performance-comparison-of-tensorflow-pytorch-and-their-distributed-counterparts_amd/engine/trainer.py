@@ -69,17 +69,19 @@ class TrainState:
         with self.phase("backward"):
             loss.backward()
         if self.ddp is not None:
-            with self.phase("comm"):     # join of the bucket all-reduces overlapped with backward
-                self.ddp.finish_gradient_sync()
-        with self.phase("optimizer"):
-            scale = self.ddp.grad_scale() if self.ddp is not None else 1.0
-            if self.clip is not None:
-                self.opt.clip_grad_norm(self.clip, pre_scale=scale, post_scale=scale)
-            else:
-                self.opt.set_grad_scale(scale if scale != 1.0 else None)
-            self.opt.step()
-            if self.sched is not None:
-                self.sched.step()
+            # join of the bucket all-reduces overlapped with backward, and the optimizer step issued
+            # per bucket as each all-reduce completes (two-phase clip when clipping)
+            with self.phase("comm+optimizer"):
+                self.ddp.finish_gradient_sync(opt=self.opt, clip=self.clip)
+        else:
+            with self.phase("optimizer"):
+                if self.clip is not None:
+                    self.opt.clip_grad_norm(self.clip)
+                else:
+                    self.opt.set_grad_scale(None)
+                self.opt.step()
+        if self.sched is not None:
+            self.sched.step()
         if self.timer is not None:
             self.timer.step()
         if self.throttle is not None:

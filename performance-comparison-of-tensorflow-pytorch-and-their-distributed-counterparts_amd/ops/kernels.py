@@ -21,7 +21,7 @@ OP_NAMES = (
     "bn_bwd_apply",
     "maxpool_fwd", "maxpool_bwd", "maxpool_bwd_bnr", "gap_fwd", "gap_bwd", "softmax_xent", "loss_mean", "xent_grad_scale", "log_softmax_bwd", "dropout", "relu_bwd", "colsum",
     "nchw_to_nhwc", "nchw_to_nhwc_f32", "image_to_s2d", "image_to_s2d_f32", "resize_image",
-    "sgd_flat", "adam_flat", "grad_clip_coef", "cast_to_bf16", "wt_transpose_multi",
+    "sgd_flat", "adam_flat", "grad_clip_coef", "grad_sumsq_parts", "clip_coef_parts", "cast_to_bf16", "wt_transpose_multi",
     "embedding_fwd", "embedding_bwd", "lstm_seq_fwd", "lstm_seq_bwd",
     "masked_mean_fwd", "masked_mean_bwd",
     "layernorm_fwd", "embed_layernorm_fwd", "layernorm_bwd", "layernorm_bwd_fused", "gelu_fwd", "gelu_bwd",

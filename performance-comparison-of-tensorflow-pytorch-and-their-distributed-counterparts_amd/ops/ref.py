@@ -472,6 +472,23 @@ def grad_clip_coef(g, pre_scale, max_norm, post_scale):
     return [norm.reshape(()), (c * post_scale).reshape(())]
 
 
+def sumsq_blocks(n):
+    """Partial-sum rows grad_sumsq_parts writes for an n-element slice (csrc/optim.hip flat_grid)."""
+    return max(1, min(2048, (n // 4 + 255) // 256))
+
+
+def grad_sumsq_parts(g, part, offset):
+    nb = sumsq_blocks(g.numel())
+    part[offset:offset + nb] = 0.0
+    part[offset] = g.double().pow(2).sum().float()
+
+
+def clip_coef_parts(part, pre_scale, max_norm, post_scale):
+    norm = part.double().sum().sqrt().float() * pre_scale
+    c = torch.clamp(max_norm / (norm + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(norm)
+    return [norm.reshape(()), (c * post_scale).reshape(())]
+
+
 def cast_to_bf16(x, y):
     y.copy_(x.to(y.dtype))
 

@@ -57,6 +57,24 @@ class _FlatOptimizer:
         else:
             self.grad_scale = torch.tensor([float(scale)], device=self.flat.device)
 
+    # ---- ranged steps: DistributedDataParallel.finish_gradient_sync(opt=...) updates each gradient
+    # bucket as soon as its all-reduce completes: begin_step(), step_range() per flat slice, end_step().
+    # The same elementwise kernel over a sub-range: bitwise equal to step() over the whole arena.
+    def begin_step(self):
+        pass
+
+    def step_range(self, lo: int, hi: int):
+        raise NotImplementedError
+
+    def end_step(self):
+        self.steps += 1
+        bump_weight_gen()
+
+    def step(self):
+        self.begin_step()
+        self.step_range(0, self.flat.numel)
+        self.end_step()
+
     def state_dict(self):
         return {"lr": self._lr, "steps": self.steps, "state": {k: v.detach().clone() for k, v in self._state().items()}}
 
@@ -76,16 +94,11 @@ class SGD(_FlatOptimizer):
         self.momentum, self.dampening, self.wd, self.nesterov = momentum, dampening, weight_decay, nesterov
         self.mom = torch.zeros_like(flat.master) if momentum != 0 else flat.master.new_empty(0)
 
-    def _sgd(self, lo, hi):
+    def step_range(self, lo, hi):
         f = self.flat
         K.sgd_flat(f.master[lo:hi], f.grad[lo:hi], self.mom[lo:hi] if self.mom.numel() else self.mom,
                    f.shadow[lo:hi] if f.shadow is not None else None, None, self.lr_t, self.grad_scale,
                    self.momentum, self.dampening, self.wd, self.nesterov, self.steps == 0)
-
-    def step(self):
-        self._sgd(0, self.flat.numel)
-        self.steps += 1
-        bump_weight_gen()
 
     def _state(self):
         return {"mom": self.mom}
@@ -102,12 +115,14 @@ class Adam(_FlatOptimizer):
         self.m2 = torch.zeros_like(flat.master)
         self.step_t = torch.zeros(1, dtype=torch.float32, device=flat.device)
 
-    def step(self):
+    def begin_step(self):
         self.step_t.add_(1.0)
-        K.adam_flat(self.flat.master, self.flat.grad, self.m1, self.m2, self.flat.shadow, None, self.lr_t,
-                    self.grad_scale, self.step_t, self.beta1, self.beta2, self.eps, self.wd, self.decoupled)
-        bump_weight_gen()
-        self.steps += 1
+
+    def step_range(self, lo, hi):
+        f = self.flat
+        K.adam_flat(f.master[lo:hi], f.grad[lo:hi], self.m1[lo:hi], self.m2[lo:hi],
+                    f.shadow[lo:hi] if f.shadow is not None else None, None, self.lr_t, self.grad_scale,
+                    self.step_t, self.beta1, self.beta2, self.eps, self.wd, self.decoupled)
 
     def _state(self):
         return {"m1": self.m1, "m2": self.m2, "step_t": self.step_t}

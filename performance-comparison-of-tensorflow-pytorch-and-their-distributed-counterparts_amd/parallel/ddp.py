@@ -17,6 +17,14 @@ synchronised data parallelism the north star asks for:
   channel chunks stays >= ~256 KB at world 8, and a small LAST bucket (default
   4 MB): the last bucket's all-reduce cannot overlap anything (it waits for the stem's gradient,
   the end of backward), so only a few MB stay exposed instead of up to a whole 32 MB bucket;
+* a parameter larger than a bucket (BERT's 23.4 M-element word embedding: 94 MB fp32) is split
+  into bucket-sized chunks (``split_param_mb``, default max(bucket, 8 MB)), each its own bucket, so its all-reduce streams in pieces instead of one
+  94 MB collective that nothing after it can overlap;
+* the optimizer runs PER BUCKET (``finish_gradient_sync(opt=...)``): each bucket's slice of the flat
+  arena is updated by the fused optimizer kernel on the comm stream as soon as that bucket's
+  all-reduce completes, overlapping the later buckets' collectives, instead of one update after the
+  last bucket.  With global-norm clipping the sum of squares is the per-bucket part (two-phase clip:
+  per-bucket partial sums as the collectives complete, then one coefficient and one update);
 * the 1/world averaging is folded into the optimizer kernel's gradient scale (no extra pass);
 * initial parameters and buffers are broadcast from rank 0 (DDP constructor semantics);
   ``broadcast_buffers="forward"`` (or ``True``) re-broadcasts the buffers (BatchNorm running
@@ -50,20 +58,43 @@ import time
 import torch
 import torch.distributed as dist
 
+from ..ops.kernels import K
+from ..ops.ref import sumsq_blocks as _sumsq_blocks
 from ..utils.flat import FlatParams
 
 
 class _Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched", "streams", "events", "t_launch")
+    __slots__ = ("index", "start", "end", "params", "pending", "work", "launched", "streams", "events", "t_launch",
+                 "part_off")
 
     def __init__(self, index, start, end, params):
         self.index, self.start, self.end, self.params = index, start, end, params
+        self.part_off = 0       # first row of this bucket's sum-of-squares partials (two-phase clip)
         self.pending = len(params)
         self.work = None
         self.launched = False
         self.streams = {}       # stream id -> stream that wrote a gradient of this bucket this step
         self.events = {}        # stream id -> reusable event (recorded when the bucket launches)
         self.t_launch = None    # timing: comm-stream event (GPU) / host seconds (CPU) at launch
+
+
+def plan_segments(sizes, max_elems, quantum=1024):
+    """Per-parameter segments (param index, lo, hi) in arena order: a slice larger than ``max_elems``
+    is split into equal chunks (multiples of ``quantum`` elements: vector-aligned sub-slices for the
+    fused optimizer kernels), every other slice is one segment."""
+    segs = []
+    for i, n in enumerate(sizes):
+        if max_elems > 0 and n > max_elems:
+            k = -(-n // max_elems)
+            step = -(-(-(-n // k)) // quantum) * quantum
+            lo = 0
+            while lo < n:
+                hi = min(n, lo + step)
+                segs.append((i, lo, hi))
+                lo = hi
+        else:
+            segs.append((i, 0, n))
+    return segs
 
 
 def plan_buckets(sizes, first_bucket_elems, bucket_elems, last_bucket_elems=0):
@@ -102,7 +133,8 @@ class DistributedDataParallel(torch.nn.Module):
 
     def __init__(self, module: torch.nn.Module, flat: FlatParams, process_group=None, bucket_cap_mb: float = 32.0,
                  first_bucket_mb: float = 4.0, broadcast_buffers: bool | str = "init", average: bool = True,
-                 last_bucket_mb: float = 4.0, force: bool | None = None, grad_dtype: torch.dtype | str | None = None):
+                 last_bucket_mb: float = 4.0, force: bool | None = None, grad_dtype: torch.dtype | str | None = None,
+                 split_param_mb: float | None = None):
         super().__init__()
         self.module = module
         self.flat = flat
@@ -131,16 +163,29 @@ class DistributedDataParallel(torch.nn.Module):
         offs = flat.offsets + [flat.numel]
         for i in range(len(flat.params)):
             sizes.append(offs[i + 1] - offs[i])
-        ranges = plan_buckets(sizes, int(first_bucket_mb * 2 ** 20 / esz), int(bucket_cap_mb * 2 ** 20 / esz),
+        cap = int(bucket_cap_mb * 2 ** 20 / esz)
+        # parameters above max(bucket, 8 MB) are chunked (never into collectives smaller than 8 MB
+        # unless asked: a tiny test bucket must not turn every conv filter into dozens of buckets)
+        split = int((split_param_mb if split_param_mb is not None else max(bucket_cap_mb, 8.0)) * 2 ** 20 / esz)
+        segs = plan_segments(sizes, split)
+        ranges = plan_buckets([hi - lo for _, lo, hi in segs], int(first_bucket_mb * 2 ** 20 / esz), cap,
                               int(last_bucket_mb * 2 ** 20 / esz))
         self.buckets = []
-        self._bucket_of = {}
-        for bi, (i0, i1) in enumerate(ranges):
-            ps = flat.params[i0:i1]
-            b = _Bucket(bi, offs[i0], offs[i1], ps)
+        self._bucket_of = {}     # id(param) -> the buckets holding (a chunk of) its gradient
+        nparts = 0
+        for bi, (s0, s1) in enumerate(ranges):
+            pis = sorted({segs[k][0] for k in range(s0, s1)})
+            ps = [flat.params[i] for i in pis]
+            b = _Bucket(bi, offs[segs[s0][0]] + segs[s0][1], offs[segs[s1 - 1][0]] + segs[s1 - 1][2], ps)
+            b.part_off = nparts
+            nparts += _sumsq_blocks(b.end - b.start)
             self.buckets.append(b)
             for p in ps:
-                self._bucket_of[id(p)] = b
+                self._bucket_of.setdefault(id(p), []).append(b)
+        self._nparts = nparts
+        self._parts = None       # sum-of-squares partial rows of every bucket (two-phase clip)
+        self._scale_t = None     # device scalar 1/world (optimizer gradient scale)
+        self._opt_in_tail = False   # the optimizer ran per bucket inside finish_gradient_sync
         for p in flat.params:
             p._grad_ready_hook = self._on_grad_ready
         self._next_launch = 0
@@ -181,7 +226,9 @@ class DistributedDataParallel(torch.nn.Module):
         wsz = torch.tensor([], dtype=self.grad_dtype).element_size()
         rep = {"active": bool(self.active), "world": self.world, "buckets": len(self.buckets),
                "bucket_mb": [round((b.end - b.start) * esz / 2 ** 20, 2) for b in self.buckets],
-               "grad_allreduce_dtype": str(self.grad_dtype).replace("torch.", "")}
+               "grad_allreduce_dtype": str(self.grad_dtype).replace("torch.", ""),
+               # exposed_ms then spans end of backward -> last bucket's update (comm + optimizer tail)
+               "optimizer_per_bucket": bool(self._opt_in_tail)}
         vals = []
         for e in self._exposed:
             if isinstance(e, tuple):
@@ -276,17 +323,20 @@ class DistributedDataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------------------------------
     def _on_grad_ready(self, p):
-        b = self._bucket_of.get(id(p))
-        if b is None:
+        bs = self._bucket_of.get(id(p))
+        if bs is None:
             return
-        if self._comm_stream is not None:
-            s = torch.cuda.current_stream(p.device)
-            b.streams[s.cuda_stream] = s
-            if self._timing and self._ev_ref is None:    # the step's first gradient: time origin
-                self._ev_ref = torch.cuda.Event(enable_timing=True)
-                self._ev_ref.record(s)
-        b.pending -= 1
-        if b.pending == 0:
+        done = False
+        for b in bs:
+            if self._comm_stream is not None:
+                s = torch.cuda.current_stream(p.device)
+                b.streams[s.cuda_stream] = s
+                if self._timing and self._ev_ref is None:    # the step's first gradient: time origin
+                    self._ev_ref = torch.cuda.Event(enable_timing=True)
+                    self._ev_ref.record(s)
+            b.pending -= 1
+            done = done or b.pending == 0
+        if done:
             self._launch_ready()
 
     def _launch_ready(self):
@@ -329,23 +379,68 @@ class DistributedDataParallel(torch.nn.Module):
             else:
                 b.work = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
-    def finish_gradient_sync(self):
+    def _opt_scale(self):
+        """Device scalar 1/world for the optimizer's gradient scale (None when it is 1)."""
+        if self.grad_scale() == 1.0:
+            return None
+        if self._scale_t is None:
+            self._scale_t = torch.tensor([self.grad_scale()], dtype=torch.float32, device=self.flat.device)
+        return self._scale_t
+
+    def _step_whole(self, opt, clip):
+        """The optimizer step after a join without collectives: clip + one update over the arena."""
+        norm = None
+        if clip is not None:
+            s = self.grad_scale()
+            norm = opt.clip_grad_norm(clip, pre_scale=s, post_scale=s)
+        else:
+            opt.grad_scale = self._opt_scale()
+        opt.step()
+        return norm
+
+    def finish_gradient_sync(self, opt=None, clip: float | None = None):
         """Call after ``loss.backward()``: launches buckets whose params produced no gradient
         (their slices hold zeros from ``zero_grad``), then joins every outstanding all-reduce.
         GPU: the comm stream waits for RCCL, casts low-precision sums back into the fp32 arena,
-        and the compute stream waits for the comm stream once; the host never blocks."""
+        and the compute stream waits for the comm stream once; the host never blocks.
+
+        ``opt`` (a :mod:`pcmp.optim` flat optimizer): the optimizer step is issued HERE, per bucket
+        on the comm stream -- each bucket's slice is updated as soon as its all-reduce completes,
+        while later buckets are still in flight (after the end of backward: the updated weights
+        must not be read by a backward kernel still queued).  ``clip``: global-norm clipping in
+        two phases (per-bucket partial sums of squares as the collectives complete, then one
+        coefficient and one update).  The caller must NOT call ``opt.step()`` again; returns the
+        pre-clip norm (device scalar) when ``clip`` is given."""
+        issued = self.active and self.require_sync
+        if opt is not None and not issued:
+            self._finish_join()
+            return self._step_whole(opt, clip)
+        return self._finish_join(opt, clip)
+
+    def _finish_join(self, opt=None, clip=None):
         cs = self._comm_stream
         timing = self._timing and self.active and self.require_sync
-        if timing and cs is not None:
-            ev_a = torch.cuda.Event(enable_timing=True)
-            ev_a.record(torch.cuda.current_stream(cs.device))
+        main = torch.cuda.current_stream(cs.device) if cs is not None else None
+        if (timing or opt is not None) and cs is not None:
+            ev_a = torch.cuda.Event(enable_timing=timing)
+            ev_a.record(main)
+        if opt is not None:
+            self._opt_in_tail = True
         t0 = time.perf_counter()
         for b in self.buckets:
             b.pending = 0
         self._launch_ready()
         ctx = torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext()
         line = []
+        norm = None
         with ctx:
+            if opt is not None:
+                if cs is not None:
+                    cs.wait_event(ev_a)       # every backward kernel that reads the weights is done
+                opt.grad_scale = self._opt_scale()
+                opt.begin_step()
+                if clip is not None and self._parts is None:
+                    self._parts = torch.zeros(self._nparts, dtype=torch.float32, device=self.flat.device)
             for b in self.buckets:
                 if b.work is not None:
                     if timing and cs is not None and b.t_launch is not None:
@@ -363,6 +458,20 @@ class DistributedDataParallel(torch.nn.Module):
                         self.flat.grad[b.start:b.end].copy_(self._lowp[b.start:b.end])
                     b.work = None
                 b.t_launch = None
+                if opt is not None:
+                    if clip is not None:
+                        K.grad_sumsq_parts(self.flat.grad[b.start:b.end], self._parts, b.part_off)
+                    else:
+                        opt.step_range(b.start, b.end)
+            if opt is not None:
+                if clip is not None:
+                    s = self.grad_scale()
+                    norm, coef = K.clip_coef_parts(self._parts, s, clip, s)
+                    opt.grad_scale = coef
+                    opt.step_range(0, self.flat.numel)
+                    if cs is not None:
+                        norm.record_stream(main)      # the caller reads it on the compute stream
+                opt.end_step()
             if timing and cs is not None:
                 ev_b = torch.cuda.Event(enable_timing=True)
                 ev_b.record(cs)
@@ -374,8 +483,9 @@ class DistributedDataParallel(torch.nn.Module):
             self._timeline.append(_EventLine(self._ev_ref, ev_a, line))
         self._ev_ref = None
         if cs is not None:
-            torch.cuda.current_stream(cs.device).wait_stream(cs)
+            main.wait_stream(cs)
         self._reset()
+        return norm
 
     def grad_scale(self) -> float:
         return 1.0 / self.world if (self.average and self.world > 1) else 1.0

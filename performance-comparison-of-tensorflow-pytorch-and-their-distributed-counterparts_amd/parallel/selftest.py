@@ -109,6 +109,50 @@ def ddp_equivalence_worker(rank, world, port, out_dir, kind="mlp", bucket_mb=0.0
     dist.destroy_process_group()
 
 
+def per_bucket_opt_worker(rank, world, port, out_dir, opt_name="sgd", clip=None, kind="bilstm", bucket_mb=0.01):
+    """The optimizer issued per bucket inside ``finish_gradient_sync(opt=...)`` against the same
+    model trained with the join + ONE whole-arena update (``opt.step()``): with plain updates the
+    parameters must be bitwise equal after several steps (the same elementwise kernel over
+    sub-ranges); with global-norm clipping (two-phase sum of squares) equal to fp32 rounding of the
+    coefficient.  ``kind='bilstm'`` at ``bucket_mb=0.01`` also splits the embedding table (the
+    largest parameter) into several bucket chunks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from .. import optim
+    from ..utils.flat import FlatParams
+    from .ddp import DistributedDataParallel
+    x, y = _batch(kind, 8 * world)
+    shard = slice(rank * 8, (rank + 1) * 8)
+    masters, nchunks = [], 0
+    for per_bucket in (False, True):
+        model = _build(kind, seed=rank)
+        flat = FlatParams(model.parameters(), shadow_dtype=None)
+        ddp = DistributedDataParallel(model, flat, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb / 4,
+                                      last_bucket_mb=bucket_mb / 4, split_param_mb=bucket_mb)
+        nchunks = max(len(v) for v in ddp._bucket_of.values())
+        kw = {"momentum": 0.9} if opt_name == "sgd" else {"weight_decay": 0.01}
+        opt = optim.build(opt_name, flat, lr=0.05 if opt_name == "sgd" else 1e-3, **kw)
+        for _ in range(3):
+            opt.zero_grad()
+            _loss(model, kind, x[shard], y[shard]).backward()
+            if per_bucket:
+                ddp.finish_gradient_sync(opt=opt, clip=clip)
+            else:
+                ddp.finish_gradient_sync()
+                sc = ddp.grad_scale()
+                if clip is not None:
+                    opt.clip_grad_norm(clip, pre_scale=sc, post_scale=sc)
+                else:
+                    opt.set_grad_scale(sc)
+                opt.step()
+        masters.append(flat.master.clone())
+    a, b = masters
+    torch.save({"bitwise": bool(torch.equal(a, b)), "maxdiff": float((a - b).abs().max()),
+                "scale": float(a.abs().max()), "nchunks": nchunks},
+               os.path.join(out_dir, f"pb{rank}.pt"))
+    dist.destroy_process_group()
+
+
 def bucket_timeline_worker(rank, world, port, out, device="cpu"):
     """Two-step data-parallel run with the per-bucket timeline on (tests/test_ddp_cpu.py,
     tests/test_ddp_gpu.py): saves comm_report() plus whether average_buffers() made the per-rank
@@ -188,10 +232,12 @@ def rccl_force_check(kind: str = "resnet18", grad_dtype: str = "fp32", steps: in
         for _ in range(steps):
             opt.zero_grad()
             cross_entropy(model.forward_logits(x), y).backward()
-            if ddp is not None:
-                ddp.finish_gradient_sync()
-            grads.append(flat.grad.clone())
-            opt.step()
+            if ddp is not None:     # per-bucket SGD on the comm stream as each all-reduce completes
+                ddp.finish_gradient_sync(opt=opt)
+                grads.append(flat.grad.clone())
+            else:
+                grads.append(flat.grad.clone())
+                opt.step()
         torch.cuda.synchronize()
         return grads, flat.master.clone(), (len(ddp.buckets) if ddp else 0)
 

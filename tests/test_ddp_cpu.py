@@ -33,6 +33,32 @@ def test_ddp_equals_single_process(tmp_path, kind, world):
         assert res["nbuckets"] >= 2
 
 
+@pytest.mark.parametrize("opt_name,clip,world", [("sgd", None, 2), ("adamw", None, 2), ("adamw", 1.0, 2),
+                                                  ("sgd", 0.05, 4)])
+def test_per_bucket_optimizer_equals_single_update(tmp_path, opt_name, clip, world):
+    """finish_gradient_sync(opt=...) updates each bucket as its all-reduce completes: bitwise equal
+    to the single whole-arena update without clipping, fp32-close with the two-phase clip."""
+    from pcmp.parallel.selftest import per_bucket_opt_worker
+    os.environ["PYTHONPATH"] = ROOT + os.pathsep + os.environ.get("PYTHONPATH", "")
+    mp.spawn(per_bucket_opt_worker, args=(world, _port(), str(tmp_path), opt_name, clip), nprocs=world, join=True)
+    for r in range(world):
+        res = torch.load(tmp_path / f"pb{r}.pt", weights_only=True)
+        assert res["nchunks"] >= 2, res          # the embedding table spans several buckets
+        if clip is None:
+            assert res["bitwise"], res
+        else:
+            assert res["maxdiff"] <= 1e-6 * max(1.0, res["scale"]), res
+
+
+def test_plan_segments_splits_oversized_params():
+    from pcmp.parallel.ddp import plan_segments
+    segs = plan_segments([100, 9600, 48], 2621)
+    assert segs[0] == (0, 0, 100) and segs[-1] == (2, 0, 48)
+    chunks = [s for s in segs if s[0] == 1]
+    assert len(chunks) == 4 and chunks[0] == (1, 0, 3072) and chunks[-1][2] == 9600
+    assert all(hi - lo <= 3072 and lo % 1024 == 0 for _, lo, hi in chunks)
+
+
 def test_plan_buckets_small_first_bucket():
     sizes = [10] * 100
     b = plan_buckets(sizes, 25, 200)

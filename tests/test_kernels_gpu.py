@@ -332,6 +332,17 @@ def test_optimizers(gpu):
     normr, coefr = ref.grad_clip_coef(g, 1.0, 1.0, 0.25)
     close(norm, normr, 1e-5, 1e-4)
     close(coef, coefr, 1e-5, 1e-7)
+    # two-phase form (per-bucket partial sums, one coefficient): the same norm over uneven buckets
+    cuts = [0, 4096, 4096 + 1024 * 5, n]
+    nb = [ref.sumsq_blocks(cuts[i + 1] - cuts[i]) for i in range(3)]
+    part = torch.full((sum(nb),), float("nan"), device=gpu)
+    off = 0
+    for i in range(3):
+        _ops().grad_sumsq_parts(g[cuts[i]:cuts[i + 1]], part, off)
+        off += nb[i]
+    norm2, coef2 = _ops().clip_coef_parts(part, 1.0, 1.0, 0.25)
+    close(norm2, normr, 1e-5, 1e-4)
+    close(coef2, coefr, 1e-5, 1e-7)
 
 
 def test_input_conversion(gpu):

@@ -14,6 +14,7 @@
 #   knob-ab      per-shape in-process knob A/B (tools/gemm_knob_ab.py): KVARIANTS='a:k=v;b:k=v' MODES
 #   prof-bench   rocprofv3 kernel stats + per-step table of the ResNet-50 bench step
 #   prof-bert    rocprofv3 kernel stats + per-step table of the BERT-base step
+#   prof-bilstm  rocprofv3 kernel stats + per-step table of the BiLSTM step (B=32, S=128)
 #   prof-infer   rocprofv3 trace of the batch-1 hipGraph inference loop: kernels / span per image
 #   tail         end-of-backward tail report (tools/tail_report.py)
 #   layer        serial event-bracketed layer profile (WGRAD side stream off)
@@ -26,7 +27,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R; mkdir -p gpurun_out; export TMPDIR=/tmp
-T=${TAG:-r5}
+T=${TAG:-r6}
 O=gpurun_out/$T
 
 die() { echo "[$1 failed]"; [ -n "$2" ] && tail -40 "$2"; exit 1; }
@@ -93,6 +94,13 @@ task_prof_bert() {
   python tools/prof_summary.py gpurun_out/prof_bert --top 45 --step-kernel adam_flat --last-steps 4 > ${O}_prof_bert.txt
   find gpurun_out/prof_bert -name "*kernel_trace.csv" -delete
   sed -n '/per step over/,+12p' ${O}_prof_bert.txt
+}
+task_prof_bilstm() {
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bilstm -o run -- \
+    python tools/prof_target.py bilstm 16 > gpurun_out/prof_bilstm.log 2>&1 || die prof-bilstm gpurun_out/prof_bilstm.log
+  python tools/prof_summary.py gpurun_out/prof_bilstm --top 30 --step-kernel adam_flat --last-steps 4 > ${O}_prof_bilstm.txt
+  find gpurun_out/prof_bilstm -name "*kernel_trace.csv" -delete
+  sed -n '/per step over/,+12p' ${O}_prof_bilstm.txt
 }
 task_prof_f32() {   # fp32 transfer-learning forward (B=64): kernel stats over 10 forwards
   cd /tmp
