@@ -104,10 +104,12 @@ constexpr unsigned kSpinLimit = 1u << 26;
 typedef __attribute__((address_space(1))) unsigned gu32;
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp): a full-precision IEEE division is ~10 dependent instructions, and
+// the cell update (3 sigmoids + 2 tanh per unit) sits on the recurrence's per-step critical path
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float tanh_f(float x) {
   const float e = __expf(-2.f * fabsf(x));
-  const float r = (1.f - e) / (1.f + e);
+  const float r = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
   return copysignf(r, x);
 }
 
@@ -163,6 +165,7 @@ struct LstmFwdParams {
   unsigned* counters;    // [2] per-direction arrival counters (zeroed by host)
   unsigned* err;
   int B, S, H;
+  unsigned long long* prof;   // knob lstm_prof: per-phase shader-clock totals of workgroup 0 (else null)
 };
 
 // grid = 2 * (H / LJ) workgroups; wg -> (dir = wg / (H/LJ), unit block ub = wg % (H/LJ))
@@ -302,6 +305,7 @@ struct LstmBwdParams {
   unsigned* counters;
   unsigned* err;
   int B, S, H;
+  unsigned long long* prof;
 };
 
 // wg owns hidden units j0..j0+LJ of its direction: cell backward for those units and
@@ -443,6 +447,491 @@ __global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p)
   }
 }
 
+// ------------------------------------------------------------------------- LSTM, role-split waves
+// Round-6 form of the two persistent recurrences (knob lstm_v2, default on): 512-thread workgroups
+// whose waves take fixed roles, so the per-step critical path -- the h_t / dgates_t hand-off between
+// the workgroups of a direction -- never waits for bulk memory traffic.  (On gfx9-family hardware
+// stores count in vmcnt like loads: in the round-1 kernels every wave streamed the step's bulk
+// inputs and outputs, so the drain before the arrival and the wait for the exchange tile also
+// waited for those.)
+//   * compute waves 0-3: wave 0 publishes this workgroup's slice (sc1 stores, drain, one agent
+//     atomic add) and polls the direction's arrival counter; after a workgroup barrier all four
+//     gather the whole exchange tile (sc1 loads to registers, up to 16 in flight per lane: one wave
+//     alone reads a fresh 64 KB slot in ~4.9 us, MI355X_MICROARCH.md handoff-payload) into LDS;
+//     they run the backward's recurrent MFMA product;
+//   * IO waves 4-7: after the cell update they store the step's outputs from LDS staging (small: 4 KB
+//     of dgates / 11 KB of activations per step); beside the MFMA product (after the gather) they
+//     issue the loads of a later step's per-unit inputs into registers, committed to LDS while the
+//     compute waves gather.
+//     Their loads are still in flight while they join the forward's MFMA product (one 16x16 output
+//     tile per wave) and both cell updates (one (b, unit) pair per thread);
+//   * every barrier is an LDS-only one (lds_barrier), so no wave's outstanding loads hold it.
+// LDS rows of the MFMA operands are XOR-swizzled by row (conflict-free 16-row fragment reads).  The
+// arithmetic (MFMA tile mapping and K order, cell math) is the round-1 kernels': results are bitwise
+// equal (tests/test_text_kernels_gpu.py::test_lstm_v2_bitwise).
+constexpr int LT2 = 512;   // threads: 4 compute + 4 IO waves
+constexpr int LC = 256;    // compute threads (waves 0-3); IO threads are tid - LC
+static_assert(LB * LJ == LT2, "lstm v2: one (b, unit) pair per thread in the cell updates");
+
+// IO-wave loads are raw buffer loads whose masked lanes read out of bounds (zeros): no branches
+// around them, so the compiler has no conditional block to unpack the data in right after the load
+// (which forced a wait on it) and the loads stay in flight until their commit
+constexpr unsigned kIoOOB = 0x80000000u;
+__device__ __forceinline__ uint4 io_ld16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return uint4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ long long io_ld8(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+  const u32x2v v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  return (long long)(((unsigned long long)v[1] << 32) | v[0]);
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global ones (__syncthreads() = workgroup release fence + s_barrier waits vmcnt(0) too, so an IO
+// wave with its loads in flight would hold every barrier of the step until they land).  Global data
+// never passes between the waves of a workgroup through memory here: the exchange tile is loaded
+// (sc1, to registers) after this barrier has ordered it behind the polling wave's match.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// chunk c of row r at 16-B slot c ^ (r & m): the 16 lanes of an MFMA fragment read 16 rows at the
+// same column, which unswizzled (row pitch a multiple of 256 B) all hit the same LDS banks
+__host__ __device__ constexpr int swz_mask(int nchunks) {
+  return ((nchunks & -nchunks) < 16 ? (nchunks & -nchunks) : 16) - 1;
+}
+__device__ __forceinline__ int swz(int row, int chunk, int nchunks) {
+  return row * nchunks + (chunk ^ (row & swz_mask(nchunks)));
+}
+
+// wave 0, lane 0 polls the arrival counter (sc1 loads); the wave's other lanes wait in lockstep
+__device__ __forceinline__ bool exch_wait(unsigned* counter, unsigned target, unsigned* err) {
+  bool ok = true;
+  if ((threadIdx.x & 63) == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load((gu32*)counter, RLX_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store((gu32*)err, 1u, RLX_AGENT);
+        ok = false;
+        break;
+      }
+    }
+  }
+  const bool r = __shfl(ok ? 1 : 0, 0) != 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler ordering only: tile loads are sc1
+  return r;
+}
+
+// exchange-tile gather by the 256 compute threads: [rows][nchunks] 16-B chunks (byte offset src),
+// sc1 loads to registers, MAXN in flight per lane, written to swizzled LDS
+template <int MAXN>
+__device__ __forceinline__ void gather_tile_sc1(__amdgpu_buffer_rsrc_t rs, unsigned src, uint4* lds, int rows,
+                                                int nchunks, int ctid) {
+  const int n = rows * nchunks / LC;   // a whole number of passes (checked on the host)
+  for (int e0 = 0; e0 < n; e0 += MAXN) {
+    uint4 v[MAXN];
+#pragma unroll
+    for (int e = 0; e < MAXN; ++e)
+      if (e0 + e < n) v[e] = ld16_sc1(rs, src + (unsigned)(((e0 + e) * LC + ctid) * 16));
+#pragma unroll
+    for (int e = 0; e < MAXN; ++e)
+      if (e0 + e < n) {
+        const int i = (e0 + e) * LC + ctid;
+        lds[swz(i / nchunks, i % nchunks, nchunks)] = v[e];
+      }
+  }
+}
+
+// phase clocks (knob lstm_prof): workgroup 0, thread 0, shader clocks per phase over the launch
+struct PhaseClock {
+  bool on;
+  unsigned long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = 0;
+  __device__ void mark(int ph) {
+    if (on) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) pc[ph] += now - tp;
+      tp = now;
+    }
+  }
+  __device__ void flush(unsigned long long* out, int n) {
+    if (on)
+      for (int i = 0; i < n; ++i) out[i] = pc[i];
+  }
+};
+
+__global__ void __launch_bounds__(LT2) lstm_fwd_persistent2(const LstmFwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = p.H, nub = H / LJ, G4 = 4 * H, NCH = H / 8;
+  const int dir = blockIdx.x / nub, ub = blockIdx.x % nub, j0 = ub * LJ;
+  __bf16* sW = reinterpret_cast<__bf16*>(smem);               // [4LJ][H]   W_hh rows (swizzled)
+  __bf16* sH = sW + 4 * LJ * H;                                // [LB][H]    h_{t-1} (swizzled)
+  float* sG = reinterpret_cast<float*>(sH + LB * H);           // [LB][4LJ]  recurrent pre-activations
+  float* sGx = sG + LB * 4 * LJ;                               // [2][LB][4LJ] input projections (ping-pong)
+  float* sA = sGx + 2 * LB * 4 * LJ;                           // [LB][4LJ]  activations i,f,g,o (staging)
+  float* sC = sA + LB * 4 * LJ;                                // [LB][LJ]   c_t (staging)
+  __bf16* sHo = reinterpret_cast<__bf16*>(sC + LB * LJ);      // [LB][LJ]   h_t (exchange + output)
+  int* sV = reinterpret_cast<int*>(sHo + LB * LJ);            // [2][LB] token valid flags; [2*LB] abort
+  const __amdgpu_buffer_rsrc_t rsH = rnn_rsrc(p.hbuf, (unsigned)(4 * LB * H * 2));
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, it = tid - LC;
+  const bool io = tid >= LC;
+  for (int i = tid; i < 4 * LJ * H / 8; i += LT2) {
+    const int r = i / NCH, c8 = i % NCH;
+    const int gate = r / LJ, jj = r % LJ;
+    reinterpret_cast<uint4*>(sW)[swz(r, c8, NCH)] =
+        reinterpret_cast<const uint4*>(p.whh + ((size_t)dir * G4 + gate * H + j0 + jj) * H)[c8];
+  }
+  for (int i = tid; i < LB * H / 8; i += LT2) reinterpret_cast<uint4*>(sH)[i] = uint4{0, 0, 0, 0};
+  if (tid == 0) sV[2 * LB] = 0;
+  unsigned* cnt = p.counters + dir;
+  // IO threads: the step's gx slice [b][gate][16 units] = 2 x 16 B per (b, gate): 256 items, + 32 ids
+  const __amdgpu_buffer_rsrc_t rsGx = rnn_rsrc(p.gx, (unsigned)((size_t)p.B * p.S * 2 * G4 * 2));
+  const __amdgpu_buffer_rsrc_t rsId = rnn_rsrc(p.ids, (unsigned)((size_t)p.B * p.S * 8));
+  uint4 fv = uint4{0, 0, 0, 0};
+  long long fid = 0;   // the raw token id: compared at commit
+  auto io_fetch = [&](int stp) {
+    const int tt = dir == 0 ? stp : p.S - 1 - stp;
+    const int b = it >> 3, g = (it >> 1) & 3, half = it & 1;
+    fv = io_ld16(rsGx, b < p.B ? (unsigned)(((((unsigned)b * p.S + tt) * 2 + dir) * G4 + g * H + j0 + half * 8) * 2)
+                               : kIoOOB);
+    fid = io_ld8(rsId, (it < LB && it < p.B) ? (unsigned)((it * p.S + tt) * 8) : kIoOOB);
+  };
+  auto io_commit = [&](int slot) {
+    const int b = it >> 3, g = (it >> 1) & 3, half = it & 1;
+    const unsigned short* u = reinterpret_cast<const unsigned short*>(&fv);
+    float* d = sGx + slot * LB * 4 * LJ + b * 4 * LJ + g * LJ + half * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = bf2f(u[e]);
+    if (it < LB) sV[slot * LB + it] = fid > 0 ? 1 : 0;
+  };
+  // IO threads: this step's outputs: activations 4 x 64 B per b, c_t 64 B per b, h_t 32 B per b
+  auto io_store = [&](int t) {
+    constexpr int NA = LB * 16, NC = LB * 4, NH = LB * 2;
+    for (int i = it; i < NA + NC + NH; i += LT2 - LC) {
+      if (i < NA) {
+        const int b = i >> 4, g = (i >> 2) & 3, q = i & 3;
+        if (b < p.B)
+          *reinterpret_cast<float4*>(p.gates + (((size_t)b * p.S + t) * 2 + dir) * G4 + g * H + j0 + q * 4) =
+              *reinterpret_cast<const float4*>(sA + b * 4 * LJ + g * LJ + q * 4);
+      } else if (i < NA + NC) {
+        const int b = (i - NA) >> 2, q = (i - NA) & 3;
+        if (b < p.B)
+          *reinterpret_cast<float4*>(p.cst + (((size_t)b * p.S + t) * 2 + dir) * H + j0 + q * 4) =
+              *reinterpret_cast<const float4*>(sC + b * LJ + q * 4);
+      } else {
+        const int b = (i - NA - NC) >> 1, half = (i - NA - NC) & 1;
+        if (b < p.B)
+          *reinterpret_cast<uint4*>(p.hout + ((size_t)b * p.S + t) * 2 * H + dir * H + j0 + half * 8) =
+              *reinterpret_cast<const uint4*>(sHo + b * LJ + half * 8);
+      }
+    }
+  };
+  if (io) {
+    io_fetch(0);
+    io_commit(0);
+    if (p.S > 1) io_fetch(1);
+  }
+  float creg = 0.f, hreg = 0.f;   // the thread's (b, unit) pair
+  PhaseClock clk{p.prof != nullptr && blockIdx.x == 0 && tid == 0};   // poll, gather, MFMA, cell, publish
+  lds_barrier();
+  for (int step = 0; step < p.S; ++step) {
+    const int t = dir == 0 ? step : p.S - 1 - step;
+    const int cur = step & 1;
+    clk.mark(-1);
+    // ---- A: wave 0 waits for every workgroup's h_{t-1} slice
+    if (wid == 0 && step > 0) {
+      if (!exch_wait(cnt, (unsigned)step * nub, p.err) && lane == 0) sV[2 * LB] = 1;
+      clk.mark(0);
+    }
+    lds_barrier();
+    if (sV[2 * LB]) return;
+    // ---- gather h_{t-1} (compute waves); the IO waves commit this step's inputs (loaded last step)
+    if (!io) {
+      if (step > 0)
+        gather_tile_sc1<4>(rsH, (unsigned)(((cur ^ 1) * 2 + dir) * LB * H) * 2u, reinterpret_cast<uint4*>(sH), LB,
+                           NCH, tid);
+      clk.mark(1);
+    } else if (step > 0) {
+      io_commit(cur);   // this step's inputs, loaded during the previous step's MFMA phase
+    }
+    lds_barrier();
+    if (io && step > 0 && step + 1 < p.S) io_fetch(step + 1);   // beside the MFMA phase, committed next step
+    // ---- B: pre-activations [LB][4LJ] = h @ Wslice^T: all 8 waves, one 16x16 tile each (m-tile
+    //      w & 1, n-tile w >> 1), round-1 K order
+    {
+      const int mt = wid & 1, nt = wid >> 1;
+      f32x4 acc = {0, 0, 0, 0};
+      const bf16x8* sH8 = reinterpret_cast<const bf16x8*>(sH);
+      const bf16x8* sW8 = reinterpret_cast<const bf16x8*>(sW);
+      const int ar = mt * 16 + (lane & 15), n0 = nt * 16 + (lane & 15);
+      for (int k0 = 0; k0 < H; k0 += 128) {   // fragments of 4 K-steps read ahead of their MFMAs
+        bf16x8 a[4], b0[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k0 + 32 * u < H) {
+            const int kc = ((k0 + 32 * u) >> 3) + (lane >> 4);
+            a[u] = sH8[swz(ar, kc, NCH)];
+            b0[u] = sW8[swz(n0, kc, NCH)];
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k0 + 32 * u < H) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b0[u], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sG[(mt * 16 + (lane >> 4) * 4 + e) * 4 * LJ + n0] = acc[e];
+      clk.mark(2);
+    }
+    lds_barrier();
+    // ---- C: cell update, one (b, jj) pair per thread (LB * LJ = 512), outputs to LDS staging
+    {
+      const int b = tid / LJ, jj = tid % LJ;
+      float hn = 0.f;
+      if (b < p.B) {
+        const bool valid = sV[cur * LB + b] != 0;
+        const float* gx = sGx + cur * LB * 4 * LJ + b * 4 * LJ;
+        float pre[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pre[g] = sG[b * 4 * LJ + g * LJ + jj] + gx[g * LJ + jj];
+        const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanh_f(pre[2]), og = sigm(pre[3]);
+        float cn, hv;
+        if (valid) {
+          cn = fg * creg + ig * gg;
+          hv = og * tanh_f(cn);
+        } else {
+          cn = creg;
+          hv = hreg;
+        }
+        creg = cn;
+        hreg = hv;
+        hn = hv;
+        float* a = sA + b * 4 * LJ + jj;
+        a[0] = ig;
+        a[LJ] = fg;
+        a[2 * LJ] = gg;
+        a[3 * LJ] = og;
+        sC[b * LJ + jj] = cn;
+      }
+      reinterpret_cast<unsigned short*>(sHo)[b * LJ + jj] = f2bf(hn);
+      clk.mark(3);
+    }
+    lds_barrier();
+    // ---- D: wave 0 publishes h_t and arrives; the IO waves store the step's outputs
+    if (wid == 0 && step + 1 < p.S) {
+      const int b = lane >> 1, half = lane & 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(sHo + b * LJ + half * 8);
+      st16_sc1(rsH, (unsigned)((cur * 2 + dir) * LB * H + b * H + j0 + half * 8) * 2u, v);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the publish store is outstanding
+      if (lane == 0) __hip_atomic_fetch_add((gu32*)cnt, 1u, RLX_AGENT);
+      clk.mark(4);
+    } else if (io) {
+      io_store(t);
+    }
+  }
+  clk.flush(p.prof, 5);
+}
+
+__global__ void __launch_bounds__(LT2) lstm_bwd_persistent2(const LstmBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = p.H, nub = H / LJ, G4 = 4 * H, NCD = G4 / 8;
+  const int dir = blockIdx.x / nub, ub = blockIdx.x % nub, j0 = ub * LJ;
+  __bf16* sWt = reinterpret_cast<__bf16*>(smem);               // [LJ][4H] W_hh columns (swizzled)
+  __bf16* sD = sWt + LJ * G4;                                   // [LB][4H] dgates_t (swizzled)
+  float* sR = reinterpret_cast<float*>(sD + LB * G4);           // [LB][LJ] dh_rec
+  __bf16* sDo = reinterpret_cast<__bf16*>(sR + LB * LJ);       // [LB][4][LJ] this slice's dgates_t
+  float* sF = reinterpret_cast<float*>(sDo + LB * 4 * LJ);      // [2][7][LB][LJ] per-step inputs
+  int* sV = reinterpret_cast<int*>(sF + 2 * 7 * LB * LJ);       // [2][LB] valid flags; [2*LB] abort
+  const __amdgpu_buffer_rsrc_t rsD = rnn_rsrc(p.dgbuf, (unsigned)(4 * LB * G4 * 2));
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, it = tid - LC;
+  const bool io = tid >= LC;
+  for (int i = tid; i < LJ * G4; i += LT2) {
+    const int jj = i / G4, r = i % G4;
+    reinterpret_cast<unsigned short*>(sWt)[swz(jj, r >> 3, NCD) * 8 + (r & 7)] =
+        reinterpret_cast<const unsigned short*>(p.whh)[((size_t)dir * G4 + r) * H + j0 + jj];
+  }
+  if (tid == 0) sV[2 * LB] = 0;
+  unsigned* cnt = p.counters + dir;
+  // IO threads: per-step inputs as 16-B items, each load instruction from ONE source (uniform buffer
+  // resource, out-of-bounds zeros for masked lanes): gates 512 items (2 per thread: b, gate, quarter),
+  // c_t 128 (threads 0-127) or c_prev 128 (threads 128-255), dh_out 64 (threads 0-63), ids 32
+  const __amdgpu_buffer_rsrc_t rsG = rnn_rsrc(p.gates, (unsigned)((size_t)p.B * p.S * 2 * G4 * 4));
+  const __amdgpu_buffer_rsrc_t rsC = rnn_rsrc(p.cst, (unsigned)((size_t)p.B * p.S * 2 * H * 4));
+  const __amdgpu_buffer_rsrc_t rsDh = rnn_rsrc(p.dhout, (unsigned)((size_t)p.B * p.S * 2 * H * 2));
+  const __amdgpu_buffer_rsrc_t rsId = rnn_rsrc(p.ids, (unsigned)((size_t)p.B * p.S * 8));
+  uint4 fv[4];
+  long long fid = 0;
+  auto io_fetch = [&](int stp) {
+    const int tt = dir == 0 ? p.S - 1 - stp : stp;
+    const int tp = dir == 0 ? tt - 1 : tt + 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {   // gates
+      const int i = it + 256 * k, b = i >> 4, g = (i >> 2) & 3, q = i & 3;
+      fv[k] = io_ld16(rsG, b < p.B ? (unsigned)(((((unsigned)b * p.S + tt) * 2 + dir) * G4 + g * H + j0 + q * 4) * 4)
+                                   : kIoOOB);
+    }
+    {   // c_t (threads 0-127) / c_prev (threads 128-255)
+      const int i = it & 127, b = i >> 2, q = i & 3, ts = it < 128 ? tt : tp;
+      const bool ok = b < p.B && ts >= 0 && ts < p.S;
+      fv[2] = io_ld16(rsC, ok ? (unsigned)(((((unsigned)b * p.S + ts) * 2 + dir) * H + j0 + q * 4) * 4) : kIoOOB);
+    }
+    {   // dh_out (threads 0-63)
+      const int b = it >> 1, half = it & 1;
+      fv[3] = io_ld16(rsDh, (it < 64 && b < p.B)
+                                ? (unsigned)((((unsigned)b * p.S + tt) * 2 * H + dir * H + j0 + half * 8) * 2) : kIoOOB);
+    }
+    fid = io_ld8(rsId, (it < LB && it < p.B) ? (unsigned)((it * p.S + tt) * 8) : kIoOOB);
+  };
+  auto io_commit = [&](int slot) {   // F rows: 0 dh_out, 1-4 gates i,f,g,o, 5 c_t, 6 c_prev
+    float* F = sF + slot * 7 * LB * LJ;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = it + 256 * k, b = i >> 4, g = (i >> 2) & 3, q = i & 3;
+      *reinterpret_cast<uint4*>(F + (1 + g) * LB * LJ + b * LJ + q * 4) = fv[k];
+    }
+    {
+      const int i = it & 127, b = i >> 2, q = i & 3;
+      *reinterpret_cast<uint4*>(F + (it < 128 ? 5 : 6) * LB * LJ + b * LJ + q * 4) = fv[2];
+    }
+    if (it < 64) {
+      const int b = it >> 1, half = it & 1;
+      const unsigned short* u = reinterpret_cast<const unsigned short*>(&fv[3]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) F[b * LJ + half * 8 + e] = bf2f(u[e]);
+    }
+    if (it < LB) sV[slot * LB + it] = fid > 0 ? 1 : 0;
+  };
+  // IO threads: this step's dgates [b][gate][16 units] bf16 = 2 x 16 B per (b, gate)
+  auto io_store = [&](int t) {
+    const int b = it >> 3, g = (it >> 1) & 3, half = it & 1;
+    if (b < p.B)
+      *reinterpret_cast<uint4*>(p.dgates + (((size_t)b * p.S + t) * 2 + dir) * G4 + g * H + j0 + half * 8) =
+          *reinterpret_cast<const uint4*>(sDo + (b * 4 + g) * LJ + half * 8);
+  };
+  if (io) {
+    io_fetch(0);
+    io_commit(0);
+    if (p.S > 1) io_fetch(1);
+  }
+  float dcreg = 0.f, dhcarry = 0.f;   // the thread's (b, unit) pair
+  PhaseClock clk{p.prof != nullptr && blockIdx.x == 0 && tid == 0};   // cell, publish, poll, gather, MFMA
+  lds_barrier();
+  for (int step = 0; step < p.S; ++step) {
+    const int t = dir == 0 ? p.S - 1 - step : step;
+    const int cur = step & 1;
+    const unsigned dst = (unsigned)((cur * 2 + dir) * LB * G4) * 2u;
+    clk.mark(-1);
+    // ---- C: cell backward (round-1 math), one (b, jj) pair per thread, dgates slice to LDS
+    {
+      const float* F = sF + cur * 7 * LB * LJ;
+      const int b = tid / LJ, jj = tid % LJ;
+      float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
+      if (b < p.B) {
+        const int o = b * LJ + jj;
+        const float dh = F[o] + dhcarry;
+        if (sV[cur * LB + b]) {
+          const float ig = F[LB * LJ + o], fg = F[2 * LB * LJ + o], gg = F[3 * LB * LJ + o], og = F[4 * LB * LJ + o];
+          const float c = F[5 * LB * LJ + o];
+          const float cprev = F[6 * LB * LJ + o];
+          const float tc = tanh_f(c);
+          const float dc = dcreg + dh * og * (1.f - tc * tc);
+          dgo = dh * tc * og * (1.f - og);
+          dgi = dc * gg * ig * (1.f - ig);
+          dgg = dc * ig * (1.f - gg * gg);
+          dgf = dc * cprev * fg * (1.f - fg);
+          dcreg = dc * fg;
+          dhcarry = 0.f;
+        } else {
+          dhcarry = dh;
+        }
+      }
+      unsigned short* d16 = reinterpret_cast<unsigned short*>(sDo) + b * 4 * LJ + jj;
+      d16[0] = f2bf(dgi);
+      d16[LJ] = f2bf(dgf);
+      d16[2 * LJ] = f2bf(dgg);
+      d16[3 * LJ] = f2bf(dgo);
+      clk.mark(0);
+    }
+    lds_barrier();
+    // ---- D: wave 0 publishes dgates_t and arrives; the IO waves store it and load the next step
+    if (wid == 0) {
+      if (step + 1 < p.S) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = lane + 64 * e, b = i >> 3, g = (i >> 1) & 3, half = i & 1;
+          const uint4 v = *reinterpret_cast<const uint4*>(sDo + (b * 4 + g) * LJ + half * 8);
+          st16_sc1(rsD, dst + (unsigned)(b * G4 + g * H + j0 + half * 8) * 2u, v);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // only the publish stores are outstanding
+        if (lane == 0) __hip_atomic_fetch_add((gu32*)cnt, 1u, RLX_AGENT);
+        clk.mark(1);
+      }
+    } else if (io) {
+      io_store(t);
+    }
+    if (step + 1 == p.S) break;
+    // ---- A: wave 0 waits for every workgroup's dgates_t slice
+    if (wid == 0) {
+      if (!exch_wait(cnt, (unsigned)(step + 1) * nub, p.err) && lane == 0) sV[2 * LB] = 1;
+      clk.mark(2);
+    }
+    lds_barrier();
+    if (sV[2 * LB]) return;
+    if (!io) {
+      gather_tile_sc1<16>(rsD, dst, reinterpret_cast<uint4*>(sD), LB, NCD, tid);
+      clk.mark(3);
+    } else {
+      io_commit(cur ^ 1);   // the next step's inputs, loaded beside the previous MFMA phase
+    }
+    lds_barrier();
+    if (io && step + 2 < p.S) io_fetch(step + 2);   // beside this MFMA phase, committed next step
+    // ---- B: dh_rec[b][jj] = sum_r dgates[b][r] W[r][j0+jj] (round-1 split: waves 2,3 the upper K half)
+    f32x4 acc = {0, 0, 0, 0};
+    const int mt = wid & 1, kh = (wid >> 1) & 1;
+    if (!io) {
+      const int kbeg = kh * (G4 / 2), kend = kbeg + G4 / 2;
+      const bf16x8* sD8 = reinterpret_cast<const bf16x8*>(sD);
+      const bf16x8* sW8 = reinterpret_cast<const bf16x8*>(sWt);
+      const int ar = mt * 16 + (lane & 15), br = lane & 15;
+      for (int k0 = kbeg; k0 < kend; k0 += 128) {
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k0 + 32 * u < kend) {
+            const int kc = ((k0 + 32 * u) >> 3) + (lane >> 4);
+            a[u] = sD8[swz(ar, kc, NCD)];
+            b[u] = sW8[swz(br, kc, NCD)];
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (k0 + 32 * u < kend) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
+      }
+      if (kh == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sR[(mt * 16 + (lane >> 4) * 4 + e) * LJ + (lane & 15)] = acc[e];
+      }
+    }
+    lds_barrier();
+    if (!io) {
+      if (kh == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sR[(mt * 16 + (lane >> 4) * 4 + e) * LJ + (lane & 15)] += acc[e];
+      }
+    }
+    lds_barrier();
+    {
+      const int b = tid / LJ, jj = tid % LJ;
+      if (b < p.B) dhcarry += sR[b * LJ + jj];
+      clk.mark(4);
+    }
+  }
+  clk.flush(p.prof, 5);
+}
+
+inline Knob kn_lstm_v2("lstm_v2", 1);
+inline Knob kn_lstm_prof("lstm_prof", 0);   // phase clocks of the v2 recurrences into sync[4:20] (tools/lstm_micro.py)
+
 // ------------------------------------------------------------------------------- host
 static int ew_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n + 255) / 256)); }
 
@@ -528,10 +1017,27 @@ std::vector<at::Tensor> lstm_seq_fwd(const at::Tensor& gx, const at::Tensor& whh
   auto gates = at::empty({B, S, 2, 4 * H}, f32);
   auto cst = at::empty({B, S, 2, H}, f32);
   auto hbuf = at::empty({2, 2, LB, H}, whh.options());
-  auto sync = at::zeros({4}, gx.options().dtype(at::kInt));
+  const bool prof = kn_lstm_prof.get() != 0;
+  auto sync = at::zeros({prof ? 4 + 16 : 4}, gx.options().dtype(at::kInt));
   LstmFwdParams p{ptr<__bf16>(gx), ptr<__bf16>(whh), idc.data_ptr<int64_t>(), ptr<__bf16>(hout), ptr<float>(gates),
                   ptr<float>(cst), ptr<__bf16>(hbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
-                  reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H};
+                  reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H,
+                  prof ? reinterpret_cast<unsigned long long*>(reinterpret_cast<int*>(sync.data_ptr()) + 4) : nullptr};
+  const size_t smem2 = (size_t)4 * LJ * H * 2 + (size_t)LB * H * 2 + (size_t)4 * LB * 4 * LJ * 4 +
+                       (size_t)LB * LJ * 4 + (size_t)LB * LJ * 2 + (2 * LB + 1) * 4;
+  // v2: the exchange tile [LB][H] is gathered in whole 256-thread passes of 16-B chunks; the IO
+  // buffer resources take 32-bit byte offsets
+  if (kn_lstm_v2.get() && smem2 <= 160 * 1024 && (LB * H / 8) % LC == 0 && gates.numel() * 4 < (1ll << 31)) {
+    static bool attr = false;
+    if (!attr) {
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_fwd_persistent2),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(lstm_fwd_persistent2, dim3(2 * (H / LJ)), dim3(LT2), smem2, cur_stream(), p);
+    PCMP_LAUNCH_CHECK();
+    return {hout, gates, cst, sync};
+  }
   const size_t smem = (size_t)4 * LJ * H * 2 + (size_t)LB * H * 2 + (size_t)LB * 4 * LJ * 4 + (size_t)LB * LJ * 2;
   TORCH_CHECK(smem <= 160 * 1024, "lstm_seq_fwd: LDS budget exceeded");
   hipLaunchKernelGGL(lstm_fwd_persistent, dim3(2 * (H / LJ)), dim3(LT), smem, cur_stream(), p);
@@ -550,10 +1056,25 @@ std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& 
   auto dh = dhout.contiguous();
   auto dgates = at::empty({B, S, 2, 4 * H}, whh.options());
   auto dgbuf = at::empty({2, 2, LB, 4 * H}, whh.options());
-  auto sync = at::zeros({4}, gates.options().dtype(at::kInt));
+  const bool prof = kn_lstm_prof.get() != 0;
+  auto sync = at::zeros({prof ? 4 + 16 : 4}, gates.options().dtype(at::kInt));
   LstmBwdParams p{ptr<float>(gates), ptr<float>(cst), ptr<__bf16>(whh), idc.data_ptr<int64_t>(), ptr<__bf16>(dh),
                   ptr<__bf16>(dgates), ptr<__bf16>(dgbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
-                  reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H};
+                  reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H,
+                  prof ? reinterpret_cast<unsigned long long*>(reinterpret_cast<int*>(sync.data_ptr()) + 4) : nullptr};
+  const size_t smem2 = (size_t)LJ * 4 * H * 2 + (size_t)LB * 4 * H * 2 + (size_t)LB * LJ * 4 +
+                       (size_t)LB * 4 * LJ * 2 + (size_t)2 * 7 * LB * LJ * 4 + (2 * LB + 1) * 4;
+  if (kn_lstm_v2.get() && smem2 <= 160 * 1024 && (LB * 4 * H / 8) % LC == 0 && gates.numel() * 4 < (1ll << 31)) {
+    static bool attr = false;
+    if (!attr) {
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_persistent2),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(lstm_bwd_persistent2, dim3(2 * (H / LJ)), dim3(LT2), smem2, cur_stream(), p);
+    PCMP_LAUNCH_CHECK();
+    return {dgates, sync};
+  }
   const size_t smem = (size_t)LJ * 4 * H * 2 + (size_t)LB * 4 * H * 2 + (size_t)LB * LJ * 4 + (size_t)LB * 4 * LJ * 2;
   TORCH_CHECK(smem <= 160 * 1024, "lstm_seq_bwd: LDS budget exceeded");
   hipLaunchKernelGGL(lstm_bwd_persistent, dim3(2 * (H / LJ)), dim3(LT), smem, cur_stream(), p);

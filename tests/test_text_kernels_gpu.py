@@ -64,6 +64,31 @@ def test_lstm_recurrence(gpu, B, S, H):
     close(dg, dgr, 5e-2, 5e-2)
 
 
+@pytest.mark.parametrize("B,S,H", [(5, 40, 64), (32, 128, 256), (17, 33, 32)])
+def test_lstm_v2_bitwise(gpu, B, S, H):
+    """The role-split recurrences (knob lstm_v2: exchange wave + IO waves) run the round-1 kernels'
+    arithmetic: every output bitwise equal to lstm_v2 = 0."""
+    torch.manual_seed(1)
+    ids = _ids(B, S, 1000, gpu)
+    gx = (torch.randn(B, S, 2, 4 * H, device=gpu) * 0.5).to(torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, device=gpu) / H ** 0.5).to(torch.bfloat16)
+    dh = torch.randn(B, S, 2 * H, device=gpu).to(torch.bfloat16)
+    outs = []
+    old = ops().set_knob("lstm_v2", 0)
+    try:
+        for v in (0, 1):
+            ops().set_knob("lstm_v2", v)
+            h, g, c, sync = ops().lstm_seq_fwd(gx, whh, ids)
+            dg, sync2 = ops().lstm_seq_bwd(dh, g, c, whh, ids)
+            torch.cuda.synchronize()
+            assert int(sync[2].item()) == 0 and int(sync2[2].item()) == 0, "barrier timeout"
+            outs.append((h, g, c, dg))
+    finally:
+        ops().set_knob("lstm_v2", old)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_layernorm_act(gpu):
     x = torch.randn(300, 768, device=gpu).to(torch.bfloat16)
     r = torch.randn(300, 768, device=gpu).to(torch.bfloat16)
