@@ -1582,7 +1582,7 @@ __device__ __forceinline__ void igemm_epilogue32(const IgemmParams& p, f32x16 (&
 // pixels x 64 B (4 lanes per pixel) instead of 32 pixels x 2 x 16 B, which is what the memory-bound
 // short-K DGRAD + BN-backward epilogues (residual, x and mask loads per output) need (per-shape A/B
 // profiles/r5_knob_dma32.txt: -14 to -25 % on the 1x1 DGRADs into 1024 / 2048 channels without it).
-template <int MODE, int BM, int BN, int WM, int WN, int EPI, int EPD = 2, bool XP = false>
+template <int MODE, int BM, int BN, int WM, int WN, int EPI, int EPD = 2>
 __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p) {
   constexpr int NW = 4, NTHR = 256;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -1678,7 +1678,7 @@ __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p
   // per-channel epilogue coefficients: loaded ahead of the first DMAs, written to LDS once the first
   // stage has landed (the prologue barrier publishes them)
   float cv[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bool ld_ct = !XP && tid < BN && (bnr || (MODE == MODE_FWD && p.bias != nullptr));
+  const bool ld_ct = tid < BN && (bnr || (MODE == MODE_FWD && p.bias != nullptr));
   if (ld_ct) {
     const int c = min(n0 + tid, p.gn - 1);
     if constexpr (bnr) {
@@ -1779,34 +1779,7 @@ __global__ void __launch_bounds__(256, 2) igemm_dma32_kernel(const IgemmParams p
   ktile(nk - 2, std::integral_constant<int, NODMA>{});
   ktile(nk - 1, std::integral_constant<int, LAST>{});
   (void)NS;
-  if constexpr (XP) {
-    // per-wave [WTM pixels][WTN + 4] fp32 image over the dead stage buffers
-    constexpr int RSX = WTN + 4;
-    __syncthreads();   // every wave's last fragment reads and tail DMAs are done
-    float* xb = reinterpret_cast<float*>(smem) + wid * WTM * RSX;
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        float* row = xb + (i * 32 + (lane & 31)) * RSX + j * 32 + 16 * (lane >> 5);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<f32x4*>(row + 4 * q) =
-              f32x4{acc[j][i][4 * q], acc[j][i][4 * q + 1], acc[j][i][4 * q + 2], acc[j][i][4 * q + 3]};
-      }
-    constexpr int TM16 = WTM / 16, TN16 = WTN / 16;
-    f32x4 a16[TN16][TM16];
-    const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-    for (int j = 0; j < TN16; ++j)
-#pragma unroll
-      for (int i = 0; i < TM16; ++i)
-        a16[j][i] = *reinterpret_cast<const f32x4*>(xb + (i * 16 + fr) * RSX + (j >> 1) * 32 + fq * 8 + (j & 1) * 4);
-    __syncthreads();   // the images are read before the epilogue reuses the LDS
-    igemm_epilogue_fd<MODE, BM, BN, WM, WN, EPI, NTHR, EPD>(p, a16, smem, tid, m0, n0, tile_m, 0);
-  } else {
-    igemm_epilogue32<MODE, BM, BN, WM, WN, EPI, EPD>(p, acc, ctab, red, tid, m0, n0, tile_m);
-  }
+  igemm_epilogue32<MODE, BM, BN, WM, WN, EPI, EPD>(p, acc, ctab, red, tid, m0, n0, tile_m);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2567,9 +2540,6 @@ inline Knob kn_dma32("dma32", 1);
 inline Knob kn_dma32_modes("dma32_modes", 1);   // bit 0: FWD, bit 1: DGRAD (whole-step A/B: FWD only, profiles/r5_bench_ab_dma32_modes.txt)
 inline Knob kn_dma32_mink("dma32_mink", 3);
 inline Knob kn_dma32_dgrad_mink("dma32_dgrad_mink", 16);
-// dma32_xpose: 0 = register epilogue everywhere, 1 = LDS-transposed igemm_epilogue_fd for the
-// BN-backward DGRAD epilogues, 2 = for every epilogue
-inline Knob kn_dma32_xpose("dma32_xpose", 0);
 static bool use_dma32(int mode, const IgemmParams& p) {
   if (!kn_dma32.get() || mode == MODE_WGRAD || p.nsplit != 1 || p.relu >= 2 || p.gn % 8 != 0 ||
       p.gk / BK < kn_dma32_mink.get())
@@ -2588,26 +2558,18 @@ static void launch_dma32(IgemmParams& p, hipStream_t st) {
   TORCH_CHECK(p.relu < 2 && p.gn % 8 == 0, "igemm_dma32: conv epilogues with 8-channel groups only");
   TORCH_CHECK(p.gk / BK >= 2, "igemm_dma32: at least two K-tiles");
   const int grid = p.tiles_m * p.tiles_n;
-  constexpr size_t smem_reg = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
-  constexpr size_t smem_xp = (size_t)4 * (BM / WM) * (BN / WN + 4) * sizeof(float);
-  constexpr size_t smem_fd = (size_t)(4 * 16 * (3 * (BN / WN) + 4) + WM * 3 * BN) * sizeof(float);
-  constexpr size_t smem = std::max(smem_reg, std::max(smem_xp, smem_fd));
+  constexpr size_t smem = (size_t)2 * (BM + BN) * BK * 2 + (size_t)(6 * BN + WM * 3 * BN) * sizeof(float);
   static_assert(2 * smem <= 160 * 1024, "igemm_dma32: two blocks per CU");
-  const int xk = kn_dma32_xpose.get();
   int epi = EPI_PLAIN;
   if (MODE == MODE_FWD && p.stats) epi = EPI_STATS;
   if (MODE == MODE_DGRAD && p.bn_x) epi = p.bn_x2 ? EPI_BNR2 : EPI_BNR;
 #define PCMP_DMA32_LAUNCH(E, D)                                                                        \
   do {                                                                                                \
-    const bool xp_ = xk >= 2 || (xk == 1 && (E == EPI_BNR || E == EPI_BNR2));                          \
-    auto kfn = xp_ ? &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, true>                              \
-                   : &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, false>;                           \
+    auto kfn = &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D>;                                        \
     static bool attr_set = false;                                                                     \
     if (!attr_set) {                                                                                  \
-      for (auto f : {&igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, true>,                             \
-                     &igemm_dma32_kernel<MODE, BM, BN, WM, WN, E, D, false>})                           \
-        PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f),                          \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                          \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
       attr_set = true;                                                                                \
     }                                                                                                 \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(256), smem, st, p);                                      \

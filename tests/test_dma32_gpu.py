@@ -65,7 +65,7 @@ SHAPES = [
 
 
 @pytest.mark.parametrize("shape", SHAPES)
-def test_dma32_fwd(gpu, shape, xpose):
+def test_dma32_fwd(gpu, shape):
     torch.manual_seed(1)
     N, H, W, C, K, R, s, p = shape
     ops = _ops()
@@ -89,15 +89,8 @@ def test_dma32_fwd(gpu, shape, xpose):
     assert torch.equal(y2, y3)
 
 
-@pytest.fixture(params=[0, 2], ids=["reg_epilogue", "lds_transposed_epilogue"])
-def xpose(request):
-    old = _ops().set_knob("dma32_xpose", request.param)
-    yield request.param
-    _ops().set_knob("dma32_xpose", old)
-
-
 @pytest.mark.parametrize("shape", SHAPES)
-def test_dma32_dgrad(gpu, shape, xpose):
+def test_dma32_dgrad(gpu, shape):
     torch.manual_seed(2)
     N, H, W, C, K, R, s, p = shape
     ops = _ops()
