@@ -81,6 +81,14 @@ int64_t autotune_load(std::vector<std::string> entries) {
   return n;
 }
 
+// forget every autotuned GEMM plan (A/B tools: a variant's predictor re-plans under its own knobs)
+int64_t autotune_clear() {
+  std::lock_guard<std::mutex> g(g_plan_mu);
+  const int64_t n = (int64_t)g_plan_cache.size();
+  g_plan_cache.clear();
+  return n;
+}
+
 // optional compiled-in kernel variants of this build (none since round 4: the measured-losing
 // epilogue variants sk_fixup / epi_coal / bn_group were removed, docs/PERF_NOTES.md)
 std::vector<std::string> build_features() { return {}; }
@@ -92,6 +100,7 @@ TORCH_LIBRARY_FRAGMENT(pcmp, m) {
   m.def("gemm_plans() -> str[]", &pcmp::gemm_plans);
   m.def("autotune_table() -> str[]", &pcmp::autotune_table);
   m.def("autotune_load(str[] entries) -> int", &pcmp::autotune_load);
+  m.def("autotune_clear() -> int", &pcmp::autotune_clear);
   m.def("plan_candidates(Tensor x, Tensor w, int stride, int pad, Tensor? bias, Tensor? resid, bool relu) -> str[]",
         &pcmp::plan_candidates);
   m.def("wt_transpose_multi(Tensor src, Tensor(a!) dst, Tensor desc, int blocks) -> ()", &pcmp::wt_transpose_multi);

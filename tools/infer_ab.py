@@ -37,6 +37,7 @@ def main():
         for name, knobs in variants:
             old = {k: ops.set_knob(k, v) for k, v in knobs.items()}
             if name not in preds:
+                ops.autotune_clear()   # each variant plans its small-M convs under its own knobs
                 preds[name] = Batch1Predictor(m, imgs[:1].to(dev), use_graph=True)
                 nfix = sum("+fix" in e for e in ops.gemm_plans())
                 print(f"{name}: plans {len(ops.gemm_plans())}, with fixup {nfix}", flush=True)
