@@ -457,8 +457,9 @@ __global__ void __launch_bounds__(LT) lstm_bwd_persistent(const LstmBwdParams p)
 //   * compute waves 0-3: wave 0 publishes this workgroup's slice (sc1 stores, drain, one agent
 //     atomic add) and polls the direction's arrival counter; after a workgroup barrier all four
 //     gather the whole exchange tile (sc1 loads to registers, up to 16 in flight per lane: one wave
-//     alone reads a fresh 64 KB slot in ~4.9 us, MI355X_MICROARCH.md handoff-payload) into LDS;
-//     they run the backward's recurrent MFMA product;
+//     alone reads a fresh 64 KB slot in ~4.9 us, MI355X_MICROARCH.md handoff-payload) into LDS
+//     (forward); in the backward each compute wave loads its own MFMA A fragments of the 64 KB
+//     dgates tile straight into registers and runs its part of the recurrent product;
 //   * IO waves 4-7: after the cell update they store the step's outputs from LDS staging (small: 4 KB
 //     of dgates / 11 KB of activations per step); beside the MFMA product (after the gather) they
 //     issue the loads of a later step's per-unit inputs into registers, committed to LDS while the
@@ -738,8 +739,7 @@ __global__ void __launch_bounds__(LT2) lstm_bwd_persistent2(const LstmBwdParams 
   const int H = p.H, nub = H / LJ, G4 = 4 * H, NCD = G4 / 8;
   const int dir = blockIdx.x / nub, ub = blockIdx.x % nub, j0 = ub * LJ;
   __bf16* sWt = reinterpret_cast<__bf16*>(smem);               // [LJ][4H] W_hh columns (swizzled)
-  __bf16* sD = sWt + LJ * G4;                                   // [LB][4H] dgates_t (swizzled)
-  float* sR = reinterpret_cast<float*>(sD + LB * G4);           // [LB][LJ] dh_rec
+  float* sR = reinterpret_cast<float*>(sWt + LJ * G4);          // [LB][LJ] dh_rec
   __bf16* sDo = reinterpret_cast<__bf16*>(sR + LB * LJ);       // [LB][4][LJ] this slice's dgates_t
   float* sF = reinterpret_cast<float*>(sDo + LB * 4 * LJ);      // [2][7][LB][LJ] per-step inputs
   int* sV = reinterpret_cast<int*>(sF + 2 * 7 * LB * LJ);       // [2][LB] valid flags; [2*LB] abort
@@ -878,35 +878,35 @@ __global__ void __launch_bounds__(LT2) lstm_bwd_persistent2(const LstmBwdParams 
     }
     lds_barrier();
     if (sV[2 * LB]) return;
-    if (!io) {
-      gather_tile_sc1<16>(rsD, dst, reinterpret_cast<uint4*>(sD), LB, NCD, tid);
-      clk.mark(3);
-    } else {
+    if (io) {
       io_commit(cur ^ 1);   // the next step's inputs, loaded beside the previous MFMA phase
+      if (step + 2 < p.S) io_fetch(step + 2);   // beside this MFMA phase, committed next step
     }
-    lds_barrier();
-    if (io && step + 2 < p.S) io_fetch(step + 2);   // beside this MFMA phase, committed next step
-    // ---- B: dh_rec[b][jj] = sum_r dgates[b][r] W[r][j0+jj] (round-1 split: waves 2,3 the upper K half)
+    // ---- B: dh_rec[b][jj] = sum_r dgates[b][r] W[r][j0+jj] (round-1 split: waves 2,3 the upper K half).
+    //      Each compute wave loads its own A fragments (rows mt*16 + lane%16, its K half) straight from
+    //      the exchange buffer into registers, all in flight at once: no LDS copy of the 64 KB tile and
+    //      no barrier between the gather and the MFMAs.
     f32x4 acc = {0, 0, 0, 0};
     const int mt = wid & 1, kh = (wid >> 1) & 1;
     if (!io) {
-      const int kbeg = kh * (G4 / 2), kend = kbeg + G4 / 2;
-      const bf16x8* sD8 = reinterpret_cast<const bf16x8*>(sD);
+      const int kbeg = kh * (G4 / 2), nks = G4 / 2 / 32;
       const bf16x8* sW8 = reinterpret_cast<const bf16x8*>(sWt);
       const int ar = mt * 16 + (lane & 15), br = lane & 15;
-      for (int k0 = kbeg; k0 < kend; k0 += 128) {
-        bf16x8 a[4], b[4];
+      const unsigned abase = dst + (unsigned)(ar * G4 + kbeg + 8 * (lane >> 4)) * 2u;
+      for (int c0 = 0; c0 < nks; c0 += 16) {
+        uint4 av[16];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (k0 + 32 * u < kend) {
-            const int kc = ((k0 + 32 * u) >> 3) + (lane >> 4);
-            a[u] = sD8[swz(ar, kc, NCD)];
-            b[u] = sW8[swz(br, kc, NCD)];
+        for (int u = 0; u < 16; ++u)
+          if (c0 + u < nks) av[u] = ld16_sc1(rsD, abase + (unsigned)((c0 + u) * 64));
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (c0 + u < nks) {
+            const int kc = ((kbeg + 32 * (c0 + u)) >> 3) + (lane >> 4);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[u]), sW8[swz(br, kc, NCD)],
+                                                          acc, 0, 0, 0);
           }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (k0 + 32 * u < kend) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[u], acc, 0, 0, 0);
       }
+      clk.mark(3);
       if (kh == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) sR[(mt * 16 + (lane >> 4) * 4 + e) * LJ + (lane & 15)] = acc[e];
@@ -1062,8 +1062,8 @@ std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& 
                   ptr<__bf16>(dgates), ptr<__bf16>(dgbuf), reinterpret_cast<unsigned*>(sync.data_ptr()),
                   reinterpret_cast<unsigned*>(sync.data_ptr()) + 2, B, S, H,
                   prof ? reinterpret_cast<unsigned long long*>(reinterpret_cast<int*>(sync.data_ptr()) + 4) : nullptr};
-  const size_t smem2 = (size_t)LJ * 4 * H * 2 + (size_t)LB * 4 * H * 2 + (size_t)LB * LJ * 4 +
-                       (size_t)LB * 4 * LJ * 2 + (size_t)2 * 7 * LB * LJ * 4 + (2 * LB + 1) * 4;
+  const size_t smem2 = (size_t)LJ * 4 * H * 2 + (size_t)LB * LJ * 4 + (size_t)LB * 4 * LJ * 2 +
+                       (size_t)2 * 7 * LB * LJ * 4 + (2 * LB + 1) * 4;
   if (kn_lstm_v2.get() && smem2 <= 160 * 1024 && (LB * 4 * H / 8) % LC == 0 && gates.numel() * 4 < (1ll << 31)) {
     static bool attr = false;
     if (!attr) {

@@ -52,7 +52,7 @@ ops.set_knob("lstm_prof", 1)
 for name, fn, phases in (
         ("fwd", lambda: ops.lstm_seq_fwd(gx, whh, ids)[3], ["poll", "gather", "MFMA", "cell", "publish"]),
         ("bwd", lambda: ops.lstm_seq_bwd(dh, g, c, whh, ids)[1],
-         ["cell", "publish", "poll", "gather", "MFMA+reduce+carry"])):
+         ["cell", "publish", "poll", "A loads + MFMA", "reduce+carry"])):
     fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
