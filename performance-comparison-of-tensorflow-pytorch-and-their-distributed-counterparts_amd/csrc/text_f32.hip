@@ -548,10 +548,7 @@ void embedding_bwd(const at::Tensor& ids, const at::Tensor& dy, at::Tensor dW, i
     hipLaunchKernelGGL(embedding_bwd_f32_kernel, dim3(tgrid(rows * E)), dim3(256), 0, cur_stream(),
                        idc.data_ptr<int64_t>(), ptr<float>(dyc), ptr<float>(dW), rows, E, padding_idx);
   } else {   // deterministic segmented reduction (rnn.hip embedding_bwd_seg_kernel)
-    auto sorted = at::sort(idc.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
-    const at::Tensor sid = std::get<0>(sorted).contiguous(), perm = std::get<1>(sorted).contiguous();
-    hipLaunchKernelGGL(embedding_bwd_seg_kernel<float>, dim3(rows), dim3(256), 0, cur_stream(), sid.data_ptr<int64_t>(),
-                       perm.data_ptr<int64_t>(), ptr<float>(dyc), ptr<float>(dW), rows, E, padding_idx);
+    embedding_bwd_det<float>(idc, ptr<float>(dyc), ptr<float>(dW), dW.size(0), E, padding_idx, cur_stream());
   }
   PCMP_LAUNCH_CHECK();
 }

@@ -191,6 +191,24 @@ def test_embedding_bwd_deterministic(gpu, dtype):
         _ops().embedding_bwd(ids, dy, dW, 0, True)
         outs.append(dW)
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    # the fixed order: per id, fp32 adds over its rows in row order, then one add into dW (the
+    # packed-key sort path must reproduce the stable-sort order exactly)
+    dyc, idl = dy.reshape(-1, E).float().cpu(), ids.flatten().tolist()
+    exp = torch.full((V, E), 0.5)
+    for v in sorted(set(idl) - {0}):
+        acc = torch.zeros(E)
+        for r, x in enumerate(idl):
+            if x == v:
+                acc = acc + dyc[r]
+        exp[v] = exp[v] + acc
+    assert torch.equal(outs[0].cpu(), exp)
+    # more rows than the one-workgroup sort takes (16,384): the library stable sort, same bits per run
+    big = torch.randint(1, V, (4, 5000), device=gpu)
+    dyb = torch.randn(4, 5000, E, device=gpu).to(dtype)
+    r1, r2 = torch.zeros(V, E, device=gpu), torch.zeros(V, E, device=gpu)
+    _ops().embedding_bwd(big, dyb, r1, 0, True)
+    _ops().embedding_bwd(big, dyb, r2, 0, True)
+    assert torch.equal(r1, r2)
     keep = (ids.flatten() != 0)
     ref = torch.zeros(V, E, dtype=torch.float64, device=gpu).index_add_(
         0, ids.flatten()[keep], dy.reshape(-1, E)[keep].double()) + 0.5

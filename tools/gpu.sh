@@ -92,6 +92,8 @@ task_prof_bert() {
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bert -o run -- \
     python tools/prof_target.py bert 16 > gpurun_out/prof_bert.log 2>&1 || die prof-bert gpurun_out/prof_bert.log
   python tools/prof_summary.py gpurun_out/prof_bert --top 45 --step-kernel adam_flat --last-steps 4 > ${O}_prof_bert.txt
+  python tools/stream_report.py gpurun_out/prof_bert --steps 4 --step-kernel adam_flat --loss-kernel xent --gaps 30 \
+    > ${O}_bert_streams.txt 2>&1 || true
   find gpurun_out/prof_bert -name "*kernel_trace.csv" -delete
   sed -n '/per step over/,+12p' ${O}_prof_bert.txt
 }
