@@ -3300,31 +3300,48 @@ static GemmPlan plan_gemm(const IgemmParams& p, __bf16* out, const at::TensorOpt
   // runs at process exit, after the HIP runtime may be gone)
   static at::Tensor* flush = nullptr;
   if (cold && flush == nullptr) flush = new at::Tensor(at::empty({64 << 20}, fopts.dtype(at::kByte)));
-  for (const GemmPlan& c : cands) {
-    run_plan<MODE>(p, c, out, fopts, st);   // warm (workspace allocation)
-    float ms = 0.f;
-    if (cold) {
+  auto consider = [&](const GemmPlan& c, float ms) {
+    if (c.nsplit > 1 && !small_m) ms += 3e-3f * kn_plan_split_us.get();   // 3 timed calls
+    if (ms < best_ms) { best_ms = ms; best = c; }
+    if (g_plan_log) g_plan_log->push_back(std::string(plan_kind_name(c.kind)) + "/split" + std::to_string(c.nsplit) +
+                                          " " + std::to_string(ms / 3 * 1000.f) + "us");
+  };
+  if (cold) {
+    // every candidate's three cold calls are enqueued with their own event pairs and the host waits
+    // ONCE per shape (a wait per call cost ~0.2 s of a transfer-learning epoch's first steps)
+    std::vector<hipEvent_t> ev(6 * cands.size());
+    for (auto& e : ev) PCMP_HIP_CHECK(hipEventCreate(&e));
+    for (size_t ci = 0; ci < cands.size(); ++ci) {
+      run_plan<MODE>(p, cands[ci], out, fopts, st);   // warm (workspace allocation)
       for (int r = 0; r < 3; ++r) {
         PCMP_HIP_CHECK(hipMemsetAsync(flush->data_ptr(), r, flush->numel(), st));
-        PCMP_HIP_CHECK(hipEventRecord(e0, st));
-        run_plan<MODE>(p, c, out, fopts, st);
-        PCMP_HIP_CHECK(hipEventRecord(e1, st));
-        PCMP_HIP_CHECK(hipEventSynchronize(e1));
+        PCMP_HIP_CHECK(hipEventRecord(ev[6 * ci + 2 * r], st));
+        run_plan<MODE>(p, cands[ci], out, fopts, st);
+        PCMP_HIP_CHECK(hipEventRecord(ev[6 * ci + 2 * r + 1], st));
+      }
+    }
+    PCMP_HIP_CHECK(hipEventSynchronize(ev.back()));
+    for (size_t ci = 0; ci < cands.size(); ++ci) {
+      float ms = 0.f;
+      for (int r = 0; r < 3; ++r) {
         float one = 0.f;
-        PCMP_HIP_CHECK(hipEventElapsedTime(&one, e0, e1));
+        PCMP_HIP_CHECK(hipEventElapsedTime(&one, ev[6 * ci + 2 * r], ev[6 * ci + 2 * r + 1]));
         ms += one;
       }
-    } else {
+      consider(cands[ci], ms);
+    }
+    for (auto& e : ev) PCMP_HIP_CHECK(hipEventDestroy(e));
+  } else {
+    for (const GemmPlan& c : cands) {
+      run_plan<MODE>(p, c, out, fopts, st);   // warm (workspace allocation)
+      float ms = 0.f;
       PCMP_HIP_CHECK(hipEventRecord(e0, st));
       for (int r = 0; r < 3; ++r) run_plan<MODE>(p, c, out, fopts, st);
       PCMP_HIP_CHECK(hipEventRecord(e1, st));
       PCMP_HIP_CHECK(hipEventSynchronize(e1));
       PCMP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      consider(c, ms);
     }
-    if (c.nsplit > 1 && !small_m) ms += 3e-3f * kn_plan_split_us.get();   // 3 timed calls
-    if (ms < best_ms) { best_ms = ms; best = c; }
-    if (g_plan_log) g_plan_log->push_back(std::string(plan_kind_name(c.kind)) + "/split" + std::to_string(c.nsplit) +
-                                          " " + std::to_string(ms / 3 * 1000.f) + "us");
   }
   PCMP_HIP_CHECK(hipEventDestroy(e0));
   PCMP_HIP_CHECK(hipEventDestroy(e1));
