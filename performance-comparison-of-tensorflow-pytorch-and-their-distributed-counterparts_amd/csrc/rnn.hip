@@ -301,7 +301,7 @@ struct LstmBwdParams {
   const int64_t* ids;
   const __bf16* dhout;   // [B][S][2H] bf16 gradient w.r.t. layer output
   __bf16* dgates;        // [B][S][2][4H] bf16 gradient w.r.t. gate pre-activations
-  __bf16* dgbuf;         // [2][2][LB][4H] bf16 ping-pong dgates exchange
+  __bf16* dgbuf;         // [2][2][LB][4H] bf16 ping-pong dgates exchange (v3: fp32 partials [2][2][nub][H][LB])
   unsigned* counters;
   unsigned* err;
   int B, S, H;
@@ -929,7 +929,216 @@ __global__ void __launch_bounds__(LT2) lstm_bwd_persistent2(const LstmBwdParams 
   clk.flush(p.prof, 5);
 }
 
-inline Knob kn_lstm_v2("lstm_v2", 1);
+// Backward, partial-sum exchange (knob lstm_v2 = 2): instead of handing the 64 KB dgates_t tile of
+// the direction to every workgroup (each then multiplies it by its own 16 columns of W_hh), each
+// workgroup multiplies ITS dgates slice [LB][4*LJ] by its 4*LJ rows of W_hh -- a partial dh_rec over
+// all H units -- and publishes that (fp32 [H][LB], 32 KB); each workgroup then sums, for its LJ units,
+// the nub partials in source order (32 KB gathered as 4-B sc1 loads).  The partial product needs no
+// exchange, so the hand-off carries a product instead of an operand and the MFMA leaves the
+// critical path's gather.  Same math in another summation order: equal to the other forms to fp32
+// reassociation (tests/test_text_kernels_gpu.py::test_lstm_bwd_partial_exchange).  dgbuf holds the
+// fp32 partials here: [2 slots][2 dirs][nub sources][H][LB].
+__global__ void __launch_bounds__(LT2) lstm_bwd_persistent3(const LstmBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = p.H, nub = H / LJ, G4 = 4 * H, NCD = G4 / 8;
+  const int dir = blockIdx.x / nub, ub = blockIdx.x % nub, j0 = ub * LJ;
+  __bf16* sWr = reinterpret_cast<__bf16*>(smem);               // [H][4LJ] this slice's W_hh rows, j-major (swizzled)
+  float* sR = reinterpret_cast<float*>(sWr + H * 4 * LJ);       // [LB][LJ] dh_rec
+  __bf16* sDo = reinterpret_cast<__bf16*>(sR + LB * LJ);       // [LB][4][LJ] this slice's dgates_t
+  float* sF = reinterpret_cast<float*>(sDo + LB * 4 * LJ);      // [2][7][LB][LJ] per-step inputs
+  int* sV = reinterpret_cast<int*>(sF + 2 * 7 * LB * LJ);       // [2][LB] valid flags; [2*LB] abort
+  const __amdgpu_buffer_rsrc_t rsP = rnn_rsrc(p.dgbuf, (unsigned)((size_t)4 * nub * H * LB * 4));
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, it = tid - LC;
+  const bool io = tid >= LC;
+  // sWr[j][r] = W_hh[dir][gate*H + j0 + jj][j], r = gate*LJ + jj: 8 chunks of 16 B per j row
+  for (int i = tid; i < H * 4 * LJ; i += LT2) {
+    const int r = i / H, j = i % H, gate = r / LJ, jj = r % LJ;
+    reinterpret_cast<unsigned short*>(sWr)[swz(j, r >> 3, 8) * 8 + (r & 7)] =
+        reinterpret_cast<const unsigned short*>(p.whh)[((size_t)dir * G4 + gate * H + j0 + jj) * H + j];
+  }
+  if (tid == 0) sV[2 * LB] = 0;
+  unsigned* cnt = p.counters + dir;
+  // IO threads: per-step inputs as 16-B items, each load instruction from ONE source (uniform buffer
+  // resource, out-of-bounds zeros for masked lanes): gates 512 items (2 per thread: b, gate, quarter),
+  // c_t 128 (threads 0-127) or c_prev 128 (threads 128-255), dh_out 64 (threads 0-63), ids 32
+  const __amdgpu_buffer_rsrc_t rsG = rnn_rsrc(p.gates, (unsigned)((size_t)p.B * p.S * 2 * G4 * 4));
+  const __amdgpu_buffer_rsrc_t rsC = rnn_rsrc(p.cst, (unsigned)((size_t)p.B * p.S * 2 * H * 4));
+  const __amdgpu_buffer_rsrc_t rsDh = rnn_rsrc(p.dhout, (unsigned)((size_t)p.B * p.S * 2 * H * 2));
+  const __amdgpu_buffer_rsrc_t rsId = rnn_rsrc(p.ids, (unsigned)((size_t)p.B * p.S * 8));
+  uint4 fv[4];
+  long long fid = 0;
+  auto io_fetch = [&](int stp) {
+    const int tt = dir == 0 ? p.S - 1 - stp : stp;
+    const int tp = dir == 0 ? tt - 1 : tt + 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {   // gates
+      const int i = it + 256 * k, b = i >> 4, g = (i >> 2) & 3, q = i & 3;
+      fv[k] = io_ld16(rsG, b < p.B ? (unsigned)(((((unsigned)b * p.S + tt) * 2 + dir) * G4 + g * H + j0 + q * 4) * 4)
+                                   : kIoOOB);
+    }
+    {   // c_t (threads 0-127) / c_prev (threads 128-255)
+      const int i = it & 127, b = i >> 2, q = i & 3, ts = it < 128 ? tt : tp;
+      const bool ok = b < p.B && ts >= 0 && ts < p.S;
+      fv[2] = io_ld16(rsC, ok ? (unsigned)(((((unsigned)b * p.S + ts) * 2 + dir) * H + j0 + q * 4) * 4) : kIoOOB);
+    }
+    {   // dh_out (threads 0-63)
+      const int b = it >> 1, half = it & 1;
+      fv[3] = io_ld16(rsDh, (it < 64 && b < p.B)
+                                ? (unsigned)((((unsigned)b * p.S + tt) * 2 * H + dir * H + j0 + half * 8) * 2) : kIoOOB);
+    }
+    fid = io_ld8(rsId, (it < LB && it < p.B) ? (unsigned)((it * p.S + tt) * 8) : kIoOOB);
+  };
+  auto io_commit = [&](int slot) {   // F rows: 0 dh_out, 1-4 gates i,f,g,o, 5 c_t, 6 c_prev
+    float* F = sF + slot * 7 * LB * LJ;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = it + 256 * k, b = i >> 4, g = (i >> 2) & 3, q = i & 3;
+      *reinterpret_cast<uint4*>(F + (1 + g) * LB * LJ + b * LJ + q * 4) = fv[k];
+    }
+    {
+      const int i = it & 127, b = i >> 2, q = i & 3;
+      *reinterpret_cast<uint4*>(F + (it < 128 ? 5 : 6) * LB * LJ + b * LJ + q * 4) = fv[2];
+    }
+    if (it < 64) {
+      const int b = it >> 1, half = it & 1;
+      const unsigned short* u = reinterpret_cast<const unsigned short*>(&fv[3]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) F[b * LJ + half * 8 + e] = bf2f(u[e]);
+    }
+    if (it < LB) sV[slot * LB + it] = fid > 0 ? 1 : 0;
+  };
+  // IO threads: this step's dgates [b][gate][16 units] bf16 = 2 x 16 B per (b, gate)
+  auto io_store = [&](int t) {
+    const int b = it >> 3, g = (it >> 1) & 3, half = it & 1;
+    if (b < p.B)
+      *reinterpret_cast<uint4*>(p.dgates + (((size_t)b * p.S + t) * 2 + dir) * G4 + g * H + j0 + half * 8) =
+          *reinterpret_cast<const uint4*>(sDo + (b * 4 + g) * LJ + half * 8);
+  };
+  if (io) {
+    io_fetch(0);
+    io_commit(0);
+    if (p.S > 1) io_fetch(1);
+  }
+  float dcreg = 0.f, dhcarry = 0.f;   // the thread's (b, unit) pair
+  PhaseClock clk{p.prof != nullptr && blockIdx.x == 0 && tid == 0};   // cell, MFMA+publish, poll, gather, carry
+  lds_barrier();
+  for (int step = 0; step < p.S; ++step) {
+    const int t = dir == 0 ? p.S - 1 - step : step;
+    const int cur = step & 1;
+    clk.mark(-1);
+    // ---- C: cell backward (round-1 math), one (b, jj) pair per thread, dgates slice to LDS
+    {
+      const float* F = sF + cur * 7 * LB * LJ;
+      const int b = tid / LJ, jj = tid % LJ;
+      float dgi = 0.f, dgf = 0.f, dgg = 0.f, dgo = 0.f;
+      if (b < p.B) {
+        const int o = b * LJ + jj;
+        const float dh = F[o] + dhcarry;
+        if (sV[cur * LB + b]) {
+          const float ig = F[LB * LJ + o], fg = F[2 * LB * LJ + o], gg = F[3 * LB * LJ + o], og = F[4 * LB * LJ + o];
+          const float c = F[5 * LB * LJ + o];
+          const float cprev = F[6 * LB * LJ + o];
+          const float tc = tanh_f(c);
+          const float dc = dcreg + dh * og * (1.f - tc * tc);
+          dgo = dh * tc * og * (1.f - og);
+          dgi = dc * gg * ig * (1.f - ig);
+          dgg = dc * ig * (1.f - gg * gg);
+          dgf = dc * cprev * fg * (1.f - fg);
+          dcreg = dc * fg;
+          dhcarry = 0.f;
+        } else {
+          dhcarry = dh;
+        }
+      }
+      unsigned short* d16 = reinterpret_cast<unsigned short*>(sDo) + b * 4 * LJ + jj;
+      d16[0] = f2bf(dgi);
+      d16[LJ] = f2bf(dgf);
+      d16[2 * LJ] = f2bf(dgg);
+      d16[3 * LJ] = f2bf(dgo);
+      clk.mark(0);
+    }
+    lds_barrier();
+    // ---- D: the IO waves store dgates_t; then every wave multiplies the slice by this workgroup's
+    //      W_hh rows (partial dh_rec for all H units: [LB] x [4LJ] x [H]) and publishes it (sc1)
+    if (io) io_store(t);
+    if (step + 1 < p.S) {   // all 8 waves: 2 m-tiles x H/16 n-tiles
+      const int mt = wid & 1;
+      const bf16x8* sD8 = reinterpret_cast<const bf16x8*>(sDo);
+      const bf16x8* sW8 = reinterpret_cast<const bf16x8*>(sWr);
+      bf16x8 a[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a[ks] = sD8[(mt * 16 + (lane & 15)) * 8 + ks * 4 + (lane >> 4)];
+      const unsigned pbase = (unsigned)(((cur * 2 + dir) * nub + ub) * H * LB) * 4u;
+      for (int nt = wid >> 1; nt < H / 16; nt += LT2 / 128) {
+        const int j = nt * 16 + (lane & 15);
+        f32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], sW8[swz(j, ks * 4 + (lane >> 4), 8)], acc, 0, 0, 0);
+        const int b0 = mt * 16 + (lane >> 4) * 4;   // 4 consecutive b of column j: one 16-B store
+        st16_sc1(rsP, pbase + (unsigned)(j * LB + b0) * 4u, __builtin_bit_cast(uint4, acc));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its partial stores
+      clk.mark(1);
+    }
+    if (step + 1 == p.S) break;
+    lds_barrier();   // every wave's partial stores drained
+    if (tid == 0) __hip_atomic_fetch_add((gu32*)cnt, 1u, RLX_AGENT);
+    // ---- A: wave 0 waits for every workgroup's partial
+    if (wid == 0) {
+      if (!exch_wait(cnt, (unsigned)(step + 1) * nub, p.err) && lane == 0) sV[2 * LB] = 1;
+      clk.mark(2);
+    }
+    lds_barrier();
+    if (sV[2 * LB]) return;
+    if (io) {
+      io_commit(cur ^ 1);   // the next step's inputs, loaded beside the previous MFMA phase
+      if (step + 2 < p.S) io_fetch(step + 2);   // beside this MFMA phase, committed next step
+    }
+    // ---- B: dh_rec[b][jj] = sum over the nub sources (in source order) of their partials: the compute
+    //      threads take 2 (b, jj) pairs each (b fastest: a wave reads 256 contiguous bytes per source),
+    //      16 sources' loads in flight per pair, branch-free (sources past nub read out of bounds: 0)
+    if (!io) {
+      const unsigned sbase = (unsigned)((cur * 2 + dir) * nub * H * LB) * 4u, sstride = (unsigned)(H * LB) * 4u;
+      unsigned o[2];
+      float acc[2] = {0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int q = tid + LC * k;
+        o[k] = sbase + (unsigned)((j0 + q / LB) * LB + (q & (LB - 1))) * 4u;
+      }
+      for (int u0 = 0; u0 < nub; u0 += 16) {
+        float v[2][16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+            v[k][u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rsP, (int)(u0 + u < nub ? o[k] + (unsigned)(u0 + u) * sstride : kIoOOB), 0, 16));   // aux 16 = sc1
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) acc[k] += v[k][u];
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int q = tid + LC * k;
+        sR[(q & (LB - 1)) * LJ + q / LB] = acc[k];
+      }
+      clk.mark(3);
+    }
+    lds_barrier();
+    {
+      const int b = tid / LJ, jj = tid % LJ;
+      if (b < p.B) dhcarry += sR[b * LJ + jj];
+      clk.mark(4);
+    }
+  }
+  clk.flush(p.prof, 5);
+}
+
+
+inline Knob kn_lstm_v2("lstm_v2", 2);   // 0: round-1 kernels, 1: role-split v2, 2 (default): v2 forward + partial-exchange backward
 inline Knob kn_lstm_prof("lstm_prof", 0);   // phase clocks of the v2 recurrences into sync[4:20] (tools/lstm_micro.py)
 
 // ------------------------------------------------------------------------------- host
@@ -1061,6 +1270,19 @@ std::vector<at::Tensor> lstm_seq_bwd(const at::Tensor& dhout, const at::Tensor& 
                   prof ? reinterpret_cast<unsigned long long*>(reinterpret_cast<int*>(sync.data_ptr()) + 4) : nullptr};
   const size_t smem2 = (size_t)LJ * 4 * H * 2 + (size_t)LB * LJ * 4 + (size_t)LB * 4 * LJ * 2 +
                        (size_t)2 * 7 * LB * LJ * 4 + (2 * LB + 1) * 4;
+  if (kn_lstm_v2.get() == 2 && smem2 <= 160 * 1024 && gates.numel() * 4 < (1ll << 31)) {
+    static bool attr3 = false;
+    if (!attr3) {
+      PCMP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_bwd_persistent3),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr3 = true;
+    }
+    auto pbuf = at::empty({2, 2, H / LJ, H, LB}, gates.options());   // fp32 partial-sum exchange
+    p.dgbuf = reinterpret_cast<__bf16*>(pbuf.data_ptr<float>());
+    hipLaunchKernelGGL(lstm_bwd_persistent3, dim3(2 * (H / LJ)), dim3(LT2), smem2, cur_stream(), p);
+    PCMP_LAUNCH_CHECK();
+    return {dgates, sync};
+  }
   if (kn_lstm_v2.get() && smem2 <= 160 * 1024 && (LB * 4 * H / 8) % LC == 0 && gates.numel() * 4 < (1ll << 31)) {
     static bool attr = false;
     if (!attr) {

@@ -89,6 +89,32 @@ def test_lstm_v2_bitwise(gpu, B, S, H):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,S,H", [(5, 40, 64), (32, 128, 256), (17, 33, 32), (8, 16, 512)])
+def test_lstm_bwd_partial_exchange(gpu, B, S, H):
+    """lstm_v2 = 2: the backward hands off fp32 partial products instead of the dgates tile -- same
+    math, another fp32 summation order, so equal to the v2 kernel's dgates to bf16 rounding."""
+    torch.manual_seed(2)
+    ids = _ids(B, S, 1000, gpu)
+    gx = (torch.randn(B, S, 2, 4 * H, device=gpu) * 0.5).to(torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, device=gpu) / H ** 0.5).to(torch.bfloat16)
+    dh = torch.randn(B, S, 2 * H, device=gpu).to(torch.bfloat16)
+    old = ops().set_knob("lstm_v2", 1)
+    try:
+        h, g, c, sync = ops().lstm_seq_fwd(gx, whh, ids)
+        dg1, s1 = ops().lstm_seq_bwd(dh, g, c, whh, ids)
+        ops().set_knob("lstm_v2", 2)
+        dg3, s3 = ops().lstm_seq_bwd(dh, g, c, whh, ids)
+        dg3b, _ = ops().lstm_seq_bwd(dh, g, c, whh, ids)
+        torch.cuda.synchronize()
+    finally:
+        ops().set_knob("lstm_v2", old)
+    assert int(s1[2].item()) == 0 and int(s3[2].item()) == 0, "barrier timeout"
+    assert torch.equal(dg3, dg3b), "partial exchange must be run-to-run deterministic"
+    close(dg3, dg1, 5e-2, 5e-2)
+    rel = (dg3.float() - dg1.float()).norm() / dg1.float().norm()
+    assert rel < 1e-2, rel
+
+
 def test_layernorm_act(gpu):
     x = torch.randn(300, 768, device=gpu).to(torch.bfloat16)
     r = torch.randn(300, 768, device=gpu).to(torch.bfloat16)

@@ -39,7 +39,7 @@ def timeit(fn, n=20):
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 h, g, c, _ = ops.lstm_seq_fwd(gx, whh, ids)
 for r in range(rounds):
-    for v in (0, 1):
+    for v in (0, 1, 2):   # 2: v2 forward + partial-exchange backward
         ops.set_knob("lstm_v2", v)
         tf = timeit(lambda: ops.lstm_seq_fwd(gx, whh, ids))
         tb = timeit(lambda: ops.lstm_seq_bwd(dh, g, c, whh, ids))
@@ -47,12 +47,14 @@ for r in range(rounds):
               flush=True)
 
 # phase clocks of workgroup 0 (knob lstm_prof): fraction of the step per phase
-ops.set_knob("lstm_v2", 1)
 ops.set_knob("lstm_prof", 1)
-for name, fn, phases in (
-        ("fwd", lambda: ops.lstm_seq_fwd(gx, whh, ids)[3], ["poll", "gather", "MFMA", "cell", "publish"]),
-        ("bwd", lambda: ops.lstm_seq_bwd(dh, g, c, whh, ids)[1],
-         ["cell", "publish", "poll", "A loads + MFMA", "reduce+carry"])):
+for v, name, fn, phases in (
+        (1, "fwd", lambda: ops.lstm_seq_fwd(gx, whh, ids)[3], ["poll", "gather", "MFMA", "cell", "publish"]),
+        (1, "bwd", lambda: ops.lstm_seq_bwd(dh, g, c, whh, ids)[1],
+         ["cell", "publish", "poll", "A loads + MFMA", "reduce+carry"]),
+        (2, "bwd v3", lambda: ops.lstm_seq_bwd(dh, g, c, whh, ids)[1],
+         ["cell", "MFMA + publish", "poll", "partials gather", "carry"])):
+    ops.set_knob("lstm_v2", v)
     fn()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -66,3 +68,4 @@ for name, fn, phases in (
     print(f"{name}: {us:.1f} us, {tot / S:.0f} clocks/step over the phases; per step: " +
           ", ".join(f"{n} {v / tot * us / S:.2f} us" for n, v in zip(phases, cyc)), flush=True)
 ops.set_knob("lstm_prof", 0)
+ops.set_knob("lstm_v2", 1)
