@@ -683,8 +683,9 @@ static Knob kn_f32_wgrad_blocks("f32_wgrad_blocks", 2048);
 static Knob kn_f32_wgrad_blocks_1x1("f32_wgrad_blocks_1x1", 512);   // 1x1: 2048 ran 5-30 % slower
 // FWD / DGRAD grids at or above f32_blocks: split up to f32_qsplit ways when that lifts the wave
 // quantisation efficiency (blocks / whole CU waves) by >= f32_qgain percent (0 / 1: off)
-static Knob kn_f32_qsplit("f32_qsplit", 0);
+static Knob kn_f32_qsplit("f32_qsplit", 5);   // TL forward 8.42 -> 8.20 ms (profiles/r6_f32_qsplit_tl_ab.txt)
 static Knob kn_f32_qgain("f32_qgain", 10);
+static Knob kn_f32_qsplit_mink("f32_qsplit_mink", 64);   // short reductions lost (l1 3x3, l2 1x1)
 
 struct F32Plan {
   bool big;
@@ -717,7 +718,7 @@ static F32Plan plan_f32(ConvP& p) {
   else if (kn_f32_split.get() && tiles() < target)
     ns = (int)std::max<int64_t>(
         1, std::min<int64_t>(ceil_div(target, tiles()), nk / std::max(1, kn_f32_split_steps.get())));
-  else if (pl.big && kn_f32_qsplit.get() > 1) {
+  else if (pl.big && kn_f32_qsplit.get() > 1 && nk >= kn_f32_qsplit_mink.get()) {
     // wave quantisation: 392 tiles (every B=64 ResNet-50 layer has 392 or 784) load the CUs 2:1;
     // a split whose block count fills whole waves of CUs evens that out, if it gains enough
     auto eff = [&](int s) {

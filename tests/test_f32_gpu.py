@@ -40,6 +40,8 @@ F32_KNOBS = {
     "big_nosplit": {"f32_blocks": 1},             # largest 32x32x2 tiles, no split
     "max_split": {"f32_blocks": 1 << 20},         # 64x64 32x32x2 tiles, split-K down to 8 K-steps
     "small_split": {"f32_big": 0, "f32_blocks": 1 << 20},
+    # wave-quantisation split on grids at or above the CU target (3 "CUs" so the small shapes split)
+    "qsplit": {"f32_blocks": 3, "f32_qsplit_mink": 1, "f32_qgain": 0},
 }
 
 
@@ -47,7 +49,7 @@ F32_KNOBS = {
 def f32_kernel(request):
     """Every launch plan of the fp32 conv GEMMs (csrc/f32.hip plan_f32): the default, the 64x64
     16x16x4 kernel, the 32x32x2 kernel without split and with the deepest split-K (partials + the
-    split epilogue), on the same shapes."""
+    split epilogue) and the wave-quantisation split, on the same shapes."""
     ops = _ops()
     olds = {k: ops.set_knob(k, v) for k, v in F32_KNOBS[request.param].items()}
     yield request.param
