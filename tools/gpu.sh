@@ -14,6 +14,7 @@
 #   knob-ab      per-shape in-process knob A/B (tools/gemm_knob_ab.py): KVARIANTS='a:k=v;b:k=v' MODES
 #   prof-bench   rocprofv3 kernel stats + per-step table of the ResNet-50 bench step
 #   prof-bert    rocprofv3 kernel stats + per-step table of the BERT-base step
+#   prof-r18     rocprofv3 kernel stats + stream report of the ResNet-18 B=256 training step
 #   prof-bilstm  rocprofv3 kernel stats + per-step table of the BiLSTM step (B=32, S=128)
 #   prof-infer   rocprofv3 trace of the batch-1 hipGraph inference loop: kernels / span per image
 #   tail         end-of-backward tail report (tools/tail_report.py)
@@ -55,7 +56,7 @@ task_bench_ab() {
     for v in "${VS[@]}"; do
       local name=${v%%=*} knobs=${v#*=}
       local line
-      line=$(PCMP_KNOBS="$knobs" timeout -k 10 240 python -u bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-8} \
+      line=$(PCMP_KNOBS="$knobs" timeout -k 10 240 python -u bench.py ${BENCH_ARGS:-} --steps ${STEPS:-20} --warmup ${WARMUP:-8} \
              --infer-images ${INFER:-0} 2>/dev/null | tail -1) || die "bench-ab $name"
       echo "$name round$r $line" | tee -a $out | cut -c1-200
     done
@@ -68,7 +69,7 @@ task_env_ab() {
     for v in "${VS[@]}"; do
       local name=${v%%:*} envs=${v#*:}
       local line
-      line=$(env $envs timeout -k 10 240 python -u bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-8} \
+      line=$(env $envs timeout -k 10 240 python -u bench.py ${BENCH_ARGS:-} --steps ${STEPS:-20} --warmup ${WARMUP:-8} \
              --infer-images ${INFER:-0} 2>/dev/null | tail -1) || die "env-ab $name"
       echo "$name round$r $line" | tee -a $out | cut -c1-200
     done
@@ -103,6 +104,15 @@ task_prof_bilstm() {
   python tools/prof_summary.py gpurun_out/prof_bilstm --top 30 --step-kernel adam_flat --last-steps 4 > ${O}_prof_bilstm.txt
   find gpurun_out/prof_bilstm -name "*kernel_trace.csv" -delete
   sed -n '/per step over/,+12p' ${O}_prof_bilstm.txt
+}
+task_prof_r18() {   # ResNet-18 B=256 training step (BASELINE.json config 2): kernel stats + stream report
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r18 -o run -- \
+    python tools/prof_target.py resnet18 12 > gpurun_out/prof_r18.log 2>&1 || die prof-r18 gpurun_out/prof_r18.log
+  python tools/prof_summary.py gpurun_out/prof_r18 --top 40 --last-steps 4 > ${O}_prof_r18.txt
+  python tools/stream_report.py gpurun_out/prof_r18 --steps 4 > ${O}_r18_streams.txt 2>&1 || true
+  find gpurun_out/prof_r18 -name "*kernel_trace.csv" -delete
+  head -8 ${O}_r18_streams.txt
+  sed -n '/per step over/,+30p' ${O}_prof_r18.txt
 }
 task_prof_f32() {   # fp32 transfer-learning forward (B=64): kernel stats over 10 forwards
   cd /tmp
