@@ -2765,11 +2765,15 @@ static void wgrad_tile(const IgemmParams& p, int& BM, int& BN) {
 
 // FWD/DGRAD grids of fewer 128x128 tiles than CUs (BERT-base's M=4096 token GEMMs with N=768:
 // 192 tiles) run 64x128 tiles instead: twice the workgroups, every CU busy.  Knob bm64_smallgrid =
-// 0 disables it (A/B runs).
+// 0 disables it (A/B runs).  FWD convs with BN statistics keep the LDS-DMA tiles (bm64_smallgrid = 1):
+// the ResNet-50 transfer-learning step at B=64 (layer-3/4 convs: 100-196 tiles) ran 2.41 -> 2.38
+// ms/step without the 64x128 register-staged form (profiles/r6_tl_bm64_ab.txt, r6_tl_bm64_ab2.txt); 2 = every GEMM.
 inline Knob kn_bm64_smallgrid("bm64_smallgrid", 1);
 static bool use_bm64_smallgrid(int mode, const IgemmParams& p) {
   if (!(mode != MODE_WGRAD && p.nsplit == 1 && p.gm > 64 && p.gn > 64)) return false;
-  return kn_bm64_smallgrid.get() && ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
+  const int k = kn_bm64_smallgrid.get();
+  if (k == 0 || (k == 1 && mode == MODE_FWD && p.stats)) return false;   // (conv_fwd sets p.stats before igemm_bm)
+  return ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256;
 }
 
 // BM of the kernel dispatch<> will pick (per-tile partial statistics are allocated per BM row tile)

@@ -66,6 +66,9 @@ static std::vector<at::Tensor> conv_fwd_impl(const at::Tensor& x, const at::Tens
       launch_fwd_stream(p, st);
       return {y, stats};
     }
+    // igemm_bm before the buffer exists: the tile choice depends on the statistics epilogue
+    // (use_bm64_smallgrid), so p.stats holds a placeholder until the buffer is allocated
+    p.stats = reinterpret_cast<float*>(uintptr_t(16));
     p.stats_cap = ceil_div(p.gm, igemm_bm(MODE_FWD, p));
     stats = at::empty({p.stats_cap, 2, K}, x.options().dtype(at::kFloat));
     p.stats = ptr<float>(stats);
