@@ -2600,6 +2600,9 @@ inline Knob kn_dma4_n64("dma4_n64", 1);
 static int dma4_mode() { return kn_dma4.get(); }
 static int dma4_n64() { return kn_dma4_n64.get(); }
 // 0: register-staged kernel; 1: 128x128; 2: 128x64; 3: 256x64
+// FWD grids with fewer 128x128 tiles than CUs (the B=64 transfer-learning step's layer-3/4 convs:
+// 100-196 tiles) take 128x64 tiles: twice the workgroups (dma4_small_n64 = 0: 128x128)
+inline Knob kn_dma4_small_n64("dma4_small_n64", 1);   // TL step 2.43 -> 2.38 ms (profiles/r6_tl_small_n64_ab.txt)
 static int use_dma4(int mode, const IgemmParams& p) {
   if (!dma4_mode() || mode == MODE_WGRAD || p.nsplit != 1) return 0;
   const int cin = mode == MODE_FWD ? p.C : p.K;
@@ -2608,6 +2611,7 @@ static int use_dma4(int mode, const IgemmParams& p) {
     const int v = dma4_n64();
     return v == 1 ? 2 : (v == 2 ? 3 : 0);
   }
+  if (mode == MODE_FWD && kn_dma4_small_n64.get() && ceil_div(p.gm, 128) * ceil_div(p.gn, 128) < 256) return 2;
   return 1;
 }
 

@@ -89,6 +89,34 @@ def test_dma32_fwd(gpu, shape):
     assert torch.equal(y2, y3)
 
 
+@pytest.mark.parametrize("shape", [
+    (16, 14, 14, 256, 256, 3, 1, 1),    # layer-3 3x3 at B=16: 25 x 2 tiles of 128x128
+    (64, 7, 7, 512, 512, 3, 1, 1),      # layer-4 3x3 at B=64: 25 x 4 tiles
+    (9, 14, 14, 1024, 192, 1, 1, 0),    # 1x1, M tail, half-empty last 64-column tile
+])
+def test_small_grid_fwd_128x64(gpu, shape):
+    """dma4_small_n64: FWD grids of fewer 128x128 tiles than CUs on 128x64 LDS-DMA tiles (every
+    N tile writes its own columns of the per-M-tile BN partial rows) against fp32 PyTorch and the
+    128x128 tiles."""
+    torch.manual_seed(2)
+    N, H, W, C, K, R, s, p = shape
+    ops = _ops()
+    x = rnd(N, H, W, C, dev=gpu)
+    w = rnd(K, R, R, C, dev=gpu, scale=(2.0 / (R * R * C)) ** 0.5)
+    old = ops.set_knob("dma4_small_n64", 1)
+    try:
+        y, st = ops.conv_fwd(x, w, s, p, None, None, False, True)
+        ops.set_knob("dma4_small_n64", 0)
+        yo, sto = ops.conv_fwd(x, w, s, p, None, None, False, True)
+    finally:
+        ops.set_knob("dma4_small_n64", old)
+    yr, str_ = ref.conv_fwd(x, w, s, p, None, None, False, True)
+    close_el(y, yr)
+    close_el(y, yo)
+    close_sum(st, str_)
+    close_sum(st, sto, rtol=2e-3, atol=5e-1)
+
+
 @pytest.mark.parametrize("shape", SHAPES)
 def test_dma32_dgrad(gpu, shape):
     torch.manual_seed(2)
